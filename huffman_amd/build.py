@@ -1,0 +1,71 @@
+"""Build the gfx950 library and CLIs in-tree with hipcc (no JIT, no cache).
+
+Outputs (git-ignored, shipped to the GPU box with the tree):
+  huffman_amd/lib/libhuffman_amd.so   C ABI of include/huffman_amd.h
+  huffman_amd/bin/archive             drop-in for the reference `archive`
+  huffman_amd/bin/extract             drop-in for the reference `extract`
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OBJ = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "lib", "libhuffman_amd.so")
+BIN = os.path.join(PKG, "bin")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+LIB_SOURCES = ["hz_kernels.hip", "hz_codebook.cpp", "hz_host.cpp"]
+HEADERS = [os.path.join(CSRC, "hz_internal.h"), os.path.join(INCLUDE, "huffman_amd.h")]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}",
+          f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build failed: {' '.join(cmd[:3])} ...")
+    elif verbose and (r.stdout or r.stderr):
+        sys.stderr.write(r.stdout + r.stderr)
+
+
+def build(verbose=False, force=False):
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    os.makedirs(BIN, exist_ok=True)
+    objs = []
+    for src in LIB_SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ, src + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [path] + HEADERS):
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            _run([HIPCC] + CFLAGS + lang + ["-c", path, "-o", obj], verbose)
+    if force or _stale(LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs, verbose)
+    for name in ("archive", "extract"):
+        src = os.path.join(CSRC, f"cli_{name}.cpp")
+        out = os.path.join(BIN, name)
+        if force or _stale(out, [src, LIB] + HEADERS):
+            _run([HIPCC] + CFLAGS + [src, "-o", out, f"-L{os.path.dirname(LIB)}", "-lhuffman_amd",
+                                     "-Wl,-rpath,$ORIGIN/../lib"], verbose)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose="-v" in sys.argv, force="-f" in sys.argv)
+    print(LIB)

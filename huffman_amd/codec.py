@@ -1,0 +1,167 @@
+"""Host-side mirror of the reference's interface for the Huffman path.
+
+The reference exposes two executables:
+  archive <file>             -> <file>.compressed          (Compressor.cu:315-632)
+  extract <file.compressed>  -> ./DECOMPRESSED_FILE[(k)]   (Decompressor.cu:47-114)
+`archive()` / `extract()` here are those entry points (same outputs, same
+file names); `encode()` / `decode()` are their in-memory forms; `Device`
+exposes the stages on device pointers (calculateFrequency -> hist16,
+gpuCodebookConstruction -> build_codebook, populateCWLength + scan +
+encodeFromCW -> pack, translateFile -> decode). Every call goes to the gfx950
+kernels of libhuffman_amd.so.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import Codebook, HeaderInfo, check, load
+
+HZ_NSYM = _lib.HZ_NSYM
+
+
+def _buf(data):
+    arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    arr = np.ascontiguousarray(arr, dtype=np.uint8)
+    return arr, arr.ctypes.data_as(ctypes.c_void_p)
+
+
+def encode(data):
+    """Bytes -> complete .compressed image (what `archive` writes)."""
+    lib = load()
+    arr, p = _buf(data)
+    n = arr.size
+    need = ctypes.c_uint64()
+    check(lib.hz_encoded_size(p, n, ctypes.byref(need)), "hz_encoded_size")
+    out = np.empty(max(need.value, 1), dtype=np.uint8)
+    got = ctypes.c_uint64()
+    check(lib.hz_encode_host(p, n, out.ctypes.data_as(ctypes.c_void_p), out.size, ctypes.byref(got)),
+          "hz_encode_host")
+    return out[:got.value].tobytes()
+
+
+def decode(blob):
+    """.compressed image -> original bytes (what `extract` writes)."""
+    lib = load()
+    arr, p = _buf(blob)
+    cb, info = parse_header(arr)
+    n_out = 2 * (info.n // 2) + (1 if info.is_odd else 0)
+    out = np.empty(max(n_out, 1), dtype=np.uint8)
+    got = ctypes.c_uint64()
+    check(lib.hz_decode_host(p, arr.size, out.ctypes.data_as(ctypes.c_void_p), out.size, ctypes.byref(got)),
+          "hz_decode_host")
+    return out[:got.value].tobytes()
+
+
+def archive(path, verbose=True):
+    """`archive <path>`: writes <path>.compressed; returns its name."""
+    check(load().hz_archive_file(str(path).encode(), int(verbose)), "hz_archive_file")
+    return str(path) + ".compressed"
+
+
+def extract(path, verbose=True):
+    """`extract <path>`: writes ./DECOMPRESSED_FILE (or (k)); returns its name."""
+    name = ctypes.create_string_buffer(256)
+    check(load().hz_extract_file(str(path).encode(), name, 256, int(verbose)), "hz_extract_file")
+    return name.value.decode()
+
+
+def build_codebook(hist):
+    """65 536-entry host histogram -> Codebook with the reference's semantics."""
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    assert h.size == HZ_NSYM
+    cb = Codebook()
+    check(load().hz_codebook_build(h.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cb)), "hz_codebook_build")
+    return cb
+
+
+def codebook_arrays(cb):
+    """(order[U], len[65536], code[65536]) numpy views of a Codebook."""
+    order = np.ctypeslib.as_array(cb.order)[:cb.nsym].copy()
+    return order, np.ctypeslib.as_array(cb.len).copy(), np.ctypeslib.as_array(cb.code).copy()
+
+
+def header_bits(cb, n):
+    v = ctypes.c_uint64()
+    check(load().hz_header_bits(ctypes.byref(cb), n, ctypes.byref(v)), "hz_header_bits")
+    return v.value
+
+
+def payload_bits(cb, hist):
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    v = ctypes.c_uint64()
+    check(load().hz_payload_bits(ctypes.byref(cb), h.ctypes.data_as(ctypes.c_void_p), ctypes.byref(v)),
+          "hz_payload_bits")
+    return v.value
+
+
+def write_header(cb, n, last_byte=0):
+    """-> (complete header bytes, pending bit count, pending byte MSB-aligned)."""
+    hb = header_bits(cb, n)
+    out = np.zeros(hb // 8 + 8, dtype=np.uint8)
+    nb, pb, pend = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint8()
+    check(load().hz_header_write(ctypes.byref(cb), n, last_byte, out.ctypes.data_as(ctypes.c_void_p), out.size,
+                                 ctypes.byref(nb), ctypes.byref(pb), ctypes.byref(pend)), "hz_header_write")
+    return out[:nb.value].tobytes(), pb.value, pend.value
+
+
+def parse_header(blob):
+    arr, p = _buf(blob)
+    cb, info = Codebook(), HeaderInfo()
+    check(load().hz_header_parse(p, arr.size, ctypes.byref(cb), ctypes.byref(info)), "hz_header_parse")
+    return cb, info
+
+
+def index_entries(nsym):
+    return load().hz_index_entries(nsym)
+
+
+class Device:
+    """Stage API on device pointers (ints), stream-ordered on one HIP stream."""
+
+    def __init__(self, device=0, stream=None):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.hz_ctx_create(device, ctypes.c_void_p(stream) if stream else None, ctypes.byref(h)),
+              "hz_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.hz_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        check(self.lib.hz_ctx_set_stream(self.h, ctypes.c_void_p(stream)), "hz_ctx_set_stream")
+
+    def sync(self):
+        check(self.lib.hz_ctx_sync(self.h), "hz_ctx_sync")
+
+    def hist16(self, d_in, n, d_hist, accumulate=False):
+        check(self.lib.hz_hist16(self.h, d_in, n, d_hist, int(accumulate)), "hz_hist16")
+
+    def upload(self, cb):
+        check(self.lib.hz_codebook_upload(self.h, ctypes.byref(cb)), "hz_codebook_upload")
+
+    def pack(self, d_in, n, start_bit, lead, d_out, out_cap, d_index=None):
+        check(self.lib.hz_pack(self.h, d_in, n, start_bit, lead, d_out, out_cap, d_index), "hz_pack")
+
+    def decode(self, d_payload, payload_bytes, nsym, d_index, d_out):
+        check(self.lib.hz_decode(self.h, d_payload, payload_bytes, nsym, d_index, d_out), "hz_decode")
+
+    def index_build(self, d_payload, payload_bytes, start_bit, nsym, d_index):
+        check(self.lib.hz_index_build(self.h, d_payload, payload_bytes, start_bit, nsym, d_index), "hz_index_build")
+
+    def generate(self, d_out, n, offset=0, kind=1, alpha=1.1, seed=42):
+        check(self.lib.hz_generate(self.h, d_out, n, offset, kind, alpha, seed), "hz_generate")
+
+    def kernel_ms(self, stage):
+        v = ctypes.c_float()
+        check(self.lib.hz_last_kernel_ms(self.h, stage, ctypes.byref(v)), "hz_last_kernel_ms")
+        return v.value

@@ -1,0 +1,377 @@
+// hz_codebook.cpp -- host codebook, header bit-writer / parser and the device
+// table images (encode and decode) built from a codebook.
+//
+// The codebook follows the reference GPU encoder exactly:
+//   order : thrust::sequence + stable sort_by_key of (count, symbol)
+//           (Compressor.cu:387-393,414,419-425)  -> (count asc, symbol asc)
+//   tree  : GenerateCL (gpuHuffmanConstruction.h:353-466) == sequential
+//           Huffman whose picks are the two smallest (count, age) nodes, leaves
+//           older than internals; pinned by oracle/generatecl_literal.py
+//   bits  : first child '1', second '0', root first (GenerateCW h:468-494 +
+//           toCpu h:562-574)
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "huffman_amd.h"
+#include "hz_internal.h"
+
+namespace {
+
+// LSD radix sort of u64 keys with 16-bit digits over the bits in use.
+void radix_sort_u64(std::vector<uint64_t>& k) {
+    if (k.size() < 2) return;
+    uint64_t mx = 0;
+    for (uint64_t v : k) mx |= v;
+    int bits = 64 - __builtin_clzll(mx | 1);
+    std::vector<uint64_t> tmp(k.size());
+    std::vector<uint32_t> cnt(65536);
+    for (int sh = 0; sh < bits; sh += 16) {
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
+        uint32_t sum = 0;
+        for (auto& c : cnt) { uint32_t t = c; c = sum; sum += t; }
+        for (uint64_t v : k) tmp[cnt[(v >> sh) & 0xffff]++] = v;
+        k.swap(tmp);
+    }
+}
+
+struct BitWriter {
+    uint8_t* p;
+    uint64_t cap, pos = 0;
+    uint64_t acc = 0;
+    int nacc = 0;
+    bool overflow = false;
+    void put(uint64_t v, int nbits) {
+        while (nbits > 0) {
+            int take = nbits > 32 ? 32 : nbits;
+            uint64_t part = (v >> (nbits - take)) & ((1ull << take) - 1);
+            acc = (acc << take) | part;
+            nacc += take;
+            nbits -= take;
+            while (nacc >= 8) {
+                nacc -= 8;
+                if (pos < cap) p[pos] = (uint8_t)(acc >> nacc);
+                else overflow = true;
+                pos++;
+            }
+        }
+    }
+};
+
+struct BitReader {
+    const uint8_t* p;
+    uint64_t len, bit = 0;
+    bool eof = false;
+    uint64_t get(int n) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; ++i) {
+            if ((bit >> 3) >= len) { eof = true; return 0; }
+            v = (v << 1) | ((p[bit >> 3] >> (7 - (bit & 7))) & 1);
+            bit++;
+        }
+        return v;
+    }
+};
+
+}  // namespace
+
+extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
+    if (!hist || !cb) return HZ_EINVAL;
+    memset(cb->len, 0, sizeof(cb->len));
+    memset(cb->code, 0, sizeof(cb->code));
+    cb->nsym = cb->max_len = cb->min_len = 0;
+    std::vector<uint64_t> keys;
+    keys.reserve(HZ_NSYM);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        if (hist[s]) {
+            if (hist[s] >> 47) return HZ_EINVAL;  // > 2^47 symbols: out of range
+            keys.push_back((hist[s] << 16) | s);
+        }
+    }
+    const uint32_t U = (uint32_t)keys.size();
+    cb->nsym = U;
+    if (U == 0) return HZ_OK;
+    radix_sort_u64(keys);  // (count, symbol) ascending == thrust stable order
+    for (uint32_t i = 0; i < U; ++i) cb->order[i] = (uint16_t)(keys[i] & 0xffff);
+    if (U == 1) {  // reference defect B4: its code would be empty; use "0"
+        cb->len[cb->order[0]] = 1;
+        cb->code[cb->order[0]] = 0;
+        cb->max_len = cb->min_len = 1;
+        return HZ_OK;
+    }
+    const uint32_t nn = 2 * U - 1;
+    std::vector<uint64_t> f(nn);
+    std::vector<uint32_t> lc(nn), rc(nn);
+    for (uint32_t i = 0; i < U; ++i) f[i] = keys[i] >> 16;
+    uint32_t li = 0, qi = U;
+    for (uint32_t nx = U; nx < nn; ++nx) {
+        uint32_t pick[2];
+        for (int j = 0; j < 2; ++j) {
+            if (li < U && (qi >= nx || f[li] <= f[qi])) pick[j] = li++;  // leaf wins ties (older)
+            else pick[j] = qi++;
+        }
+        f[nx] = f[pick[0]] + f[pick[1]];
+        lc[nx] = pick[0];
+        rc[nx] = pick[1];
+    }
+    std::vector<uint32_t> dep(nn);
+    std::vector<uint64_t> cw(nn);
+    dep[nn - 1] = 0;
+    cw[nn - 1] = 0;
+    for (uint32_t v = nn - 1; v >= U; --v) {
+        dep[lc[v]] = dep[v] + 1; cw[lc[v]] = (cw[v] << 1) | 1u;  // first child '1'
+        dep[rc[v]] = dep[v] + 1; cw[rc[v]] = cw[v] << 1;         // second child '0'
+        if (dep[lc[v]] > HZ_MAXLEN) return HZ_ETOOLONG;
+    }
+    uint32_t mx = 0, mn = 255;
+    for (uint32_t i = 0; i < U; ++i) {
+        const uint32_t s = cb->order[i];
+        if (dep[i] > HZ_MAXLEN) return HZ_ETOOLONG;
+        cb->len[s] = (uint8_t)dep[i];
+        cb->code[s] = cw[i];
+        mx = std::max(mx, dep[i]);
+        mn = std::min(mn, dep[i]);
+    }
+    cb->max_len = mx;
+    cb->min_len = mn;
+    return HZ_OK;
+}
+
+extern "C" int hz_header_bits(const hz_codebook* cb, uint64_t n, uint64_t* bits) {
+    if (!cb || !bits) return HZ_EINVAL;
+    uint64_t b = 8ull * (3 + (n & 1)) + 64;
+    for (uint32_t i = 0; i < cb->nsym; ++i) b += 24 + cb->len[cb->order[i]];
+    *bits = b;
+    return HZ_OK;
+}
+
+extern "C" int hz_payload_bits(const hz_codebook* cb, const uint64_t* hist, uint64_t* bits) {
+    if (!cb || !hist || !bits) return HZ_EINVAL;
+    uint64_t b = 0;
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) b += hist[s] * cb->len[s];
+    *bits = b;
+    return HZ_OK;
+}
+
+// Compressor.cu:431-487 with the writer semantics of :637-669,692-700.
+extern "C" int hz_header_write(const hz_codebook* cb, uint64_t n, uint8_t last_byte, uint8_t* out, uint64_t cap,
+                               uint64_t* bytes, uint32_t* pending_bits, uint8_t* pending) {
+    if (!cb || !out || !bytes || !pending_bits || !pending) return HZ_EINVAL;
+    BitWriter w{out, cap};
+    w.put(cb->nsym & 0xff, 8);            // fwrite(&uniqueSymbolCount, 2, ...) LE   :434
+    w.put((cb->nsym >> 8) & 0xff, 8);
+    w.put(n & 1, 8);                      // isOdd                                   :438
+    if (n & 1) w.put(last_byte, 8);       // lastByte                                :439-443
+    for (uint32_t i = 0; i < cb->nsym; ++i) {
+        const uint32_t s = cb->order[i];
+        w.put(s, 16);                     // writeFromUShort, high byte first        :463,648-656
+        w.put(cb->len[s] & 0xff, 8);      // writeFromUChar(L)                        :465
+        w.put(cb->code[s], cb->len[s]);   // code string, first char first           :470-481
+    }
+    for (int b = 0; b < 8; ++b) w.put((n >> (8 * b)) & 0xff, 8);  // writeFileSize    :487,661-669
+    if (w.overflow) return HZ_ECAP;
+    *bytes = w.pos;
+    *pending_bits = (uint32_t)w.nacc;
+    *pending = w.nacc ? (uint8_t)((w.acc << (8 - w.nacc)) & 0xff) : 0;
+    return HZ_OK;
+}
+
+// Decompressor.cu:65-103 (+ the build's U == 0 convention).
+extern "C" int hz_header_parse(const uint8_t* f, uint64_t len, hz_codebook* cb, hz_header_info* info) {
+    if (!f || !cb || !info) return HZ_EINVAL;
+    if (len < 3) return HZ_EFORMAT;
+    uint32_t U = (uint32_t)f[0] | ((uint32_t)f[1] << 8);
+    const int odd = f[2] != 0;
+    uint64_t pre = 3;
+    uint8_t last = 0;
+    if (odd) {
+        if (len < 4) return HZ_EFORMAT;
+        last = f[3];
+        pre = 4;
+    }
+    if (U == 0) U = (len == pre + 8) ? 0 : 65536;
+    memset(cb->len, 0, sizeof(cb->len));
+    memset(cb->code, 0, sizeof(cb->code));
+    cb->nsym = U;
+    BitReader r{f, len, pre * 8};
+    uint32_t mx = 0, mn = 255;
+    for (uint32_t i = 0; i < U; ++i) {
+        const uint32_t s = (uint32_t)r.get(16);
+        const uint32_t L = (uint32_t)r.get(8);
+        if (r.eof) return HZ_EFORMAT;
+        if (L == 0 || L > HZ_MAXLEN) return HZ_EFORMAT;  // reference reads 0 as 65536 (:94-95)
+        if (cb->len[s]) return HZ_EFORMAT;               // duplicate symbol
+        cb->order[i] = (uint16_t)s;
+        cb->len[s] = (uint8_t)L;
+        cb->code[s] = r.get((int)L);
+        mx = std::max(mx, L);
+        mn = std::min(mn, L);
+    }
+    uint64_t n = 0;
+    for (int b = 0; b < 8; ++b) n |= r.get(8) << (8 * b);
+    if (r.eof) return HZ_EFORMAT;
+    cb->max_len = U ? mx : 0;
+    cb->min_len = U ? mn : 0;
+    info->n = n;
+    info->payload_byte = r.bit >> 3;
+    info->payload_bit = (uint32_t)(r.bit & 7);
+    info->is_odd = (uint32_t)odd;
+    info->last_byte = last;
+    info->nsym = U;
+    if (n / 2 > 0 && U == 0) return HZ_EFORMAT;
+    return HZ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Device table images.
+// ---------------------------------------------------------------------------
+namespace hz {
+
+int select_enc_mode(const hz_codebook* cb) {
+    if (cb->max_len <= 16) return ENC_DENSE;
+    if (cb->max_len <= kNarrowMaxLen) return ENC_HOT;
+    return ENC_WIDE;
+}
+
+// DENSE: entry s = (code << 1 | 1) << (16 - L), 17 bits at bit 17*s (LE bit order).
+std::vector<uint32_t> build_enc_dense(const hz_codebook* cb) {
+    std::vector<uint32_t> img((kDenseLdsBytes + 16) / 4, 0u);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const uint32_t L = cb->len[s];
+        if (!L) continue;
+        const uint64_t f = ((cb->code[s] << 1) | 1u) << (16 - L);
+        const uint64_t bit = (uint64_t)s * 17;
+        const uint64_t w = bit >> 5, sh = bit & 31;
+        const uint64_t v = f << sh;
+        img[w] |= (uint32_t)v;
+        img[w + 1] |= (uint32_t)(v >> 32);
+    }
+    return img;
+}
+
+// HOT: slot (s & 0x7fff) holds the shorter-coded of {slot, slot | 0x8000} when its
+// code fits 25 bits: valid << 31 | (s >> 15) << 30 | L << 25 | code.
+std::vector<uint32_t> build_enc_hot(const hz_codebook* cb) {
+    std::vector<uint32_t> img(kHotLdsBytes / 4, 0u);
+    for (uint32_t slot = 0; slot < 32768; ++slot) {
+        int best = -1;
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t s = slot | (h << 15);
+            const uint32_t L = cb->len[s];
+            if (!L || L > (uint32_t)kHotMaxLen) continue;
+            if (best < 0 || L < cb->len[best]) best = (int)s;
+        }
+        if (best >= 0) {
+            const uint32_t s = (uint32_t)best;
+            img[slot] = (1u << 31) | ((s >> 15) << 30) | ((uint32_t)cb->len[s] << 25) | (uint32_t)cb->code[s];
+        }
+    }
+    return img;
+}
+
+std::vector<uint64_t> build_enc_wide(const hz_codebook* cb) {
+    std::vector<uint64_t> t(HZ_NSYM, 0ull);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) t[s] = ((uint64_t)cb->len[s] << 56) | cb->code[s];
+    return t;
+}
+
+int select_dec_mode(const hz_codebook* cb) {
+    if (cb->max_len <= 16 && cb->max_len - cb->min_len <= 3) return DEC_DENSE;
+    return DEC_LUT;
+}
+
+// DENSE decode: u16 symbol per K-bit window, then 2-bit (L - min_len) per window.
+int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K) {
+    K = (int)cb->max_len;
+    const uint32_t ent = 1u << K;
+    const uint32_t symwords = ent / 2 ? ent / 2 : 1;
+    const uint32_t lenwords = ent / 16 ? ent / 16 : 1;
+    uint32_t words = symwords + lenwords;
+    words = (words + 3) & ~3u;
+    img.assign(words, 0u);
+    std::vector<uint8_t> seen(ent, 0);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const uint32_t L = cb->len[s];
+        if (!L) continue;
+        const uint32_t lo = (uint32_t)cb->code[s] << (K - L), hi = ((uint32_t)cb->code[s] + 1) << (K - L);
+        for (uint32_t i = lo; i < hi; ++i) {
+            if (seen[i]) return HZ_EFORMAT;  // not a prefix code
+            seen[i] = 1;
+            img[i >> 1] |= s << (16 * (i & 1));
+            img[symwords + (i >> 4)] |= (L - cb->min_len) << ((i & 15) * 2);
+        }
+    }
+    return HZ_OK;
+}
+
+namespace {
+struct CodeRec { uint64_t code; uint32_t len; uint32_t sym; };
+
+constexpr uint32_t kLeafBit = 1u << 31;
+inline uint32_t leaf(uint32_t L, uint32_t sym) { return kLeafBit | (L << 16) | sym; }
+
+// Fill a table of 2^nb entries for codes whose first D bits are consumed.
+int fill_level(std::vector<uint32_t>& tab, size_t base, int nb, int D, const std::vector<CodeRec>& recs,
+               std::vector<uint32_t>& l2) {
+    // group codes longer than D + nb by their next nb bits
+    std::vector<std::vector<CodeRec>> deeper;
+    std::vector<int> deeper_idx(1u << nb, -1);
+    for (const CodeRec& c : recs) {
+        const uint32_t rem = c.len - D;  // bits after the consumed prefix
+        const uint64_t r = c.code & ((rem >= 64) ? ~0ull : ((1ull << rem) - 1));
+        if ((int)rem <= nb) {
+            const uint64_t lo = r << (nb - rem), hi = (r + 1) << (nb - rem);
+            for (uint64_t i = lo; i < hi; ++i) {
+                if (tab[base + i]) return HZ_EFORMAT;
+                tab[base + i] = leaf(c.len, c.sym);
+            }
+        } else {
+            const uint32_t q = (uint32_t)(r >> (rem - nb));
+            if (deeper_idx[q] < 0) { deeper_idx[q] = (int)deeper.size(); deeper.emplace_back(); }
+            deeper[deeper_idx[q]].push_back(c);
+        }
+    }
+    for (uint32_t q = 0; q < (1u << nb); ++q) {
+        if (deeper_idx[q] < 0) continue;
+        if (tab[base + q]) return HZ_EFORMAT;
+        const std::vector<CodeRec>& sub = deeper[deeper_idx[q]];
+        uint32_t mx = 0;
+        for (const CodeRec& c : sub) mx = std::max(mx, c.len);
+        const int D2 = D + nb;
+        const int nb2 = std::min<int>((int)mx - D2, kDecLevelBits);
+        const size_t off = l2.size();
+        if (off + (1ull << nb2) >= (1ull << 26)) return HZ_ENOMEM;
+        l2.resize(off + (1ull << nb2), 0u);
+        tab[base + q] = ((uint32_t)nb2 << 26) | (uint32_t)off;
+        int rc = fill_level(l2, off, nb2, D2, sub, l2);
+        if (rc) return rc;
+    }
+    return HZ_OK;
+}
+}  // namespace
+
+// LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
+    K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
+    if (K1 < 1) K1 = 1;
+    std::vector<CodeRec> recs;
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) recs.push_back({cb->code[s], cb->len[s], s});
+    img.assign(1u << K1, 0u);
+    l2.clear();
+    int rc = fill_level(img, 0, K1, 0, recs, l2);
+    if (rc) return rc;
+    // Unused windows (incomplete codes) decode as a 1-bit filler so a lane
+    // that runs past its unit's end never stalls.
+    for (auto& e : img) if (!e) e = leaf(1, 0);
+    for (auto& e : l2) if (!e) e = leaf(1, 0);
+    if (l2.empty()) l2.push_back(leaf(1, 0));
+    return HZ_OK;
+}
+
+}  // namespace hz

@@ -1,0 +1,557 @@
+// hz_host.cpp -- C ABI implementation: contexts, stage wrappers, and the
+// file-level `archive` / `extract` flow (Compressor.cu:315-632,
+// Decompressor.cu:47-114). Device work always runs through the gfx950 kernels
+// of hz_kernels.hip; there is no CPU fallback for any stage.
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <iostream>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "huffman_amd.h"
+#include "hz_internal.h"
+
+namespace hz {
+int select_enc_mode(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_dense(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_hot(const hz_codebook* cb);
+std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
+int select_dec_mode(const hz_codebook* cb);
+int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
+}  // namespace hz
+
+using namespace hz;
+
+#define HZ_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return HZ_EHIP; } while (0)
+
+struct hz_ctx {
+    int device = 0;
+    int ncu = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    Tables t;
+    unsigned long long* d_desc = nullptr;
+    uint64_t desc_cap = 0;          // entries
+    uint32_t* d_err = nullptr;
+    uint32_t* h_err = nullptr;      // pinned
+    unsigned long long* d_thr = nullptr;
+    double thr_alpha = -1.0;
+    hipEvent_t ev[4][2] = {};
+    bool ev_used[4] = {false, false, false, false};
+};
+
+extern "C" const char* hz_strerror(int st) {
+    switch (st) {
+        case HZ_OK: return "ok";
+        case HZ_EINVAL: return "invalid argument";
+        case HZ_ENOMEM: return "out of memory";
+        case HZ_EHIP: return "HIP runtime error";
+        case HZ_ETOOLONG: return "code longer than supported";
+        case HZ_EFORMAT: return "malformed compressed stream";
+        case HZ_ECAP: return "output capacity too small";
+        case HZ_ETIMEOUT: return "device wait timed out";
+        case HZ_EIO: return "file I/O error";
+        case HZ_ENODEV: return "no usable gfx950 device";
+        default: return "unknown error";
+    }
+}
+
+extern "C" int hz_version(void) { return 1; }
+
+static void free_tables(Tables& t) {
+    (void)hipFree(t.d_enc_lds);
+    (void)hipFree(t.d_enc_wide);
+    (void)hipFree(t.d_dec_lds);
+    (void)hipFree(t.d_dec_l2);
+    t = Tables();
+}
+
+extern "C" int hz_ctx_create(int device, void* stream, hz_ctx** out) {
+    if (!out) return HZ_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return HZ_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HZ_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HZ_ENODEV;
+    std::unique_ptr<hz_ctx> c(new hz_ctx());
+    c->device = device;
+    c->ncu = prop.multiProcessorCount;
+    HZ_TRY(hipSetDevice(device));
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+    } else {
+        HZ_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    HZ_TRY(hipMalloc(&c->d_err, 16));
+    HZ_TRY(hipMemset(c->d_err, 0, 16));
+    HZ_TRY(hipHostMalloc(&c->h_err, 16, hipHostMallocDefault));
+    *c->h_err = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 2; ++j) HZ_TRY(hipEventCreate(&c->ev[i][j]));
+    *out = c.release();
+    return HZ_OK;
+}
+
+extern "C" int hz_ctx_destroy(hz_ctx* c) {
+    if (!c) return HZ_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_tables(c->t);
+    (void)hipFree(c->d_desc);
+    (void)hipFree(c->d_err);
+    (void)hipFree(c->d_thr);
+    (void)hipHostFree(c->h_err);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 2; ++j) (void)hipEventDestroy(c->ev[i][j]);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return HZ_OK;
+}
+
+extern "C" int hz_ctx_set_stream(hz_ctx* c, void* stream) {
+    if (!c || !stream) return HZ_EINVAL;
+    if (c->own_stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+        c->own_stream = false;
+    }
+    c->stream = (hipStream_t)stream;
+    return HZ_OK;
+}
+
+extern "C" int hz_ctx_sync(hz_ctx* c) {
+    if (!c) return HZ_EINVAL;
+    (void)hipSetDevice(c->device);
+    HZ_TRY(hipStreamSynchronize(c->stream));
+    if (*c->h_err) {
+        const uint32_t e = *c->h_err;
+        *c->h_err = 0;
+        HZ_TRY(hipMemset(c->d_err, 0, 16));
+        return (e & 1u) ? HZ_ETIMEOUT : (e & 4u) ? HZ_ECAP : HZ_EFORMAT;
+    }
+    return HZ_OK;
+}
+
+static int arm_err_check(hz_ctx* c) {
+    HZ_TRY(hipMemcpyAsync(c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return HZ_OK;
+}
+
+extern "C" int hz_last_kernel_ms(hz_ctx* c, int stage, float* ms) {
+    if (!c || !ms || stage < 0 || stage > 3) return HZ_EINVAL;
+    if (!c->ev_used[stage]) { *ms = 0.f; return HZ_OK; }
+    HZ_TRY(hipEventElapsedTime(ms, c->ev[stage][0], c->ev[stage][1]));
+    return HZ_OK;
+}
+
+extern "C" int hz_hist16(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d_hist, int accumulate) {
+    if (!c || !d_hist || (n && !d_in)) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    if (!accumulate) HZ_TRY(hipMemsetAsync(d_hist, 0, HZ_NSYM * sizeof(uint64_t), c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][0], c->stream));
+    HZ_TRY(launch_hist16(d_in, n, reinterpret_cast<unsigned long long*>(d_hist), c->ncu, c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
+    c->ev_used[HZ_STAGE_HIST] = true;
+    return HZ_OK;
+}
+
+template <typename T>
+static int upload(T** dptr, const std::vector<T>& v, hipStream_t s) {
+    if (*dptr) { (void)hipFree(*dptr); *dptr = nullptr; }
+    if (v.empty()) return HZ_OK;
+    HZ_TRY(hipMalloc(dptr, v.size() * sizeof(T)));
+    HZ_TRY(hipMemcpyAsync(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    HZ_TRY(hipStreamSynchronize(s));  // v may be a temporary
+    return HZ_OK;
+}
+
+extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
+    if (!c || !cb) return HZ_EINVAL;
+    if (cb->max_len > HZ_MAXLEN) return HZ_ETOOLONG;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(hipStreamSynchronize(c->stream));  // previous tables may still be in use
+    Tables& t = c->t;
+    free_tables(t);
+    if (cb->nsym == 0) return HZ_OK;
+    t.max_len = (int)cb->max_len;
+    t.min_len = (int)cb->min_len;
+    t.enc_mode = select_enc_mode(cb);
+    int rc;
+    if (t.enc_mode == ENC_DENSE) {
+        std::vector<uint32_t> img = build_enc_dense(cb);
+        t.enc_lds_bytes = (uint32_t)(img.size() * 4);
+        if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
+    } else if (t.enc_mode == ENC_HOT) {
+        std::vector<uint32_t> img = build_enc_hot(cb);
+        t.enc_lds_bytes = (uint32_t)(img.size() * 4);
+        if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
+    }
+    if ((rc = upload(&t.d_enc_wide, build_enc_wide(cb), c->stream))) return rc;
+    t.dec_mode = select_dec_mode(cb);
+    std::vector<uint32_t> dimg, l2;
+    if (t.dec_mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
+    if (rc) return rc;
+    while (dimg.size() % 4) dimg.push_back(0);
+    t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
+    if ((rc = upload(&t.d_dec_lds, dimg, c->stream))) return rc;
+    if (l2.empty()) l2.push_back(0x80010000u);
+    t.dec_l2_entries = l2.size();
+    if ((rc = upload(&t.d_dec_l2, l2, c->stream))) return rc;
+    return HZ_OK;
+}
+
+extern "C" uint64_t hz_index_stride(void) { return kDUSyms; }
+extern "C" uint64_t hz_index_entries(uint64_t nsym) { return (nsym + kDUSyms - 1) / kDUSyms; }
+extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) {
+    return 2 * ((nsym + kBlockSyms - 1) / kBlockSyms) * sizeof(uint64_t);
+}
+
+static int ensure_desc(hz_ctx* c, uint64_t nblocks) {
+    if (c->desc_cap >= 2 * nblocks) return HZ_OK;
+    HZ_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(c->d_desc);
+    c->d_desc = nullptr;
+    c->desc_cap = 0;
+    HZ_TRY(hipMalloc(&c->d_desc, 2 * nblocks * sizeof(unsigned long long)));
+    c->desc_cap = 2 * nblocks;
+    return HZ_OK;
+}
+
+extern "C" int hz_pack(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_bit, uint32_t lead, uint8_t* d_out,
+                       uint64_t out_cap, uint64_t* d_index) {
+    if (!c || !d_out) return HZ_EINVAL;
+    if (((uintptr_t)d_out) & 3) return HZ_EINVAL;
+    const uint64_t nsym = n / 2;
+    if (nsym == 0) return HZ_OK;
+    if (!d_in || (((uintptr_t)d_in) & 15)) return HZ_EINVAL;
+    if (c->t.enc_mode < 0) return HZ_EINVAL;
+    // d_out must hold ceil((start_bit + payload_bits) / 32) words; the kernel
+    // drops (and flags HZ_ECAP) any block that would write past out_cap.
+    if (out_cap < 4) return HZ_ECAP;
+    HZ_TRY(hipSetDevice(c->device));
+    const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
+    int rc = ensure_desc(c, nblocks);
+    if (rc) return rc;
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][0], c->stream));
+    HZ_TRY(launch_pack(c->t, d_in, nsym, start_bit, lead, reinterpret_cast<uint32_t*>(d_out), out_cap / 4, c->d_desc,
+                       reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->ncu, c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][1], c->stream));
+    c->ev_used[HZ_STAGE_PACK] = true;
+    return arm_err_check(c);
+}
+
+extern "C" int hz_decode(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
+                         const uint64_t* d_index, uint8_t* d_out) {
+    if (!c) return HZ_EINVAL;
+    if (nsym == 0) return HZ_OK;
+    if (!d_payload || !d_index || !d_out || (((uintptr_t)d_out) & 15)) return HZ_EINVAL;
+    if (c->t.dec_mode < 0) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_DECODE][0], c->stream));
+    HZ_TRY(launch_decode(c->t, d_payload, payload_bytes, nsym, reinterpret_cast<const unsigned long long*>(d_index),
+                         d_out, c->d_err, c->ncu, c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_DECODE][1], c->stream));
+    c->ev_used[HZ_STAGE_DECODE] = true;
+    return arm_err_check(c);
+}
+
+extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                              uint64_t nsym, uint64_t* d_index) {
+    if (!c) return HZ_EINVAL;
+    if (nsym == 0) return HZ_OK;
+    if (!d_payload || !d_index) return HZ_EINVAL;
+    if (c->t.dec_mode < 0) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][0], c->stream));
+    HZ_TRY(launch_index_serial(c->t, d_payload, payload_bytes, start_bit, nsym,
+                               reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][1], c->stream));
+    c->ev_used[HZ_STAGE_INDEX] = true;
+    return arm_err_check(c);
+}
+
+// Zipf thresholds: thr[r-1] = floor(2^64 * sum_{j<=r} j^-alpha / H); thr[255] = max.
+static void zipf_thresholds(double alpha, unsigned long long* thr) {
+    double H = 0.0;
+    for (int r = 1; r <= 256; ++r) H += pow((double)r, -alpha);
+    double cum = 0.0;
+    for (int r = 1; r <= 256; ++r) {
+        cum += pow((double)r, -alpha);
+        const double x = cum / H;
+        thr[r - 1] = (r == 256 || x >= 1.0) ? ~0ull : (unsigned long long)ldexp(x, 64);
+    }
+}
+
+extern "C" int hz_generate(hz_ctx* c, uint8_t* d_out, uint64_t n, uint64_t offset, int kind, double alpha,
+                           uint64_t seed) {
+    if (!c || (n && !d_out) || kind < 0 || kind > 1) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    if (!c->d_thr) HZ_TRY(hipMalloc(&c->d_thr, 256 * sizeof(unsigned long long)));
+    if (kind == 1 && c->thr_alpha != alpha) {
+        static unsigned long long thr[256];
+        zipf_thresholds(alpha, thr);
+        HZ_TRY(hipMemcpy(c->d_thr, thr, sizeof(thr), hipMemcpyHostToDevice));
+        c->thr_alpha = alpha;
+    }
+    HZ_TRY(launch_generate(d_out, n, offset, kind, seed, c->d_thr, c->stream));
+    return HZ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Whole-buffer flows (device work inside) used by the CLI and tests.
+// ---------------------------------------------------------------------------
+namespace {
+
+std::mutex g_mu;
+hz_ctx* g_ctx = nullptr;
+
+int default_ctx(hz_ctx** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx) {
+        int rc = hz_ctx_create(0, nullptr, &g_ctx);
+        if (rc) return rc;
+    }
+    *out = g_ctx;
+    return HZ_OK;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int alloc(size_t n) { return hipMalloc(&p, n ? n : 16) == hipSuccess ? HZ_OK : HZ_ENOMEM; }
+};
+
+struct EncodePlan {
+    std::unique_ptr<hz_codebook> cb{new hz_codebook()};
+    std::vector<uint64_t> hist = std::vector<uint64_t>(HZ_NSYM);
+    uint64_t header_bits = 0, payload_bits = 0;
+};
+
+// Histogram on the device, codebook on the host.
+int plan_encode(hz_ctx* c, const uint8_t* d_in, uint64_t n, EncodePlan& p) {
+    DevBuf dh;
+    int rc = dh.alloc(HZ_NSYM * 8);
+    if (rc) return rc;
+    if ((rc = hz_hist16(c, d_in, n, (uint64_t*)dh.p, 0))) return rc;
+    HZ_TRY(hipMemcpyAsync(p.hist.data(), dh.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = hz_ctx_sync(c))) return rc;
+    if ((rc = hz_codebook_build(p.hist.data(), p.cb.get()))) return rc;
+    hz_header_bits(p.cb.get(), n, &p.header_bits);
+    hz_payload_bits(p.cb.get(), p.hist.data(), &p.payload_bits);
+    return HZ_OK;
+}
+
+// Encode a host buffer into a complete .compressed image.
+int encode_image(const uint8_t* in, uint64_t n, std::vector<uint8_t>& out, uint32_t* nsym_out) {
+    hz_ctx* c;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    HZ_TRY(hipSetDevice(c->device));
+    DevBuf din;
+    if ((rc = din.alloc(n))) return rc;
+    if (n) HZ_TRY(hipMemcpyAsync(din.p, in, n, hipMemcpyHostToDevice, c->stream));
+    EncodePlan p;
+    if ((rc = plan_encode(c, (const uint8_t*)din.p, n, p))) return rc;
+    if (nsym_out) *nsym_out = p.cb->nsym;
+    const uint64_t hbytes_full = p.header_bits / 8;
+    const uint64_t total_bits = p.header_bits + p.payload_bits;
+    const uint64_t file_bytes = (total_bits + 7) / 8;
+    out.assign(file_bytes + 8, 0);
+    uint64_t hb;
+    uint32_t pend_bits;
+    uint8_t pend;
+    rc = hz_header_write(p.cb.get(), n, n & 1 ? in[n - 1] : 0, out.data(), out.size(), &hb, &pend_bits, &pend);
+    if (rc) return rc;
+    if (hb != hbytes_full) return HZ_EINVAL;
+    const uint64_t nsym = n / 2;
+    if (nsym > 0) {
+        if ((rc = hz_codebook_upload(c, p.cb.get()))) return rc;
+        const uint64_t start_bit = pend_bits;
+        const uint64_t pay_bytes = file_bytes - hbytes_full;
+        const uint64_t words = (start_bit + p.payload_bits + 31) / 32;
+        DevBuf dout;
+        if ((rc = dout.alloc(words * 4))) return rc;
+        if ((rc = hz_pack(c, (const uint8_t*)din.p, n, start_bit, (uint32_t)(pend >> (8 - pend_bits)) * (pend_bits ? 1 : 0),
+                          (uint8_t*)dout.p, words * 4, nullptr)))
+            return rc;
+        HZ_TRY(hipMemcpyAsync(out.data() + hbytes_full, dout.p, pay_bytes, hipMemcpyDeviceToHost, c->stream));
+        if ((rc = hz_ctx_sync(c))) return rc;
+    } else if (pend_bits) {
+        out[hbytes_full] = pend;  // unreachable (header is byte aligned without symbols) but kept exact
+    }
+    out.resize(file_bytes);
+    return HZ_OK;
+}
+
+// Decode a complete .compressed image.
+int decode_image(const uint8_t* f, uint64_t len, std::vector<uint8_t>& out) {
+    std::unique_ptr<hz_codebook> cb(new hz_codebook());
+    hz_header_info info;
+    int rc = hz_header_parse(f, len, cb.get(), &info);
+    if (rc) return rc;
+    const uint64_t nsym = info.n / 2;
+    out.assign(2 * nsym + (info.is_odd ? 1 : 0), 0);
+    if (nsym > 0) {
+        hz_ctx* c;
+        if ((rc = default_ctx(&c))) return rc;
+        HZ_TRY(hipSetDevice(c->device));
+        if ((rc = hz_codebook_upload(c, cb.get()))) return rc;
+        const uint64_t pay = len - info.payload_byte;
+        DevBuf dpay, didx, dout;
+        if ((rc = dpay.alloc(pay + 16))) return rc;
+        HZ_TRY(hipMemsetAsync(dpay.p, 0, pay + 16, c->stream));
+        HZ_TRY(hipMemcpyAsync(dpay.p, f + info.payload_byte, pay, hipMemcpyHostToDevice, c->stream));
+        if ((rc = didx.alloc(hz_index_entries(nsym) * 8))) return rc;
+        if ((rc = dout.alloc(2 * nsym + 16))) return rc;
+        if ((rc = hz_index_build(c, (const uint8_t*)dpay.p, pay, info.payload_bit, nsym, (uint64_t*)didx.p))) return rc;
+        if ((rc = hz_decode(c, (const uint8_t*)dpay.p, pay, nsym, (const uint64_t*)didx.p, (uint8_t*)dout.p))) return rc;
+        HZ_TRY(hipMemcpyAsync(out.data(), dout.p, 2 * nsym, hipMemcpyDeviceToHost, c->stream));
+        if ((rc = hz_ctx_sync(c))) return rc;
+    }
+    if (info.is_odd) out[2 * nsym] = (uint8_t)info.last_byte;
+    return HZ_OK;
+}
+
+bool file_exists(const char* name) {
+    struct stat st;
+    return stat(name, &st) == 0;
+}
+
+// Decompressor.cu:185-219: "DECOMPRESSED_FILE", else "DECOMPRESSED_FILE(k)", k = 1..9.
+std::string output_name() {
+    std::string base = "DECOMPRESSED_FILE";
+    if (!file_exists(base.c_str())) return base;
+    std::string name;
+    for (int k = 1; k < 10; ++k) {
+        name = base + "(" + std::to_string(k) + ")";
+        if (!file_exists(name.c_str())) break;
+    }
+    return name;
+}
+
+int read_file(const char* path, std::vector<uint8_t>& buf) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return HZ_EIO;
+    fseek(fp, 0, SEEK_END);
+    long sz = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    if (sz < 0) { fclose(fp); return HZ_EIO; }
+    buf.resize((size_t)sz);
+    size_t got = sz ? fread(buf.data(), 1, (size_t)sz, fp) : 0;
+    fclose(fp);
+    return got == (size_t)sz ? HZ_OK : HZ_EIO;
+}
+
+int write_file(const std::string& path, const uint8_t* p, uint64_t n) {
+    FILE* fp = fopen(path.c_str(), "wb");
+    if (!fp) return HZ_EIO;
+    size_t put = n ? fwrite(p, 1, n, fp) : 0;
+    fclose(fp);
+    return put == n ? HZ_OK : HZ_EIO;
+}
+
+}  // namespace
+
+extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    if ((!in && n) || !out_len) return HZ_EINVAL;
+    std::vector<uint8_t> img;
+    int rc = encode_image(in, n, img, nullptr);
+    if (rc) return rc;
+    *out_len = img.size();
+    if (!out || cap < img.size()) return HZ_ECAP;
+    memcpy(out, img.data(), img.size());
+    return HZ_OK;
+}
+
+extern "C" int hz_encoded_size(const uint8_t* in, uint64_t n, uint64_t* out_len) {
+    if ((!in && n) || !out_len) return HZ_EINVAL;
+    hz_ctx* c;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    HZ_TRY(hipSetDevice(c->device));
+    DevBuf din;
+    if ((rc = din.alloc(n))) return rc;
+    if (n) HZ_TRY(hipMemcpyAsync(din.p, in, n, hipMemcpyHostToDevice, c->stream));
+    EncodePlan p;
+    if ((rc = plan_encode(c, (const uint8_t*)din.p, n, p))) return rc;
+    *out_len = (p.header_bits + p.payload_bits + 7) / 8;
+    return HZ_OK;
+}
+
+extern "C" int hz_decode_host(const uint8_t* file, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* out_n) {
+    if (!file || !out_n) return HZ_EINVAL;
+    std::vector<uint8_t> dec;
+    int rc = decode_image(file, len, dec);
+    if (rc) return rc;
+    *out_n = dec.size();
+    if (cap < dec.size() || (!out && dec.size())) return HZ_ECAP;
+    if (dec.size()) memcpy(out, dec.data(), dec.size());
+    return HZ_OK;
+}
+
+// Compressor.cu:315-632, stdout lines kept (:335-336,385,612-631).
+extern "C" int hz_archive_file(const char* path, int verbose) {
+    if (!path) return HZ_EINVAL;
+    std::vector<uint8_t> in;
+    if (read_file(path, in)) {
+        if (verbose) std::cout << path << " file does not exist" << std::endl << "Process has been terminated" << std::endl;
+        return HZ_EIO;
+    }
+    const uint64_t n = in.size();
+    if (verbose) std::cout << "The size of the sum of ORIGINAL files is: " << n << " bytes" << std::endl;
+    std::vector<uint8_t> img;
+    uint32_t U = 0;
+    int rc = encode_image(in.data(), n, img, &U);
+    if (rc) {
+        if (verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;
+        return rc;
+    }
+    if (verbose) std::cout << "Unique symbols count: " << U << std::endl;
+    std::string outname = std::string(path) + ".compressed";
+    if ((rc = write_file(outname, img.data(), img.size()))) return rc;
+    if (verbose) {
+        const long sz = (long)img.size();
+        std::cout << "The size of the COMPRESSED file is: " << sz << " bytes" << std::endl;
+        const float ratio = 100.0f * (float)sz / (float)n;
+        std::cout << "Compressed file's size is [" << ratio << "%] of the original files." << std::endl;
+        if ((uint64_t)sz > n)
+            std::cout << "\nWARNING: The compressed file's size is larger than the sum of the originals.\n\n";
+        std::cout << std::endl << "Created compressed file: " << outname << std::endl;
+        std::cout << "Compression is complete" << std::endl;
+    }
+    return HZ_OK;
+}
+
+// Decompressor.cu:47-114.
+extern "C" int hz_extract_file(const char* path, char* out_name, size_t out_name_cap, int verbose) {
+    if (!path) return HZ_EINVAL;
+    std::vector<uint8_t> f;
+    if (read_file(path, f)) {
+        if (verbose) std::cout << path << " does not exist" << std::endl;
+        return HZ_EIO;
+    }
+    std::vector<uint8_t> dec;
+    int rc = decode_image(f.data(), f.size(), dec);
+    if (rc) {
+        if (verbose) std::cerr << "extract: " << hz_strerror(rc) << std::endl;
+        return rc;
+    }
+    std::string name = output_name();
+    if ((rc = write_file(name, dec.data(), dec.size()))) return rc;
+    if (out_name && out_name_cap) {
+        strncpy(out_name, name.c_str(), out_name_cap - 1);
+        out_name[out_name_cap - 1] = 0;
+    }
+    if (verbose) std::cout << "Decompression is complete" << std::endl;
+    return HZ_OK;
+}

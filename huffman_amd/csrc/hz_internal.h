@@ -1,0 +1,70 @@
+// hz_internal.h -- shared layout constants and launch interfaces between the
+// host side (hz_host.cpp) and the gfx950 kernels (hz_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hz {
+
+// ---- pack: one wavefront owns a block of 64 lanes x kSPT symbols ----------
+constexpr int kWave = 64;
+constexpr int kSPT = 32;                       // symbols per lane (64 input bytes)
+constexpr int kBlockSyms = kWave * kSPT;       // 2048 symbols = 4 KiB of input
+constexpr int kDUSyms = 512;                   // decode unit: one decode lane's run
+constexpr int kLanesPerDU = kDUSyms / kSPT;    // 16 pack lanes per decode unit
+constexpr int kDUPerBlock = kBlockSyms / kDUSyms;
+constexpr int kPackThreads = 1024;             // 16 waves per CU share one LDS table
+
+// Encode table modes (selected on the host per codebook, DESIGN.md "Pack").
+enum EncMode : int {
+    ENC_DENSE = 0,  // max_len <= 16: 65536 x 17-bit sentinel entries, 139 264 B LDS
+    ENC_HOT = 1,    // max_len <= 26: 32768 u32 slots (tag,len,code) + u64 escapes
+    ENC_WIDE = 2    // anything up to 56 bits: u64 table in global memory
+};
+constexpr uint32_t kDenseLdsBytes = 65536u * 17u / 8u;   // 139 264
+constexpr uint32_t kHotLdsBytes = 32768u * 4u;           // 131 072
+constexpr int kHotMaxLen = 25;                           // codes in a HOT slot
+constexpr int kNarrowMaxLen = 26;                        // u32 register entries
+
+// Decode table modes.
+enum DecMode : int {
+    DEC_DENSE = 0,  // max_len <= 16, max-min <= 3: 2^K u16 symbols + 2-bit lengths in LDS
+    DEC_LUT = 1     // 2^K1 u32 level-1 entries in LDS, deeper levels in global
+};
+constexpr int kDecLutMaxK1 = 14;
+constexpr int kDecLevelBits = 8;
+
+// Look-back descriptor flags (one 8-byte granule each; DESIGN.md "Look-back").
+constexpr unsigned long long kFlagReady = 1ull << 63;
+
+struct Tables {
+    int enc_mode = -1;
+    int dec_mode = -1;
+    int max_len = 0;
+    int min_len = 0;
+    int dec_k = 0;                 // DENSE window bits / LUT level-1 bits
+    uint32_t enc_lds_bytes = 0;
+    uint32_t dec_lds_bytes = 0;
+    uint32_t* d_enc_lds = nullptr; // LDS image for the pack kernel
+    uint64_t* d_enc_wide = nullptr;// 65536 x u64: len << 56 | code
+    uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
+    uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
+    uint64_t dec_l2_entries = 0;
+};
+
+// Launchers (hz_kernels.hip). All stream ordered; return hipError_t.
+hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu,
+                         hipStream_t s);
+hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit,
+                       uint32_t lead, uint32_t* d_out, uint64_t out_words, unsigned long long* d_desc,
+                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s);
+hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                         uint64_t nsym, const unsigned long long* d_index, uint8_t* d_out,
+                         uint32_t* d_err, int ncu, hipStream_t s);
+hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index,
+                               uint32_t* d_err, hipStream_t s);
+hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
+                           const unsigned long long* d_thr, hipStream_t s);
+
+}  // namespace hz

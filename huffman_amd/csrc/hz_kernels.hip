@@ -1,0 +1,712 @@
+// hz_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the Huffman hot path.
+//
+//   k_hist16   65 536-bin histogram of u16 symbols      <- Compressor.cu:38-48
+//   k_pack     codeword lookup + bit-length scan + pack  <- Compressor.cu:50-61,541-576,182-313
+//   k_decode   block-parallel table decode              <- Decompressor.cu:259-291
+//   k_index_serial  decode-unit index of an index-less stream (reference files)
+//   k_generate synthetic Zipf / uniform byte streams (this build's generator)
+//
+// Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
+#include "hz_internal.h"
+
+namespace hz {
+
+#define HZ_DEV __device__ __forceinline__
+
+HZ_DEV uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+HZ_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+HZ_DEV uint32_t shfl_up_u32(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
+HZ_DEV uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+HZ_DEV uint32_t shfl_xor_u32(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
+HZ_DEV uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        uint32_t lo = shfl_xor_u32((uint32_t)v, m), hi = shfl_xor_u32((uint32_t)(v >> 32), m);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+// ===========================================================================
+// Synthetic input generator (not a reference function).
+// ===========================================================================
+HZ_DEV uint8_t gen_byte(uint64_t j, int kind, uint64_t seed, const unsigned long long* t) {
+    uint64_t u = splitmix64(seed ^ j);
+    if (kind == 0) return (uint8_t)u;
+    int lo = 0, hi = 255;
+    while (lo < hi) {
+        int m = (lo + hi) >> 1;
+        if (u < t[m]) hi = m; else lo = m + 1;
+    }
+    return (uint8_t)lo;
+}
+
+__global__ __launch_bounds__(256) void k_generate(uint8_t* __restrict__ out, uint64_t n, uint64_t offset,
+                                                 int kind, uint64_t seed,
+                                                 const unsigned long long* __restrict__ thr) {
+    __shared__ unsigned long long t[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) t[i] = thr ? thr[i] : 0ull;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const bool aligned = (((uintptr_t)out) & 7) == 0;
+    const uint64_t nv = aligned ? n / 8 : 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w |= (uint64_t)gen_byte(offset + i * 8 + k, kind, seed, t) << (8 * k);
+        reinterpret_cast<uint64_t*>(out)[i] = w;
+    }
+    for (uint64_t j = nv * 8 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += stride)
+        out[j] = gen_byte(offset + j, kind, seed, t);
+}
+
+hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
+                           const unsigned long long* d_thr, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t want = (n / 8 + 255) / 256;
+    unsigned grid = (unsigned)(want < 8192 ? (want ? want : 1) : 8192);
+    hipLaunchKernelGGL(k_generate, dim3(grid), dim3(256), 0, s, d_out, n, offset, kind, seed, d_thr);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// Histogram: 65 536 u16 counters packed two per LDS dword (128 KiB, one
+// 1024-thread workgroup per CU). A counter half that wraps is corrected
+// exactly through the value the LDS atomic returns (DESIGN.md "Histogram").
+// ===========================================================================
+constexpr int kHistThreads = 1024;
+constexpr int kHistUnroll = 4;
+
+// Fix-up after `old = atomicAdd(&lds[s >> 1], inc)`; rare (once per 65 536 adds of a bin).
+HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old) {
+    const uint32_t inc = (s & 1) ? 0x10000u : 1u;
+    if (old + inc < old) atomicAdd(&hist[s | 1], 65536ull);  // the dword (high half) wrapped
+    if (!(s & 1) && (old & 0xffffu) == 0xffffu) {            // low half crossed 65 536: undo its carry
+        atomicAdd(&hist[s], 65536ull);
+        uint32_t o2 = atomicSub(&lds[s >> 1], 0x10000u);
+        if (o2 < 0x10000u) atomicAdd(&hist[s | 1], (unsigned long long)(-65536ll));
+    }
+}
+
+HZ_DEV bool hist_needs_fix(uint32_t s, uint32_t old) {
+    const uint32_t inc = (s & 1) ? 0x10000u : 1u;
+    return (old + inc < old) | (!(s & 1) & ((old & 0xffffu) == 0xffffu));
+}
+
+HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s) {
+    uint32_t old = atomicAdd(&lds[s >> 1], (s & 1) ? 0x10000u : 1u);
+    if (hist_needs_fix(s, old)) hist_fix(lds, hist, s, old);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restrict__ in, uint64_t nsym,
+                                                         unsigned long long* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    for (int i = threadIdx.x; i < 32768; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+    uint64_t tail_begin = 0;
+    if (VEC) {
+        const uint4* in4 = reinterpret_cast<const uint4*>(in);
+        const uint64_t nvec = nsym / 8;
+        const uint64_t step = (uint64_t)blockDim.x * kHistUnroll;
+        uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+        per = (per + step - 1) / step * step;
+        const uint64_t beg = blockIdx.x * per;
+        const uint64_t end = beg + per < nvec ? beg + per : nvec;
+        for (uint64_t i = beg + threadIdx.x; i < end; i += step) {
+            uint4 v[kHistUnroll];
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u) {
+                const uint64_t j = i + (uint64_t)u * blockDim.x;
+                v[u] = j < end ? in4[j] : make_uint4(0, 0, 0, 0);
+            }
+            uint32_t old[kHistUnroll * 8];
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u) {
+                const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                const bool ok = i + (uint64_t)u * blockDim.x < end;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                    old[u * 8 + k] = atomicAdd(&lds[s >> 1], ok ? ((s & 1) ? 0x10000u : 1u) : 0u);
+                }
+            }
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u) {
+                const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    any |= hist_needs_fix((wd[k >> 1] >> (16 * (k & 1))) & 0xffffu, old[u * 8 + k]);
+            }
+            if (__builtin_expect(any, 0)) {
+                for (int u = 0; u < kHistUnroll; ++u) {
+                    if (i + (uint64_t)u * blockDim.x >= end) continue;
+                    const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                        if (hist_needs_fix(s, old[u * 8 + k])) hist_fix(lds, hist, s, old[u * 8 + k]);
+                    }
+                }
+            }
+        }
+        tail_begin = nvec * 8;
+    }
+    // Scalar symbols: the < 8-symbol tail (VEC) or everything (unaligned input).
+    {
+        const uint64_t nscalar = nsym - tail_begin;
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nscalar; k += stride) {
+            const uint64_t i = tail_begin + k;
+            hist_one(lds, hist, (uint32_t)in[2 * i] | ((uint32_t)in[2 * i + 1] << 8));
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
+        const uint32_t v = lds[i];
+        if (v & 0xffffu) atomicAdd(&hist[2 * i], (unsigned long long)(v & 0xffffu));
+        if (v >> 16) atomicAdd(&hist[2 * i + 1], (unsigned long long)(v >> 16));
+    }
+}
+
+hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu, hipStream_t s) {
+    const uint64_t nsym = n / 2;
+    if (nsym == 0) return hipSuccess;
+    const bool vec = (((uintptr_t)d_in) & 15) == 0;
+    const void* fn = vec ? (const void*)k_hist16<true> : (const void*)k_hist16<false>;
+    static bool attr_done[2] = {false, false};
+    if (!attr_done[vec]) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        if (e != hipSuccess) return e;
+        attr_done[vec] = true;
+    }
+    // One workgroup per CU; fewer for small inputs (every WG zeroes + flushes 128 KiB).
+    uint64_t want = (nsym + 65535) / 65536;
+    unsigned grid = (unsigned)(want < (uint64_t)ncu ? (want ? want : 1) : ncu);
+    if (vec)
+        hipLaunchKernelGGL(k_hist16<true>, dim3(grid), dim3(kHistThreads), 131072, s, d_in, nsym, d_hist);
+    else
+        hipLaunchKernelGGL(k_hist16<false>, dim3(grid), dim3(kHistThreads), 131072, s, d_in, nsym, d_hist);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// Pack. One wavefront owns a block of 2048 symbols (4 KiB of input, 64 lanes x
+// 32 contiguous symbols). Per block:
+//   1. 16-B loads of the lane's 64 input bytes; codeword lookups in the LDS
+//      table (DENSE / HOT) or global memory (escapes / WIDE);
+//   2. a wave scan of (bit count, last 32 bits) gives every lane its offset in
+//      the block and the bits that precede it;
+//   3. decoupled look-back over per-block 8-byte descriptors gives the
+//      block's absolute start bit (blocks are dealt to waves round-robin, all
+//      waves resident, spins bounded);
+//   4. every lane writes the 32-bit words whose LAST bit falls in its run, so
+//      each output word is written exactly once, by plain stores, with no
+//      pre-zeroing and no atomics.
+// ===========================================================================
+struct PackArgs {
+    const uint8_t* in;
+    uint64_t nsym;
+    uint64_t nblocks;
+    const uint32_t* lds_img;
+    uint32_t lds_words;
+    const unsigned long long* wide;
+    uint32_t* out;
+    uint64_t out_words;          // stores beyond this are dropped (caller under-sized d_out)
+    uint64_t start_bit;
+    uint32_t lead;
+    unsigned long long* g1;      // aggregate: flag | tail32 << 24 | bits
+    unsigned long long* g2;      // inclusive: flag | absolute end bit
+    unsigned long long* index;   // decode-unit start bits (optional)
+    uint32_t* err;
+};
+
+template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
+template <> struct PackEnt<ENC_WIDE> { using T = uint64_t; static constexpr int kShift = 56; };
+
+constexpr uint32_t kSpinLimit = 1u << 24;
+
+constexpr int pack_threads(int mode) { return mode == ENC_WIDE ? 512 : kPackThreads; }
+
+template <int MODE>
+__global__ __launch_bounds__(pack_threads(MODE)) void k_pack(PackArgs a) {
+    using T = typename PackEnt<MODE>::T;
+    constexpr int SH = PackEnt<MODE>::kShift;
+    constexpr T CMASK = (T(1) << SH) - 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (MODE != ENC_WIDE) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
+        const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+        const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
+        // ---- 1. load + lookup ------------------------------------------------
+        uint32_t raw[kSPT / 2];
+        if (nvalid == kSPT) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
+#pragma unroll
+            for (int q = 0; q < kSPT / 8; ++q) {
+                const uint4 v = p[q];
+                raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSPT / 2; ++k) {
+                uint32_t w = 0;
+                if (2 * k < nvalid) w = (uint32_t)a.in[2 * (sym0 + 2 * k)] | ((uint32_t)a.in[2 * (sym0 + 2 * k) + 1] << 8);
+                if (2 * k + 1 < nvalid) w |= ((uint32_t)a.in[2 * (sym0 + 2 * k + 1)] | ((uint32_t)a.in[2 * (sym0 + 2 * k + 1) + 1] << 8)) << 16;
+                raw[k] = w;
+            }
+        }
+        T e[kSPT];
+        if (MODE == ENC_DENSE) {
+#pragma unroll
+            for (int k = 0; k < kSPT; ++k) {
+                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                const uint32_t bit = s * 17u;
+                const uint32_t w = bit >> 5;
+                const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
+                const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
+                const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
+                e[k] = (k < nvalid && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
+            }
+        } else if (MODE == ENC_HOT) {
+            uint32_t miss = 0;
+#pragma unroll
+            for (int k = 0; k < kSPT; ++k) {
+                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                const uint32_t v = lds[s & 0x7fffu];
+                const bool hit = (v >> 30) == (2u | (s >> 15));
+                e[k] = (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu));
+                if (!hit && k < nvalid) miss |= 1u << k;
+                if (k >= nvalid) e[k] = 0;
+            }
+            if (miss) {  // rare for skewed data: slot collisions and codes > 25 bits
+#pragma unroll
+                for (int k = 0; k < kSPT; ++k) {
+                    if (miss & (1u << k)) {
+                        const unsigned long long wv = a.wide[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
+                        e[k] = (T)(((wv >> 56) << SH) | (wv & CMASK));
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSPT; ++k) {
+                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
+            }
+        }
+        // ---- 2. lane totals and the wave scan ---------------------------------
+        uint32_t n = 0;
+        uint64_t t64 = 0;
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t L = (uint32_t)(e[k] >> SH);
+            n += L;
+            t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
+        }
+        uint32_t sn = n, st = (uint32_t)t64;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t on = shfl_up_u32(sn, d), ot = shfl_up_u32(st, d);
+            if (lane >= d) {
+                st = sn >= 32 ? st : (sn == 0 ? ot : ((ot << sn) | st));
+                sn += on;
+            }
+        }
+        uint32_t ex_n = shfl_up_u32(sn, 1), ex_t = shfl_up_u32(st, 1);
+        if (lane == 0) { ex_n = 0; ex_t = 0; }
+        const uint32_t agg = shfl_u32(sn, 63), btail = shfl_u32(st, 63);
+        if (lane == 0)
+            __hip_atomic_store(&a.g1[blk], kFlagReady | ((unsigned long long)btail << 24) | agg,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- 3. decoupled look-back -------------------------------------------
+        uint64_t excl = 0;
+        int64_t j = (int64_t)blk - 1;
+        uint32_t spins = 0;
+        bool failed = false;
+        for (;;) {
+            const int64_t jj = j - lane;
+            uint64_t val = 0;
+            int stt = 0;  // 0 not ready, 1 aggregate, 2 inclusive
+            if (jj < 0) {
+                stt = 2; val = a.start_bit;
+            } else {
+                const unsigned long long v2 = __hip_atomic_load(&a.g2[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v2 & kFlagReady) {
+                    stt = 2; val = v2 & ~kFlagReady;
+                } else {
+                    const unsigned long long v1 = __hip_atomic_load(&a.g1[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v1 & kFlagReady) { stt = 1; val = v1 & 0xffffffull; }
+                }
+            }
+            const uint64_t incm = __ballot(stt == 2);
+            const uint64_t nrm = __ballot(stt == 0);
+            const int fi = incm ? __builtin_ctzll(incm) : 64;
+            const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+            if (nrm & upto) {
+                if (++spins > kSpinLimit) { failed = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += wave_sum_u64(lane <= fi ? val : 0);
+            if (fi < 64) break;
+            j -= 64;
+        }
+        if (failed) {
+            if (lane == 0) atomicOr(a.err, 1u);
+            return;
+        }
+        uint32_t ptail = a.lead;
+        if (blk > 0) {
+            unsigned long long v1 = 0;
+            if (lane == 0) {
+                uint32_t sp = 0;
+                while (!((v1 = __hip_atomic_load(&a.g1[blk - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kFlagReady)
+                       && ++sp < kSpinLimit)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            ptail = (uint32_t)(shfl_u32((uint32_t)(v1 >> 24), 0));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store(&a.g2[blk], kFlagReady | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- 4. emit -----------------------------------------------------------
+        const uint64_t o = excl + ex_n;
+        const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
+        uint32_t na = (uint32_t)(o & 31);
+        uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
+        uint64_t wi = o >> 5;
+        // Every word this lane writes lies below the block's inclusive end,
+        // so one bound check per block covers all of them.
+        const bool fits = ((excl + agg + 31) >> 5) <= a.out_words;
+        if (!fits && lane == 0) atomicOr(a.err, 4u);
+        uint32_t* dst = a.out + wi;
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t L = (uint32_t)(e[k] >> SH);
+            uint64_t c = (uint64_t)(e[k] & CMASK);
+            if (MODE == ENC_WIDE && L > 32) {
+                const uint32_t Lh = L - 32;
+                acc = (acc << Lh) | (c >> 32);
+                na += Lh;
+                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
+                acc = (acc << 32) | (c & 0xffffffffull);
+                na += 32;
+                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
+            } else if (L) {
+                acc = (acc << L) | c;
+                na += L;
+                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
+            }
+        }
+        if (fits && nvalid > 0 && sym0 + (uint64_t)nvalid == a.nsym && na > 0)
+            *dst = bswap32((uint32_t)(acc << (32 - na)));
+        if (a.index && (lane % kLanesPerDU) == 0 && nvalid > 0)
+            a.index[sym0 / kDUSyms] = o;
+    }
+}
+
+hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
+                       uint32_t* d_out, uint64_t out_words, unsigned long long* d_desc, unsigned long long* d_index, uint32_t* d_err,
+                       int ncu, hipStream_t s) {
+    if (nsym == 0) return hipSuccess;
+    const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
+    hipError_t e = hipMemsetAsync(d_desc, 0, nblocks * 2 * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    PackArgs a;
+    a.in = d_in; a.nsym = nsym; a.nblocks = nblocks;
+    a.lds_img = t.d_enc_lds; a.lds_words = t.enc_lds_bytes / 4;
+    a.wide = reinterpret_cast<const unsigned long long*>(t.d_enc_wide);
+    a.out = d_out; a.out_words = out_words; a.start_bit = start_bit; a.lead = lead;
+    a.g1 = d_desc; a.g2 = d_desc + nblocks; a.index = d_index; a.err = d_err;
+    // Every wave must be resident (look-back waits on other waves' blocks):
+    // one 1024-thread workgroup per CU, never more workgroups than CUs.
+    const uint64_t waves_needed = nblocks;
+    const int threads = t.enc_mode == ENC_WIDE ? pack_threads(ENC_WIDE) : kPackThreads;
+    uint64_t wgs = (waves_needed + (threads / 64) - 1) / (threads / 64);
+    if (wgs > (uint64_t)ncu) wgs = ncu;
+    const uint32_t lds = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes;
+    const void* fn = t.enc_mode == ENC_DENSE ? (const void*)k_pack<ENC_DENSE>
+                   : t.enc_mode == ENC_HOT ? (const void*)k_pack<ENC_HOT> : (const void*)k_pack<ENC_WIDE>;
+    static bool attr[3] = {false, false, false};
+    if (!attr[t.enc_mode]) {
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr[t.enc_mode] = true;
+    }
+    switch (t.enc_mode) {
+        case ENC_DENSE: hipLaunchKernelGGL(k_pack<ENC_DENSE>, dim3(wgs), dim3(kPackThreads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL(k_pack<ENC_HOT>, dim3(wgs), dim3(kPackThreads), lds, s, a); break;
+        default: hipLaunchKernelGGL(k_pack<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// Decode. One lane decodes one decode unit (512 symbols) from the start bit
+// the index gives, through an LDS table:
+//   DENSE: 2^K u16 symbols + 2-bit (len - min_len), K = max_len <= 16;
+//   LUT:   2^K1 u32 level-1 entries (leaf: 1|len<<16|sym; link: nbits<<26|offset)
+//          with deeper levels in global memory (L2 resident).
+// ===========================================================================
+struct DecArgs {
+    const uint32_t* words;   // payload, aligned down to 4 bytes
+    uint64_t nwords;
+    uint32_t bit_adj;        // payload bit 0 = bit bit_adj of words
+    uint64_t nsym;
+    uint64_t ndu;
+    const unsigned long long* index;
+    const uint32_t* lds_img;
+    uint32_t lds_words;
+    int k;
+    int min_len;
+    int max_len;
+    const uint32_t* l2;
+    uint8_t* out;
+    uint32_t* err;
+};
+
+HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) {
+    return w < a.nwords ? bswap32(__builtin_nontemporal_load(a.words + w)) : 0u;
+}
+
+template <int MODE>
+HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint32_t& sym, uint32_t& L) {
+    if (MODE == DEC_DENSE) {
+        const uint32_t idx = (uint32_t)(win >> (64 - a.k));
+        const uint16_t* l16 = reinterpret_cast<const uint16_t*>(lds);
+        sym = l16[idx];
+        const uint32_t lw = lds[(1u << a.k) / 2 + (idx >> 4)];
+        L = (uint32_t)a.min_len + ((lw >> ((idx & 15) * 2)) & 3u);
+    } else {
+        uint32_t e = lds[(uint32_t)(win >> (64 - a.k))];
+        uint32_t D = (uint32_t)a.k;
+        while (!(e >> 31)) {
+            const uint32_t nb = (e >> 26) & 31u;
+            const uint32_t off = e & 0x3ffffffu;
+            e = a.l2[off + (uint32_t)((win << D) >> (64 - nb))];
+            D += nb;
+        }
+        L = (e >> 16) & 63u;
+        sym = e & 0xffffu;
+    }
+}
+
+// Bit reader over big-endian words: `buf` holds `nb` valid bits at its top;
+// `nxt` is the following word. Supports codes up to 56 bits.
+struct BitReader {
+    uint64_t buf;
+    uint32_t nb;
+    uint32_t nxt;
+    uint64_t wpos;  // index of the word after nxt
+};
+
+HZ_DEV void br_init(BitReader& r, const DecArgs& a, uint64_t p) {
+    const uint64_t w = p >> 5;
+    const uint32_t sh = (uint32_t)(p & 31);
+    r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
+    r.nb = 64 - sh;
+    r.nxt = ld_word(a, w + 2);
+    r.wpos = w + 3;
+}
+
+HZ_DEV uint64_t br_window(BitReader& r) {
+    if (r.nb <= 32) {
+        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+        r.nb += 32;
+        r.nxt = 0;  // refilled by br_next
+    }
+    return r.buf;
+}
+
+HZ_DEV uint64_t br_window_wide(BitReader& r) {
+    // up to 64 valid bits in buf plus the next word for codes > 32 bits
+    return r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
+}
+
+template <int MODE, bool WIDE>
+__global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t du = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; du < a.ndu; du += stride) {
+        const uint64_t s0 = du * kDUSyms;
+        const uint32_t cnt = a.nsym - s0 >= (uint64_t)kDUSyms ? kDUSyms : (uint32_t)(a.nsym - s0);
+        BitReader r;
+        br_init(r, a, a.index[du] + a.bit_adj);
+        uint8_t* o = a.out + 2 * s0;
+        for (uint32_t i = 0; i < cnt; i += 8) {
+            uint32_t pk[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                uint32_t sym = 0, L = 0;
+                if (!WIDE) {
+                    if (r.nb <= 32) {
+                        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+                        r.nb += 32;
+                        r.nxt = ld_word(a, r.wpos++);
+                    }
+                    dec_lookup<MODE>(a, lds, r.buf, sym, L);
+                    r.buf <<= L;
+                    r.nb -= L;
+                } else {
+                    if (r.nb <= 32) {
+                        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+                        r.nb += 32;
+                        r.nxt = ld_word(a, r.wpos++);
+                    }
+                    const uint64_t win = br_window_wide(r);
+                    dec_lookup<MODE>(a, lds, win, sym, L);
+                    if (L < r.nb) {
+                        r.buf <<= L;
+                        r.nb -= L;
+                    } else {
+                        const uint32_t rr = L - r.nb;  // bits taken from nxt
+                        r.buf = rr ? ((uint64_t)r.nxt << (32 + rr)) : ((uint64_t)r.nxt << 32);
+                        r.nb = 32 - rr;
+                        r.nxt = ld_word(a, r.wpos++);
+                    }
+                }
+                pk[q >> 1] |= sym << (16 * (q & 1));
+            }
+            if (i + 8 <= cnt) {
+                *reinterpret_cast<uint4*>(o + 2 * i) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            } else {
+                for (uint32_t q = 0; q < cnt - i; ++q) {
+                    const uint32_t sym = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                    o[2 * (i + q)] = (uint8_t)sym;
+                    o[2 * (i + q) + 1] = (uint8_t)(sym >> 8);
+                }
+            }
+        }
+    }
+}
+
+static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                          uint64_t nsym) {
+    const uintptr_t base = (uintptr_t)d_payload & ~(uintptr_t)3;
+    a.words = reinterpret_cast<const uint32_t*>(base);
+    a.bit_adj = (uint32_t)(((uintptr_t)d_payload & 3) * 8);
+    a.nwords = (payload_bytes + ((uintptr_t)d_payload & 3) + 3) / 4;
+    a.nsym = nsym;
+    a.ndu = (nsym + kDUSyms - 1) / kDUSyms;
+    a.lds_img = t.d_dec_lds;
+    a.lds_words = t.dec_lds_bytes / 4;
+    a.k = t.dec_k;
+    a.min_len = t.min_len;
+    a.max_len = t.max_len;
+    a.l2 = t.d_dec_l2;
+}
+
+hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
+                         const unsigned long long* d_index, uint8_t* d_out, uint32_t* d_err, int ncu,
+                         hipStream_t s) {
+    if (nsym == 0) return hipSuccess;
+    DecArgs a;
+    fill_dec_args(a, t, d_payload, payload_bytes, nsym);
+    a.index = d_index; a.out = d_out; a.err = d_err;
+    const bool wide = t.max_len > 32;
+    const int variant = (t.dec_mode == DEC_DENSE ? 0 : 2) + (wide ? 1 : 0);
+    const void* fns[4] = {(const void*)k_decode<DEC_DENSE, false>, (const void*)k_decode<DEC_DENSE, true>,
+                          (const void*)k_decode<DEC_LUT, false>, (const void*)k_decode<DEC_LUT, true>};
+    static bool attr[4] = {false, false, false, false};
+    if (!attr[variant]) {
+        hipError_t e = hipFuncSetAttribute(fns[variant], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr[variant] = true;
+    }
+    uint64_t wgs = (a.ndu + 1023) / 1024;
+    const uint64_t cap = (uint64_t)ncu * 8;
+    if (wgs > cap) wgs = cap;
+    const uint32_t lds = t.dec_lds_bytes;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((k_decode<DEC_DENSE, false>), dim3(wgs), dim3(1024), lds, s, a); break;
+        case 1: hipLaunchKernelGGL((k_decode<DEC_DENSE, true>), dim3(wgs), dim3(1024), lds, s, a); break;
+        case 2: hipLaunchKernelGGL((k_decode<DEC_LUT, false>), dim3(wgs), dim3(1024), lds, s, a); break;
+        default: hipLaunchKernelGGL((k_decode<DEC_LUT, true>), dim3(wgs), dim3(1024), lds, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+// Serial index build for an index-less stream: one lane walks the stream and
+// records the start bit of every decode unit. Correct for any stream; used for
+// reference-produced files (the parallel self-synchronising builder is the
+// next step).
+template <int MODE>
+__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* index) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    uint64_t pos = start_bit;
+    BitReader r;
+    br_init(r, a, pos + a.bit_adj);
+    for (uint64_t i = 0; i < a.nsym; ++i) {
+        if (i % kDUSyms == 0) index[i / kDUSyms] = pos;
+        if (r.nb <= 32) {
+            r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+            r.nb += 32;
+            r.nxt = ld_word(a, r.wpos++);
+        }
+        const uint64_t win = br_window_wide(r);
+        uint32_t sym, L;
+        dec_lookup<MODE>(a, lds, win, sym, L);
+        if (L == 0) { atomicOr(a.err, 2u); return; }
+        pos += L;
+        if (L < r.nb) {
+            r.buf <<= L;
+            r.nb -= L;
+        } else {
+            const uint32_t rr = L - r.nb;
+            r.buf = rr ? ((uint64_t)r.nxt << (32 + rr)) : ((uint64_t)r.nxt << 32);
+            r.nb = 32 - rr;
+            r.nxt = ld_word(a, r.wpos++);
+        }
+    }
+}
+
+hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index, uint32_t* d_err,
+                               hipStream_t s) {
+    if (nsym == 0) return hipSuccess;
+    DecArgs a;
+    fill_dec_args(a, t, d_payload, payload_bytes, nsym);
+    a.index = nullptr; a.out = nullptr; a.err = d_err;
+    const void* fn = t.dec_mode == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE> : (const void*)k_index_serial<DEC_LUT>;
+    static bool attr[2] = {false, false};
+    if (!attr[t.dec_mode]) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr[t.dec_mode] = true;
+    }
+    if (t.dec_mode == DEC_DENSE)
+        hipLaunchKernelGGL(k_index_serial<DEC_DENSE>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index);
+    else
+        hipLaunchKernelGGL(k_index_serial<DEC_LUT>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index);
+    return hipGetLastError();
+}
+
+}  // namespace hz

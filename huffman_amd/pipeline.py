@@ -1,0 +1,115 @@
+"""Device-resident encode/decode of a byte stream (torch tensors in HBM).
+
+This is the flow `archive` runs, kept on the device end to end so it can be
+timed with inputs already resident in HBM (bench.py) and sharded across ranks
+(huffman_amd/dist.py):
+
+    hist16 (GPU) -> host codebook + header (reference semantics) -> table
+    upload -> pack (GPU, one bit stream + decode-unit index) -> decode (GPU)
+
+PyTorch provides device memory and the stream; every compute stage is a
+gfx950 kernel of libhuffman_amd.so.
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from .codec import Device, build_codebook, header_bits, index_entries, payload_bits, write_header
+
+
+class Plan:
+    """Codebook and stream geometry for one encode."""
+
+    def __init__(self, cb, n_total, hist_local, first_shard=True, shard_bit_offset=0, last_byte=0):
+        self.cb = cb
+        self.n_total = n_total
+        self.header_bits = header_bits(cb, n_total)
+        self.payload_bits = payload_bits(cb, hist_local)        # bits of this shard
+        # absolute payload bit where this shard starts (header pending bits first)
+        self.stream_bit = self.header_bits % 8 + shard_bit_offset
+        self.start_bit = self.stream_bit % 32 if not first_shard else self.stream_bit
+        self.lead = 0
+        self.header = b""
+        if first_shard:
+            self.header, pbits, pend = write_header(cb, n_total, last_byte)
+            self.lead = (pend >> (8 - pbits)) if pbits else 0
+        self.words = (self.start_bit + self.payload_bits + 31) // 32
+
+
+class StreamCodec:
+    def __init__(self, device_index=0):
+        self.device = torch.device("cuda", device_index)
+        torch.cuda.set_device(self.device)
+        # A real (non-null) stream shared by torch and the library, so torch
+        # ops and the HIP kernels are ordered on one queue.
+        self.stream = torch.cuda.Stream(device=self.device)
+        torch.cuda.set_stream(self.stream)
+        self.dev = Device(device_index, stream=self.stream.cuda_stream)
+        self.hist = torch.zeros(_lib.HZ_NSYM, dtype=torch.int64, device=self.device)
+        self.timings = {}
+
+    # -- stages ---------------------------------------------------------------
+    def histogram(self, x, accumulate=False):
+        self.dev.hist16(x.data_ptr(), x.numel(), self.hist.data_ptr(), accumulate)
+        return self.hist
+
+    def make_plan(self, hist_host, n_total, hist_local=None, first_shard=True, shard_bit_offset=0, last_byte=0,
+                  cb=None):
+        t0 = time.perf_counter()
+        cb = build_codebook(hist_host) if cb is None else cb
+        plan = Plan(cb, n_total, hist_host if hist_local is None else hist_local, first_shard, shard_bit_offset,
+                    last_byte)
+        t1 = time.perf_counter()
+        self.dev.upload(cb)
+        t2 = time.perf_counter()
+        self.timings["codebook_ms"] = (t1 - t0) * 1e3
+        self.timings["upload_ms"] = (t2 - t1) * 1e3
+        return plan
+
+    def alloc_payload(self, plan, nsym):
+        out = torch.empty(max(plan.words, 1) * 4 + 16, dtype=torch.uint8, device=self.device)
+        index = torch.empty(max(index_entries(nsym), 1), dtype=torch.int64, device=self.device)
+        return out, index
+
+    def pack(self, x, plan, out, index):
+        self.dev.pack(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
+                      index.data_ptr())
+        return out
+
+    def decode(self, payload, nsym, index, out):
+        self.dev.decode(payload.data_ptr(), payload.numel(), nsym, index.data_ptr(), out.data_ptr())
+        return out
+
+    def sync(self):
+        self.dev.sync()
+
+    def kernel_ms(self):
+        return {
+            "hist": self.dev.kernel_ms(_lib.STAGE_HIST),
+            "pack": self.dev.kernel_ms(_lib.STAGE_PACK),
+            "decode": self.dev.kernel_ms(_lib.STAGE_DECODE),
+        }
+
+    # -- whole stream (one device) ----------------------------------------------
+    def encode(self, x):
+        """Encode a device tensor. Returns (plan, payload tensor, index tensor)."""
+        n = x.numel()
+        self.histogram(x)
+        h = self.hist.cpu().numpy().view(np.uint64)
+        last = int(x[-1].item()) if n % 2 else 0
+        plan = self.make_plan(h, n, last_byte=last)
+        out, index = self.alloc_payload(plan, n // 2)
+        if n // 2:
+            self.pack(x, plan, out, index)
+        return plan, out, index
+
+    def file_image(self, plan, payload):
+        """Complete .compressed bytes (header + payload) on the host."""
+        total = plan.header_bits + plan.payload_bits
+        nbytes = (total + 7) // 8 - plan.header_bits // 8
+        pay = payload[:nbytes].cpu().numpy().tobytes() if nbytes else b""
+        if not pay and plan.header_bits % 8:
+            pay = bytes([plan.lead << (8 - plan.header_bits % 8)])
+        return plan.header + pay

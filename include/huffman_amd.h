@@ -1,0 +1,167 @@
+/*
+ * huffman_amd.h -- C ABI of the MI355X-native Huffman codec (gfx950 / CDNA4).
+ *
+ * Drop-in boundary for the reference yechuan51/huffman path: the `archive` /
+ * `extract` executables and their on-disk `.compressed` format. The reference
+ * has no library API; every entry point below replaces one
+ * stage of Compressor.cu / Decompressor.cu, cited per function.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. `d_*` arguments are device pointers
+ *     (hipMalloc / torch CUDA tensors) and are used stream-ordered on the
+ *     context's stream; host arguments are plain host memory.
+ *   - The caller owns every buffer. A context owns only its scratch, its
+ *     device code tables and (optionally) its stream.
+ *   - Errors: negative HZ_E* status, never abort(). hz_strerror() names them.
+ *   - Threading: one context per device per host thread.
+ *   - Symbols are 16-bit little-endian byte pairs (Compressor.cu:45); an odd
+ *     trailing byte is carried raw in the header (Compressor.cu:339-351).
+ */
+#ifndef HUFFMAN_AMD_H
+#define HUFFMAN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HZ_NSYM 65536  /* alphabet: every u16 value (Compressor.cu:323 kMaxSymbolSize) */
+#define HZ_MAXLEN 56   /* longest supported code (needs > ~5e11 symbols to exceed) */
+
+enum {
+    HZ_OK = 0,
+    HZ_EINVAL = -1,    /* bad argument / alignment */
+    HZ_ENOMEM = -2,    /* host or device allocation failed */
+    HZ_EHIP = -3,      /* HIP runtime error */
+    HZ_ETOOLONG = -4,  /* a code longer than HZ_MAXLEN bits */
+    HZ_EFORMAT = -5,   /* malformed or truncated .compressed stream */
+    HZ_ECAP = -6,      /* output capacity too small */
+    HZ_ETIMEOUT = -7,  /* a device-side wait exceeded its bound (look-back) */
+    HZ_EIO = -8,       /* file I/O error */
+    HZ_ENODEV = -9     /* no usable gfx950 device */
+};
+
+/* Codebook in the reference's order and bit conventions. */
+typedef struct hz_codebook {
+    uint32_t nsym;              /* U, number of symbols with nonzero count */
+    uint32_t max_len;           /* longest code */
+    uint32_t min_len;           /* shortest code */
+    uint32_t reserved;
+    uint16_t order[HZ_NSYM];    /* header order: (count asc, symbol asc) */
+    uint8_t len[HZ_NSYM];       /* code length per symbol value (0 = absent) */
+    uint64_t code[HZ_NSYM];     /* code per symbol, right aligned; first bit = MSB */
+} hz_codebook;
+
+/* Parsed .compressed header (Decompressor.cu:65-103). */
+typedef struct hz_header_info {
+    uint64_t n;                 /* original size in bytes */
+    uint64_t payload_byte;      /* file byte holding the first payload bit */
+    uint32_t payload_bit;       /* bit (MSB = 0) of that byte where the payload starts */
+    uint32_t is_odd;
+    uint32_t last_byte;
+    uint32_t nsym;
+} hz_header_info;
+
+typedef struct hz_ctx hz_ctx;
+
+const char *hz_strerror(int status);
+int hz_version(void);
+
+/* Context: device + stream (stream may be NULL: the context creates its own). */
+int hz_ctx_create(int device, void *stream, hz_ctx **out);
+int hz_ctx_destroy(hz_ctx *ctx);
+int hz_ctx_set_stream(hz_ctx *ctx, void *stream);
+int hz_ctx_sync(hz_ctx *ctx);
+
+/* ---- encode stages ----------------------------------------------------- */
+
+/* 65 536-bin histogram of the u16 symbols of d_in[0..n) into d_hist (u64 x
+ * 65536); accumulate != 0 adds to d_hist instead of overwriting.
+ * Replaces calculateFrequency (Compressor.cu:38-48, launch :369-372). */
+int hz_hist16(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, int accumulate);
+
+/* Host codebook from a host histogram with the reference's semantics: thrust
+ * stable sort (Compressor.cu:378-393,414,419-425) + GenerateCL / GenerateCW /
+ * toCpu (gpuHuffmanConstruction.h:353-494,551-579). U == 1 gets code "0"
+ * (reference defect B4). */
+int hz_codebook_build(const uint64_t *hist, hz_codebook *cb);
+
+/* Header bit length for a codebook and input size: 8*(3 + odd) + sum(24 + L) + 64.
+ * The payload starts at that bit (Compressor.cu:431-487). */
+int hz_header_bits(const hz_codebook *cb, uint64_t n, uint64_t *bits);
+
+/* Payload bits: sum over symbols of hist[s] * len[s]. */
+int hz_payload_bits(const hz_codebook *cb, const uint64_t *hist, uint64_t *bits);
+
+/* Write the header (Compressor.cu:431-487; writers :637-669). Writes
+ * floor(header_bits/8) complete bytes to out; the remaining header_bits%8
+ * bits are returned MSB-aligned in *pending (they begin the payload's first
+ * byte, Compressor.cu:541). */
+int hz_header_write(const hz_codebook *cb, uint64_t n, uint8_t last_byte, uint8_t *out,
+                     uint64_t cap, uint64_t *bytes, uint32_t *pending_bits, uint8_t *pending);
+
+/* Parse a header from the first `len` bytes of a .compressed file.
+ * Replaces Decompressor.cu:65-103 (U 0 => 65536 :69-71; L 0 => 65536 :94-95). */
+int hz_header_parse(const uint8_t *file, uint64_t len, hz_codebook *cb, hz_header_info *info);
+
+/* Upload a codebook's device tables (encode + decode) to the context. */
+int hz_codebook_upload(hz_ctx *ctx, const hz_codebook *cb);
+
+/* Index granularity used by hz_pack / hz_decode (symbols per decode unit). */
+uint64_t hz_index_stride(void);
+uint64_t hz_index_entries(uint64_t nsym);
+uint64_t hz_scratch_bytes(uint64_t nsym);
+
+/* Pack the n/2 symbols of d_in with the uploaded codebook into d_out as one
+ * MSB-first bit stream beginning at bit `start_bit` of d_out (d_out 4-byte
+ * aligned; bits of d_out's first word before start_bit are taken from `lead`,
+ * right aligned, i.e. the header's pending bits). Bits after the stream's end
+ * up to the next 32-bit word are zero. d_index (optional, hz_index_entries()
+ * u64) receives the absolute start bit of every decode unit. Replaces
+ * populateCWLength + transform_inclusive_scan + encodeFromCW
+ * (Compressor.cu:50-61,541-576,182-313) and writeFileContent (:673-684,597-601). */
+int hz_pack(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t start_bit, uint32_t lead,
+            uint8_t *d_out, uint64_t out_cap, uint64_t *d_index);
+
+/* Decode nsym symbols from d_payload (bit stream as hz_pack writes it) into
+ * d_out (2*nsym bytes). d_index: start bit of every decode unit (from hz_pack,
+ * or hz_index_build for an index-less stream). Replaces translateFile
+ * (Decompressor.cu:259-291). */
+int hz_decode(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t nsym,
+              const uint64_t *d_index, uint8_t *d_out);
+
+/* Build the decode-unit index of an index-less stream (a .compressed file from
+ * the reference encoder) on the device. */
+int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                   uint64_t nsym, uint64_t *d_index);
+
+/* Kernel timings of the last hz_hist16 / hz_pack / hz_decode call on this
+ * context, in milliseconds (HIP events on the context stream). */
+int hz_last_kernel_ms(hz_ctx *ctx, int stage, float *ms);
+enum { HZ_STAGE_HIST = 0, HZ_STAGE_PACK = 1, HZ_STAGE_DECODE = 2, HZ_STAGE_INDEX = 3 };
+
+/* Synthetic inputs on the device (DESIGN.md "Synthetic inputs"): byte i of the
+ * stream = f(splitmix64(seed ^ (offset + i))); kind 0 uniform, 1 Zipf(alpha). */
+int hz_generate(hz_ctx *ctx, uint8_t *d_out, uint64_t n, uint64_t offset, int kind, double alpha,
+                uint64_t seed);
+
+/* ---- file level: the CLI contract ---------------------------------------- */
+
+/* `archive <path>`: writes <path>.compressed (Compressor.cu:315-632). */
+int hz_archive_file(const char *path, int verbose);
+/* `extract <path>`: writes ./DECOMPRESSED_FILE or DECOMPRESSED_FILE(k)
+ * (Decompressor.cu:47-114,185-219). out_name may be NULL. */
+int hz_extract_file(const char *path, char *out_name, size_t out_name_cap, int verbose);
+
+/* Whole-buffer host API (device work inside): encode host bytes to a complete
+ * .compressed image / decode one. */
+int hz_encode_host(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int hz_encoded_size(const uint8_t *in, uint64_t n, uint64_t *out_len);
+int hz_decode_host(const uint8_t *file, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *out_n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HUFFMAN_AMD_H */

@@ -1,0 +1,112 @@
+"""ctypes wrapper of oracle/hz_oracle.c -- the CHECKER used by tests only."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "_build", "libhzoracle.so")
+REF_DIR = os.path.join(ORACLE_DIR, "_ref")
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ORACLE_DIR, "hz_oracle.c")):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    lib = ctypes.CDLL(LIB)
+    P, U64 = ctypes.c_void_p, ctypes.c_uint64
+    lib.hzo_hist16.argtypes = [P, U64, P]
+    lib.hzo_codebook.argtypes = [P, P, P, P]
+    lib.hzo_codebook.restype = ctypes.c_int
+    lib.hzo_encode.argtypes = [P, U64, P, U64, ctypes.POINTER(U64)]
+    lib.hzo_encode.restype = ctypes.c_int
+    lib.hzo_decode.argtypes = [P, U64, P, U64, ctypes.POINTER(U64)]
+    lib.hzo_decode.restype = ctypes.c_int
+    lib.hzo_pack_range.argtypes = [P, U64, U64, P, P, U64, P]
+    lib.hzo_encoded_bits.argtypes = [U64, ctypes.c_uint32, P, P, ctypes.POINTER(U64)]
+    lib.hzo_encoded_bits.restype = U64
+    lib.hzo_zipf_thresholds.argtypes = [ctypes.c_double, P]
+    lib.hzo_gen.argtypes = [P, U64, U64, ctypes.c_int, U64, P]
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def as_u8(data):
+    return np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                dtype=np.uint8)
+
+
+def hist16(data):
+    a = as_u8(data)
+    h = np.zeros(65536, dtype=np.uint64)
+    load().hzo_hist16(_p(a), a.size, _p(h))
+    return h
+
+
+def codebook(hist):
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    order = np.zeros(65536, dtype=np.uint16)
+    ln = np.zeros(65536, dtype=np.uint8)
+    code = np.zeros(65536, dtype=np.uint64)
+    U = load().hzo_codebook(_p(h), _p(order), _p(ln), _p(code))
+    if U < 0:
+        raise RuntimeError(f"hzo_codebook {U}")
+    return order[:U].copy(), ln, code
+
+
+def encode(data):
+    a = as_u8(data)
+    cap = 2 * a.size + 400000
+    out = np.zeros(cap, dtype=np.uint8)
+    n = ctypes.c_uint64()
+    rc = load().hzo_encode(_p(a), a.size, _p(out), cap, ctypes.byref(n))
+    if rc:
+        raise RuntimeError(f"hzo_encode {rc}")
+    return out[:n.value].tobytes()
+
+
+def decode(blob, cap=None):
+    a = as_u8(blob)
+    cap = cap if cap is not None else 16 * a.size + 1024
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = ctypes.c_uint64()
+    rc = load().hzo_decode(_p(a), a.size, _p(out), out.size, ctypes.byref(n))
+    if rc:
+        raise RuntimeError(f"hzo_decode {rc}")
+    return out[:n.value].tobytes()
+
+
+def pack_range(data, sym0, count, ln, code, bit0, nbytes):
+    a = as_u8(data)
+    out = np.zeros(nbytes, dtype=np.uint8)
+    load().hzo_pack_range(_p(a), sym0, count, _p(np.ascontiguousarray(ln)), _p(np.ascontiguousarray(code)), bit0,
+                          _p(out))
+    return out
+
+
+def zipf_thresholds(alpha=1.1):
+    t = np.zeros(256, dtype=np.uint64)
+    load().hzo_zipf_thresholds(alpha, _p(t))
+    return t
+
+
+def generate(n, offset=0, kind=1, seed=42, alpha=1.1):
+    t = zipf_thresholds(alpha)
+    out = np.zeros(n, dtype=np.uint8)
+    load().hzo_gen(_p(out), n, offset, kind, seed, _p(t))
+    return out
+
+
+def ref_binary(name):
+    p = os.path.join(REF_DIR, name)
+    return p if os.path.exists(p) else None

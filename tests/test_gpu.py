@@ -1,0 +1,220 @@
+"""GPU parity: the gfx950 path against the CPU oracle (bit-exact), the golden
+fixtures, the reference decoder, and size-independent properties at scale.
+
+Tolerance: none -- every check is bit-exact (integer/bit work)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+INPUTS = ["romeo.txt", "synth_zipf_65537.bin", "synth_unif_65536.bin", "synth_zipf_4099.bin"]
+JPEG = "pexels-vlad-alexandru-popa-1402787.jpg"
+
+
+def read(name):
+    with open(os.path.join(GOLD, name), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="module")
+def hz(built_lib):
+    import huffman_amd
+    return huffman_amd
+
+
+@pytest.fixture(scope="module")
+def codec(built_lib):
+    import torch
+    from huffman_amd.pipeline import StreamCodec
+    return StreamCodec(0)
+
+
+# ---- whole-file parity ---------------------------------------------------------
+@pytest.mark.parametrize("name", INPUTS + [JPEG])
+def test_encode_matches_oracle(hz, name):
+    data = read(name)
+    got = hz.encode(data)
+    assert got == oracle_lib.encode(data)
+    if name in INPUTS:
+        assert got == read(name + ".compressed")
+
+
+@pytest.mark.parametrize("name", INPUTS)
+def test_decode_golden_and_baseline_files(hz, name):
+    data = read(name)
+    assert hz.decode(read(name + ".compressed")) == data
+    assert hz.decode(read(name + ".baseline.compressed")) == data   # reference baseline encoder's bytes
+
+
+def test_decode_baseline_jpeg(hz, tmp_path):
+    exe = oracle_lib.ref_binary("archive_baseline")
+    if exe is None:
+        pytest.skip("reference baseline encoder not built")
+    (tmp_path / "in").write_bytes(read(JPEG))
+    subprocess.run([exe, "in"], cwd=tmp_path, check=True, capture_output=True, timeout=300)
+    assert hz.decode((tmp_path / "in.compressed").read_bytes()) == read(JPEG)
+
+
+def _zipf_bytes(n, seed):
+    return oracle_lib.generate(n, offset=seed * 1000003, kind=1, seed=seed).tobytes()
+
+
+EDGE_SIZES = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 33, 63, 64, 65, 127, 1023, 1024, 1025, 4095, 4096, 4097,
+              8191, 8192, 8193, 2 * 4096 * 16 - 2, 2 * 4096 * 16, 2 * 4096 * 16 + 3, 1000001]
+
+
+@pytest.mark.parametrize("n", EDGE_SIZES)
+def test_edge_sizes(hz, n):
+    data = _zipf_bytes(n, n)
+    blob = hz.encode(data)
+    assert blob == oracle_lib.encode(data)
+    assert hz.decode(blob) == data
+
+
+@pytest.mark.parametrize("data", [b"abab" * 100, b"ab", b"\x00\x00" * 5000 + b"\x01", b"\xff" * 3,
+                                  bytes(range(256)) * 512, b"xy" * 3 + b"z"])
+def test_degenerate_alphabets(hz, data):
+    blob = hz.encode(data)
+    assert blob == oracle_lib.encode(data)
+    assert hz.decode(blob) == data
+
+
+def _fib_input(depth, seed=0):
+    """Symbols with Fibonacci counts: code lengths grow to ~depth bits."""
+    fib = [1, 1]
+    while len(fib) < depth + 1:
+        fib.append(fib[-1] + fib[-2])
+    sym = np.repeat(np.arange(len(fib), dtype=np.uint16) * 257 + 3, fib)
+    np.random.default_rng(seed).shuffle(sym)
+    return sym.astype("<u2").tobytes()
+
+
+@pytest.mark.parametrize("depth,mode", [(20, "HOT"), (28, "WIDE"), (36, "WIDE>32")])
+def test_long_codes_wide_tables(hz, depth, mode):
+    data = _fib_input(depth)
+    h = oracle_lib.hist16(data)
+    _, ln, _ = oracle_lib.codebook(h)
+    assert ln.max() >= depth - 2
+    blob = hz.encode(data)
+    assert blob == oracle_lib.encode(data)
+    assert hz.decode(blob) == data
+
+
+def test_uniform_dense_tables(hz):
+    data = oracle_lib.generate(1 << 22, kind=0, seed=3).tobytes()   # all 65536 symbols, 16-bit codes
+    blob = hz.encode(data)
+    assert blob == oracle_lib.encode(data)
+    assert hz.decode(blob) == data
+
+
+# ---- CLI drop-in -------------------------------------------------------------------
+def test_cli_archive_extract(hz, tmp_path):
+    (tmp_path / "romeo.txt").write_bytes(read("romeo.txt"))
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "archive"), "romeo.txt"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Compression is complete" in r.stdout and "Unique symbols count: 1268" in r.stdout
+    assert (tmp_path / "romeo.txt.compressed").read_bytes() == read("romeo.txt.compressed")
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "romeo.txt.compressed"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "Decompression is complete" in r.stdout
+    assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == read("romeo.txt")
+    # second extract picks DECOMPRESSED_FILE(1) (Decompressor.cu:185-219)
+    subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "romeo.txt.compressed"], cwd=tmp_path, check=True,
+                   capture_output=True, timeout=300)
+    assert (tmp_path / "DECOMPRESSED_FILE(1)").read_bytes() == read("romeo.txt")
+    ref = oracle_lib.ref_binary("extract")
+    if ref:
+        d = tmp_path / "ref"
+        d.mkdir()
+        (d / "x.compressed").write_bytes((tmp_path / "romeo.txt.compressed").read_bytes())
+        subprocess.run([ref, "x.compressed"], cwd=d, check=True, capture_output=True, timeout=300)
+        assert (d / "DECOMPRESSED_FILE").read_bytes() == read("romeo.txt")
+
+
+def test_cli_exit_codes(hz, tmp_path):
+    a = os.path.join(hz.BIN_DIR, "archive")
+    e = os.path.join(hz.BIN_DIR, "extract")
+    assert subprocess.run([a], cwd=tmp_path, capture_output=True).returncode == 0
+    assert subprocess.run([a, "missing"], cwd=tmp_path, capture_output=True).returncode == 0
+    assert subprocess.run([e], cwd=tmp_path, capture_output=True).returncode == 1
+    assert subprocess.run([e, "missing"], cwd=tmp_path, capture_output=True).returncode == 0
+
+
+# ---- device pipeline at scale --------------------------------------------------------
+def test_generator_matches_oracle(codec):
+    import torch
+    n = 1 << 24
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for kind in (0, 1):
+        codec.dev.generate(x.data_ptr(), n, offset=123456789, kind=kind, alpha=1.1, seed=42)
+        torch.cuda.synchronize()
+        host = x.cpu().numpy()
+        for off in (0, 777777, n - 4096):
+            assert np.array_equal(host[off:off + 4096],
+                                  oracle_lib.generate(4096, offset=123456789 + off, kind=kind, seed=42))
+
+
+@pytest.mark.parametrize("kind", [1, 0])
+def test_pipeline_256mib_matches_oracle(codec, kind):
+    import torch
+    n = (256 << 20) + 1  # odd: last byte rides in the header
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=42)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    host = x.cpu().numpy()
+    h_dev = codec.hist.cpu().numpy().view(np.uint64)
+    assert np.array_equal(h_dev, oracle_lib.hist16(host))
+    order, ln, code = oracle_lib.codebook(h_dev)
+    # payload slices against the oracle's packer (bit-exact, block boundaries included)
+    pay = payload.cpu().numpy()
+    nsym = n // 2
+    for sym0, cnt in [(0, 5000), (2048 * 1000 - 7, 9000), (nsym - 6000, 6000)]:
+        # start bit of sym0 from the oracle's lengths
+        pre = int(np.sum(ln[(host[0:2 * sym0:2].astype(np.uint32) | (host[1:2 * sym0:2].astype(np.uint32) << 8))]
+                         .astype(np.uint64)))
+        bit0 = plan.start_bit + pre
+        nbits = int(np.sum(ln[(host[2 * sym0:2 * (sym0 + cnt):2].astype(np.uint32)
+                               | (host[2 * sym0 + 1:2 * (sym0 + cnt):2].astype(np.uint32) << 8))].astype(np.uint64)))
+        b0, b1 = bit0 // 8 + 1, (bit0 + nbits) // 8   # whole bytes inside the slice
+        ref = oracle_lib.pack_range(host, sym0, cnt, ln, code, bit0 - 8 * (bit0 // 8), (nbits + 40) // 8 + 2)
+        assert np.array_equal(pay[b0:b1], ref[b0 - bit0 // 8:b1 - bit0 // 8])
+    # whole file == oracle whole-file encoder
+    assert codec.file_image(plan, payload) == oracle_lib.encode(host)
+    # decode on the device
+    out = torch.empty(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(payload, nsym, index, out)
+    codec.sync()
+    assert torch.equal(out[:2 * nsym], x[:2 * nsym])
+
+
+def test_pipeline_4gib_roundtrip_properties(codec):
+    """Above the reference's 4 GiB int-index limit: u64 counts, round trip,
+    total bits == sum(hist * len), index monotone."""
+    import torch
+    n = (4 << 30) + 6
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=7)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    h = codec.hist.cpu().numpy().view(np.uint64)
+    assert int(h.sum()) == n // 2
+    from huffman_amd import codebook_arrays
+    _, ln, _ = codebook_arrays(plan.cb)
+    assert plan.payload_bits == int(np.sum(h * ln.astype(np.uint64)))
+    idx = index.cpu().numpy()
+    assert idx[0] == plan.start_bit and np.all(np.diff(idx) > 0)
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(payload, n // 2, index, out)
+    codec.sync()
+    assert torch.equal(out[:n], x[:n])
+    del x, out, payload
+    torch.cuda.empty_cache()

@@ -1,0 +1,123 @@
+"""CPU-side checks of the product library: it loads, exports every entry point
+include/huffman_amd.h declares, and its host stages (codebook, header writer,
+header parser) match the oracle byte for byte. No compute on a GPU here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def read(name):
+    with open(os.path.join(GOLD, name), "rb") as f:
+        return f.read()
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "huffman_amd.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(hz_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(built_lib, s), s
+    from huffman_amd._lib import PROTOTYPES
+    assert sorted(n for n, _, _ in PROTOTYPES) == syms
+
+
+def test_cli_binaries_built(built_lib):
+    import huffman_amd
+    for name in ("archive", "extract"):
+        assert os.access(os.path.join(huffman_amd.BIN_DIR, name), os.X_OK)
+
+
+def test_ctx_create_fails_loudly_without_gpu(built_lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = built_lib.hz_ctx_create(0, None, ctypes.byref(h))
+    assert rc == -9  # HZ_ENODEV: no silent CPU path
+
+
+def _hist_random(seed, U, hi):
+    rng = np.random.default_rng(seed)
+    h = np.zeros(65536, dtype=np.uint64)
+    h[rng.choice(65536, U, replace=False)] = rng.integers(1, hi, U)
+    return h
+
+
+@pytest.mark.parametrize("U,hi", [(1, 5), (2, 3), (3, 3), (257, 4), (5000, 1000), (65536, 100000)])
+def test_codebook_matches_oracle(built_lib, U, hi):
+    import huffman_amd
+    h = _hist_random(U, U, hi)
+    cb = huffman_amd.build_codebook(h)
+    order, ln, code = huffman_amd.codebook_arrays(cb)
+    o_order, o_ln, o_code = oracle_lib.codebook(h)
+    assert np.array_equal(order, o_order)
+    assert np.array_equal(ln, o_ln)
+    assert np.array_equal(code, o_code)
+    assert cb.max_len == ln.max() and cb.min_len == ln[ln > 0].min()
+
+
+@pytest.mark.parametrize("name", ["romeo.txt", "synth_zipf_65537.bin", "synth_unif_65536.bin", "synth_zipf_4099.bin"])
+def test_header_matches_golden(built_lib, name):
+    import huffman_amd
+    data = read(name)
+    h = oracle_lib.hist16(data)
+    cb = huffman_amd.build_codebook(h)
+    hdr, pbits, pend = huffman_amd.write_header(cb, len(data), data[-1] if len(data) % 2 else 0)
+    gold = read(name + ".compressed")
+    hb = huffman_amd.header_bits(cb, len(data))
+    assert len(hdr) == hb // 8 and pbits == hb % 8
+    assert gold[:len(hdr)] == hdr
+    # pending header bits are the top bits of the first payload byte
+    if pbits:
+        assert (gold[len(hdr)] >> (8 - pbits)) == (pend >> (8 - pbits))
+    total = hb + huffman_amd.payload_bits(cb, h)
+    assert (total + 7) // 8 == len(gold)
+
+
+@pytest.mark.parametrize("name", ["romeo.txt.compressed", "romeo.txt.baseline.compressed",
+                                  "synth_unif_65536.bin.baseline.compressed"])
+def test_header_parse(built_lib, name):
+    import huffman_amd
+    blob = read(name)
+    cb, info = huffman_amd.parse_header(blob)
+    src = read(name.split(".compressed")[0].replace(".baseline", ""))
+    assert info.n == len(src) and info.is_odd == len(src) % 2
+    if info.is_odd:
+        assert info.last_byte == src[-1]
+    assert cb.nsym == np.count_nonzero(oracle_lib.hist16(src))
+
+
+def test_header_parse_rejects_garbage(built_lib):
+    import huffman_amd
+    from huffman_amd import HZError
+    with pytest.raises(HZError):
+        huffman_amd.parse_header(b"\x05\x00\x00\x12")          # truncated codebook
+    with pytest.raises(HZError):
+        huffman_amd.parse_header(b"\x01")
+
+
+def test_header_parse_empty_conventions(built_lib):
+    import huffman_amd
+    for data in (b"", b"x"):
+        blob = oracle_lib.encode(data)
+        cb, info = huffman_amd.parse_header(blob)
+        assert cb.nsym == 0 and info.n == len(data)
+
+
+def test_index_geometry(built_lib):
+    assert built_lib.hz_index_stride() == 512
+    assert built_lib.hz_index_entries(0) == 0
+    assert built_lib.hz_index_entries(513) == 2
