@@ -1,0 +1,80 @@
+"""Multi-process (gloo, CPU) test of the sharded path's exchange logic
+(huffman_amd/dist.py): histogram all-reduce -> global codebook -> all-gather
+of payload bits -> per-shard packing at global bit offsets -> gather + OR
+reassembly. The reassembled file must equal the single-stream encoder's output
+byte for byte. The per-shard packer here is the oracle's (this runs without a
+GPU); on the GPU the same geometry feeds hz_pack (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, kind, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import huffman_amd
+        from huffman_amd import dist as hd
+        data = oracle_lib.generate(n_total, offset=0, kind=kind, seed=11)
+        beg, end = hd.shard_range(n_total, world, rank)
+        shard = data[beg:end]
+        assert beg % 2 == 0
+        hist_local = torch.from_numpy(oracle_lib.hist16(shard).astype(np.int64))
+        h = hd.global_histogram(hist_local).numpy().astype(np.uint64)
+        cb = huffman_amd.build_codebook(h)
+        hb = huffman_amd.header_bits(cb, n_total)
+        pbits = huffman_amd.payload_bits(cb, hist_local.numpy().astype(np.uint64))
+        off, totals = hd.shard_bit_offsets(pbits, torch.device("cpu"))
+        word0, start, words = hd.local_geometry(hb, off, pbits, rank == 0)
+        _, ln, code = huffman_amd.codebook_arrays(cb)
+        buf = oracle_lib.pack_range(shard, 0, shard.size // 2, ln, code, start, words * 4 + 8)
+        if rank == 0:
+            header, pend_bits, pend = huffman_amd.write_header(cb, n_total, int(data[-1]) if n_total % 2 else 0)
+            buf[0] |= pend
+        nbytes = (start + pbits + 7) // 8
+        shards = hd.gather_to(torch.from_numpy(buf), nbytes, dst=0)
+        if rank == 0:
+            # every shard's global word offset from the gathered totals
+            word0s = [hd.local_geometry(hb, sum(totals[:g]), totals[g], g == 0)[0] for g in range(world)]
+            payload = hd.reassemble(shards, word0s, sum(totals), hb)
+            blob = header + payload.tobytes()
+            ok = blob == oracle_lib.encode(data)
+            with open(result_path, "w") as f:
+                f.write("ok" if ok else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,kind", [(2, 1 << 20, 1), (2, (1 << 20) + 3, 0), (3, 300001, 1),
+                                                (4, 4 * 4096 + 2, 1)])
+def test_sharded_stream_equals_single_stream(tmp_path, world, n_total, kind):
+    result = str(tmp_path / "result.txt")
+    mp.start_processes(_worker, args=(world, _free_port(), n_total, kind, result), nprocs=world, join=True,
+                       start_method="spawn")
+    with open(result) as f:
+        assert f.read() == "ok"
+
+
+def test_shard_ranges_cover_and_align():
+    from huffman_amd import dist as hd
+    for n, w in [(10, 3), (1 << 20, 8), (7, 2), (100001, 4)]:
+        rs = [hd.shard_range(n, w, r) for r in range(w)]
+        assert rs[0][0] == 0 and rs[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+        assert all(b % 2 == 0 for b, _ in rs)
