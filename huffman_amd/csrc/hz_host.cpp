@@ -38,8 +38,8 @@ struct hz_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     Tables t;
-    unsigned long long* d_desc = nullptr;
-    uint64_t desc_cap = 0;          // entries
+    unsigned long long* d_desc = nullptr;  // pack scratch: block counts, starts, tile sums
+    uint64_t desc_cap = 0;          // u64 words
     uint32_t* d_err = nullptr;
     uint32_t* h_err = nullptr;      // pinned
     unsigned long long* d_thr = nullptr;
@@ -136,7 +136,7 @@ extern "C" int hz_ctx_sync(hz_ctx* c) {
         const uint32_t e = *c->h_err;
         *c->h_err = 0;
         HZ_TRY(hipMemset(c->d_err, 0, 16));
-        return (e & 1u) ? HZ_ETIMEOUT : (e & 4u) ? HZ_ECAP : HZ_EFORMAT;
+        return (e & 4u) ? HZ_ECAP : HZ_EFORMAT;
     }
     return HZ_OK;
 }
@@ -212,18 +212,16 @@ extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
 
 extern "C" uint64_t hz_index_stride(void) { return kDUSyms; }
 extern "C" uint64_t hz_index_entries(uint64_t nsym) { return (nsym + kDUSyms - 1) / kDUSyms; }
-extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) {
-    return 2 * ((nsym + kBlockSyms - 1) / kBlockSyms) * sizeof(uint64_t);
-}
+extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) { return pack_scratch_words(nsym) * sizeof(uint64_t); }
 
-static int ensure_desc(hz_ctx* c, uint64_t nblocks) {
-    if (c->desc_cap >= 2 * nblocks) return HZ_OK;
+static int ensure_scratch(hz_ctx* c, uint64_t words) {
+    if (c->desc_cap >= words) return HZ_OK;
     HZ_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(c->d_desc);
     c->d_desc = nullptr;
     c->desc_cap = 0;
-    HZ_TRY(hipMalloc(&c->d_desc, 2 * nblocks * sizeof(unsigned long long)));
-    c->desc_cap = 2 * nblocks;
+    HZ_TRY(hipMalloc(&c->d_desc, words * sizeof(unsigned long long)));
+    c->desc_cap = words;
     return HZ_OK;
 }
 
@@ -239,8 +237,7 @@ extern "C" int hz_pack(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t star
     // drops (and flags HZ_ECAP) any block that would write past out_cap.
     if (out_cap < 4) return HZ_ECAP;
     HZ_TRY(hipSetDevice(c->device));
-    const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
-    int rc = ensure_desc(c, nblocks);
+    int rc = ensure_scratch(c, pack_scratch_words(nsym));
     if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][0], c->stream));
     HZ_TRY(launch_pack(c->t, d_in, nsym, start_bit, lead, reinterpret_cast<uint32_t*>(d_out), out_cap / 4, c->d_desc,

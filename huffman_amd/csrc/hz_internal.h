@@ -34,8 +34,6 @@ enum DecMode : int {
 constexpr int kDecLutMaxK1 = 14;
 constexpr int kDecLevelBits = 8;
 
-// Look-back descriptor flags (one 8-byte granule each; DESIGN.md "Look-back").
-constexpr unsigned long long kFlagReady = 1ull << 63;
 
 struct Tables {
     int enc_mode = -1;
@@ -56,8 +54,9 @@ struct Tables {
 hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu,
                          hipStream_t s);
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit,
-                       uint32_t lead, uint32_t* d_out, uint64_t out_words, unsigned long long* d_desc,
+                       uint32_t lead, uint32_t* d_out, uint64_t out_words, unsigned long long* d_scratch,
                        unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s);
+uint64_t pack_scratch_words(uint64_t nsym);  // u64 words of d_scratch hz_pack needs
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                          uint64_t nsym, const unsigned long long* d_index, uint8_t* d_out,
                          uint32_t* d_err, int ncu, hipStream_t s);

@@ -198,18 +198,18 @@ hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_
 }
 
 // ===========================================================================
-// Pack. One wavefront owns a block of 2048 symbols (4 KiB of input, 64 lanes x
-// 32 contiguous symbols). Per block:
-//   1. 16-B loads of the lane's 64 input bytes; codeword lookups in the LDS
-//      table (DENSE / HOT) or global memory (escapes / WIDE);
-//   2. a wave scan of (bit count, last 32 bits) gives every lane its offset in
-//      the block and the bits that precede it;
-//   3. decoupled look-back over per-block 8-byte descriptors gives the
-//      block's absolute start bit (blocks are dealt to waves round-robin, all
-//      waves resident, spins bounded);
-//   4. every lane writes the 32-bit words whose LAST bit falls in its run, so
-//      each output word is written exactly once, by plain stores, with no
-//      pre-zeroing and no atomics.
+// Pack. A block is 2048 symbols (4 KiB of input): one wavefront, 64 lanes x
+// 32 contiguous symbols. Three stream-ordered steps replace the reference's
+// populateCWLength + transform_inclusive_scan + encodeFromCW
+// (Compressor.cu:50-61,541-576,182-313):
+//   k_pack_count : per block, bit count and the block's last 32 code bits
+//   k_scan_*     : exclusive scan of block bit counts -> absolute start bits
+//   k_pack_write : per block, codeword lookup + wave scan of (bits, tail) +
+//                  each lane writes the 32-bit words whose LAST bit falls in
+//                  its run (every word written exactly once, plain stores, no
+//                  pre-zeroing, no atomics, no inter-workgroup waits)
+// Code tables live in LDS (DENSE 17-bit sentinel entries, or HOT tagged
+// slots) and are loaded once per workgroup of a grid-stride kernel.
 // ===========================================================================
 struct PackArgs {
     const uint8_t* in;
@@ -219,11 +219,10 @@ struct PackArgs {
     uint32_t lds_words;
     const unsigned long long* wide;
     uint32_t* out;
-    uint64_t out_words;          // stores beyond this are dropped (caller under-sized d_out)
-    uint64_t start_bit;
-    uint32_t lead;
-    unsigned long long* g1;      // aggregate: flag | tail32 << 24 | bits
-    unsigned long long* g2;      // inclusive: flag | absolute end bit
+    uint64_t out_words;          // stores beyond this are dropped and flagged
+    uint32_t lead;               // bits before the stream's first bit (header pending bits)
+    unsigned long long* blk;     // per block: tail32 << 32 | bits (count) -> start bit (after scan)
+    const unsigned long long* blk_start;
     unsigned long long* index;   // decode-unit start bits (optional)
     uint32_t* err;
 };
@@ -231,174 +230,159 @@ struct PackArgs {
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
 template <> struct PackEnt<ENC_WIDE> { using T = uint64_t; static constexpr int kShift = 56; };
 
-constexpr uint32_t kSpinLimit = 1u << 24;
-
 constexpr int pack_threads(int mode) { return mode == ENC_WIDE ? 512 : kPackThreads; }
 
 template <int MODE>
-__global__ __launch_bounds__(pack_threads(MODE)) void k_pack(PackArgs a) {
+HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid,
+                             typename PackEnt<MODE>::T (&e)[kSPT]) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t raw[kSPT / 2];
+    if (nvalid == kSPT) {
+        const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
+#pragma unroll
+        for (int q = 0; q < kSPT / 8; ++q) {
+            const uint4 v = p[q];
+            raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSPT / 2; ++k) {
+            uint32_t w = 0;
+            if (2 * k < nvalid) w = (uint32_t)a.in[2 * (sym0 + 2 * k)] | ((uint32_t)a.in[2 * (sym0 + 2 * k) + 1] << 8);
+            if (2 * k + 1 < nvalid)
+                w |= ((uint32_t)a.in[2 * (sym0 + 2 * k + 1)] | ((uint32_t)a.in[2 * (sym0 + 2 * k + 1) + 1] << 8)) << 16;
+            raw[k] = w;
+        }
+    }
+    if (MODE == ENC_DENSE) {
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            const uint32_t bit = s * 17u;
+            const uint32_t w = bit >> 5;
+            const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
+            const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
+            const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
+            e[k] = (k < nvalid && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
+        }
+    } else if (MODE == ENC_HOT) {
+        uint32_t miss = 0;
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            const uint32_t v = lds[s & 0x7fffu];
+            const bool hit = (v >> 30) == (2u | (s >> 15));
+            e[k] = k < nvalid ? (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu)) : (T)0;
+            if (!hit && k < nvalid) miss |= 1u << k;
+        }
+        if (miss) {  // rare for skewed data: slot collisions and codes > 25 bits
+#pragma unroll
+            for (int k = 0; k < kSPT; ++k) {
+                if (miss & (1u << k)) {
+                    const unsigned long long wv = a.wide[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
+                    e[k] = (T)(((wv >> 56) << SH) | (wv & CMASK));
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
+        }
+    }
+}
+
+// Lane bit count + last 32 bits, then the wave's inclusive scan of (bits, tail).
+template <int MODE>
+HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane, uint32_t& n, uint32_t& sn,
+                           uint32_t& st) {
+    using T = typename PackEnt<MODE>::T;
+    constexpr int SH = PackEnt<MODE>::kShift;
+    constexpr T CMASK = (T(1) << SH) - 1;
+    n = 0;
+    uint64_t t64 = 0;
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        const uint32_t L = (uint32_t)(e[k] >> SH);
+        n += L;
+        t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
+    }
+    sn = n;
+    st = (uint32_t)t64;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t on = shfl_up_u32(sn, d), ot = shfl_up_u32(st, d);
+        if (lane >= d) {
+            st = sn >= 32 ? st : (sn == 0 ? ot : ((ot << sn) | st));
+            sn += on;
+        }
+    }
+}
+
+template <int MODE>
+HZ_DEV void load_lds_table(uint32_t* lds, const uint32_t* img, uint32_t words) {
     if (MODE != ENC_WIDE) {
-        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
+        const uint4* src = reinterpret_cast<const uint4*>(img);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(pack_threads(MODE)) void k_pack_count(PackArgs a) {
+    using T = typename PackEnt<MODE>::T;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
         const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
         const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
-        // ---- 1. load + lookup ------------------------------------------------
-        uint32_t raw[kSPT / 2];
-        if (nvalid == kSPT) {
-            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
-#pragma unroll
-            for (int q = 0; q < kSPT / 8; ++q) {
-                const uint4 v = p[q];
-                raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kSPT / 2; ++k) {
-                uint32_t w = 0;
-                if (2 * k < nvalid) w = (uint32_t)a.in[2 * (sym0 + 2 * k)] | ((uint32_t)a.in[2 * (sym0 + 2 * k) + 1] << 8);
-                if (2 * k + 1 < nvalid) w |= ((uint32_t)a.in[2 * (sym0 + 2 * k + 1)] | ((uint32_t)a.in[2 * (sym0 + 2 * k + 1) + 1] << 8)) << 16;
-                raw[k] = w;
-            }
-        }
         T e[kSPT];
-        if (MODE == ENC_DENSE) {
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k) {
-                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                const uint32_t bit = s * 17u;
-                const uint32_t w = bit >> 5;
-                const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
-                const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
-                const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
-                e[k] = (k < nvalid && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
-            }
-        } else if (MODE == ENC_HOT) {
-            uint32_t miss = 0;
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k) {
-                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                const uint32_t v = lds[s & 0x7fffu];
-                const bool hit = (v >> 30) == (2u | (s >> 15));
-                e[k] = (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu));
-                if (!hit && k < nvalid) miss |= 1u << k;
-                if (k >= nvalid) e[k] = 0;
-            }
-            if (miss) {  // rare for skewed data: slot collisions and codes > 25 bits
-#pragma unroll
-                for (int k = 0; k < kSPT; ++k) {
-                    if (miss & (1u << k)) {
-                        const unsigned long long wv = a.wide[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
-                        e[k] = (T)(((wv >> 56) << SH) | (wv & CMASK));
-                    }
-                }
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k) {
-                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
-            }
-        }
-        // ---- 2. lane totals and the wave scan ---------------------------------
-        uint32_t n = 0;
-        uint64_t t64 = 0;
-#pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            const uint32_t L = (uint32_t)(e[k] >> SH);
-            n += L;
-            t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
-        }
-        uint32_t sn = n, st = (uint32_t)t64;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t on = shfl_up_u32(sn, d), ot = shfl_up_u32(st, d);
-            if (lane >= d) {
-                st = sn >= 32 ? st : (sn == 0 ? ot : ((ot << sn) | st));
-                sn += on;
-            }
-        }
+        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e);
+        uint32_t n, sn, st;
+        pack_lane_scan<MODE>(e, lane, n, sn, st);
+        if (lane == 63) a.blk[blk] = ((unsigned long long)st << 32) | sn;
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
+    using T = typename PackEnt<MODE>::T;
+    constexpr int SH = PackEnt<MODE>::kShift;
+    constexpr T CMASK = (T(1) << SH) - 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
+    const int lane = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
+        const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+        const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
+        T e[kSPT];
+        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e);
+        uint32_t n, sn, st;
+        pack_lane_scan<MODE>(e, lane, n, sn, st);
         uint32_t ex_n = shfl_up_u32(sn, 1), ex_t = shfl_up_u32(st, 1);
         if (lane == 0) { ex_n = 0; ex_t = 0; }
-        const uint32_t agg = shfl_u32(sn, 63), btail = shfl_u32(st, 63);
-        if (lane == 0)
-            __hip_atomic_store(&a.g1[blk], kFlagReady | ((unsigned long long)btail << 24) | agg,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- 3. decoupled look-back -------------------------------------------
-        uint64_t excl = 0;
-        int64_t j = (int64_t)blk - 1;
-        uint32_t spins = 0;
-        bool failed = false;
-        for (;;) {
-            const int64_t jj = j - lane;
-            uint64_t val = 0;
-            int stt = 0;  // 0 not ready, 1 aggregate, 2 inclusive
-            if (jj < 0) {
-                stt = 2; val = a.start_bit;
-            } else {
-                const unsigned long long v2 = __hip_atomic_load(&a.g2[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v2 & kFlagReady) {
-                    stt = 2; val = v2 & ~kFlagReady;
-                } else {
-                    const unsigned long long v1 = __hip_atomic_load(&a.g1[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (v1 & kFlagReady) { stt = 1; val = v1 & 0xffffffull; }
-                }
-            }
-            const uint64_t incm = __ballot(stt == 2);
-            const uint64_t nrm = __ballot(stt == 0);
-            const int fi = incm ? __builtin_ctzll(incm) : 64;
-            const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
-            if (nrm & upto) {
-                if (++spins > kSpinLimit) { failed = true; break; }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += wave_sum_u64(lane <= fi ? val : 0);
-            if (fi < 64) break;
-            j -= 64;
-        }
-        if (failed) {
-            if (lane == 0) atomicOr(a.err, 1u);
-            return;
-        }
-        uint32_t ptail = a.lead;
-        if (blk > 0) {
-            unsigned long long v1 = 0;
-            if (lane == 0) {
-                uint32_t sp = 0;
-                while (!((v1 = __hip_atomic_load(&a.g1[blk - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kFlagReady)
-                       && ++sp < kSpinLimit)
-                    __builtin_amdgcn_s_sleep(1);
-            }
-            ptail = (uint32_t)(shfl_u32((uint32_t)(v1 >> 24), 0));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(&a.g2[blk], kFlagReady | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- 4. emit -----------------------------------------------------------
-        const uint64_t o = excl + ex_n;
+        const uint64_t bstart = a.blk_start[blk];
+        const uint64_t bend = bstart + shfl_u32(sn, 63);
+        const uint32_t ptail = blk ? (uint32_t)(a.blk[blk - 1] >> 32) : a.lead;
+        const uint64_t o = bstart + ex_n;
         const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
         uint32_t na = (uint32_t)(o & 31);
         uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
-        uint64_t wi = o >> 5;
-        // Every word this lane writes lies below the block's inclusive end,
-        // so one bound check per block covers all of them.
-        const bool fits = ((excl + agg + 31) >> 5) <= a.out_words;
+        // every word this block writes lies below ceil(bend / 32)
+        const bool fits = ((bend + 31) >> 5) <= a.out_words;
         if (!fits && lane == 0) atomicOr(a.err, 4u);
-        uint32_t* dst = a.out + wi;
+        uint32_t* dst = a.out + (o >> 5);
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t L = (uint32_t)(e[k] >> SH);
-            uint64_t c = (uint64_t)(e[k] & CMASK);
+            const uint64_t c = (uint64_t)(e[k] & CMASK);
             if (MODE == ENC_WIDE && L > 32) {
                 const uint32_t Lh = L - 32;
                 acc = (acc << Lh) | (c >> 32);
@@ -420,38 +404,134 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack(PackArgs a) {
     }
 }
 
+// ---- exclusive scan of block bit counts (low 32 bits of blk[]) -------------
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 16;                         // counts per thread
+constexpr int kScanTile = kScanThreads * kScanPer;   // 16 384 blocks per tile
+
+HZ_DEV uint64_t block_exclusive_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t lo = shfl_up_u32((uint32_t)x, d), hi = shfl_up_u32((uint32_t)(x >> 32), d);
+        if (lane >= d) x += ((uint64_t)hi << 32) | lo;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int w = 0; w < nw; ++w) { const uint64_t t = sh[w]; sh[w] = s; s += t; }
+        sh[nw] = s;
+    }
+    __syncthreads();
+    total = sh[nw];
+    const uint64_t r = sh[wid] + x - v;
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const unsigned long long* blk, uint64_t nblocks,
+                                                              unsigned long long* tile_sum) {
+    __shared__ uint64_t sh[17];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+        if (base + k < nblocks) s += (uint32_t)blk[base + k];
+    uint64_t total;
+    block_exclusive_scan(s, sh, total);
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(unsigned long long* tile_sum, uint64_t ntiles,
+                                                             uint64_t start_bit) {
+    __shared__ uint64_t sh[17];
+    uint64_t carry = start_bit;
+    for (uint64_t b = 0; b < ntiles; b += kScanThreads) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? tile_sum[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_exclusive_scan(v, sh, total);
+        if (i < ntiles) tile_sum[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long long* blk, uint64_t nblocks,
+                                                             const unsigned long long* tile_off,
+                                                             unsigned long long* blk_start) {
+    __shared__ uint64_t sh[17];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint32_t c[kScanPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        c[k] = base + k < nblocks ? (uint32_t)blk[base + k] : 0u;
+        s += c[k];
+    }
+    uint64_t total;
+    uint64_t run = tile_off[blockIdx.x] + block_exclusive_scan(s, sh, total);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        if (base + k < nblocks) blk_start[base + k] = run;
+        run += c[k];
+    }
+}
+
+uint64_t pack_scratch_words(uint64_t nsym) {
+    const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
+    const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
+    return 2 * nblocks + ntiles;
+}
+
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
-                       uint32_t* d_out, uint64_t out_words, unsigned long long* d_desc, unsigned long long* d_index, uint32_t* d_err,
-                       int ncu, hipStream_t s) {
+                       uint32_t* d_out, uint64_t out_words, unsigned long long* d_scratch,
+                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s) {
     if (nsym == 0) return hipSuccess;
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
-    hipError_t e = hipMemsetAsync(d_desc, 0, nblocks * 2 * sizeof(unsigned long long), s);
-    if (e != hipSuccess) return e;
+    const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
     PackArgs a;
     a.in = d_in; a.nsym = nsym; a.nblocks = nblocks;
     a.lds_img = t.d_enc_lds; a.lds_words = t.enc_lds_bytes / 4;
     a.wide = reinterpret_cast<const unsigned long long*>(t.d_enc_wide);
-    a.out = d_out; a.out_words = out_words; a.start_bit = start_bit; a.lead = lead;
-    a.g1 = d_desc; a.g2 = d_desc + nblocks; a.index = d_index; a.err = d_err;
-    // Every wave must be resident (look-back waits on other waves' blocks):
-    // one 1024-thread workgroup per CU, never more workgroups than CUs.
-    const uint64_t waves_needed = nblocks;
+    a.out = d_out; a.out_words = out_words; a.lead = lead;
+    a.blk = d_scratch;
+    unsigned long long* blk_start = d_scratch + nblocks;
+    unsigned long long* tiles = d_scratch + 2 * nblocks;
+    a.blk_start = blk_start; a.index = d_index; a.err = d_err;
     const int threads = t.enc_mode == ENC_WIDE ? pack_threads(ENC_WIDE) : kPackThreads;
-    uint64_t wgs = (waves_needed + (threads / 64) - 1) / (threads / 64);
-    if (wgs > (uint64_t)ncu) wgs = ncu;
+    const uint64_t waves = (uint64_t)threads / 64;
+    uint64_t wgs = (nblocks + waves - 1) / waves;
+    const uint64_t cap = (uint64_t)ncu * (t.enc_mode == ENC_WIDE ? 4 : 1);  // LDS table: one WG per CU
+    if (wgs > cap) wgs = cap;
     const uint32_t lds = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes;
-    const void* fn = t.enc_mode == ENC_DENSE ? (const void*)k_pack<ENC_DENSE>
-                   : t.enc_mode == ENC_HOT ? (const void*)k_pack<ENC_HOT> : (const void*)k_pack<ENC_WIDE>;
     static bool attr[3] = {false, false, false};
     if (!attr[t.enc_mode]) {
-        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        const void* fc[3] = {(const void*)k_pack_count<ENC_DENSE>, (const void*)k_pack_count<ENC_HOT>,
+                             (const void*)k_pack_count<ENC_WIDE>};
+        const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE>, (const void*)k_pack_write<ENC_HOT>,
+                             (const void*)k_pack_write<ENC_WIDE>};
+        hipError_t e = hipFuncSetAttribute(fc[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(fw[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr[t.enc_mode] = true;
     }
     switch (t.enc_mode) {
-        case ENC_DENSE: hipLaunchKernelGGL(k_pack<ENC_DENSE>, dim3(wgs), dim3(kPackThreads), lds, s, a); break;
-        case ENC_HOT: hipLaunchKernelGGL(k_pack<ENC_HOT>, dim3(wgs), dim3(kPackThreads), lds, s, a); break;
-        default: hipLaunchKernelGGL(k_pack<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_DENSE: hipLaunchKernelGGL(k_pack_count<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL(k_pack_count<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a); break;
+        default: hipLaunchKernelGGL(k_pack_count<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+    }
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
+                       nblocks, tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, start_bit);
+    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
+                       nblocks, (const unsigned long long*)tiles, blk_start);
+    switch (t.enc_mode) {
+        case ENC_DENSE: hipLaunchKernelGGL(k_pack_write<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL(k_pack_write<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a); break;
+        default: hipLaunchKernelGGL(k_pack_write<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
     }
     return hipGetLastError();
 }
@@ -538,8 +618,16 @@ HZ_DEV uint64_t br_window_wide(BitReader& r) {
     return r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
 }
 
+// Each lane decodes kDecStreams consecutive decode units interleaved: one
+// symbol of every stream per step, so the step's LDS lookups, its rare
+// global (deeper-level) lookups and its bit-stream refills are all issued
+// before one wait, and a wave's stall on a long-code lookup is paid once per
+// kDecStreams x 64 symbols instead of once per 64.
+constexpr int kDecStreams = 4;
+
 template <int MODE, bool WIDE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
+    constexpr int S = kDecStreams;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
@@ -547,54 +635,93 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
         for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
+    const uint64_t nlanes = (a.ndu + S - 1) / S;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t du = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; du < a.ndu; du += stride) {
-        const uint64_t s0 = du * kDUSyms;
-        const uint32_t cnt = a.nsym - s0 >= (uint64_t)kDUSyms ? kDUSyms : (uint32_t)(a.nsym - s0);
-        BitReader r;
-        br_init(r, a, a.index[du] + a.bit_adj);
-        uint8_t* o = a.out + 2 * s0;
-        for (uint32_t i = 0; i < cnt; i += 8) {
-            uint32_t pk[4] = {0, 0, 0, 0};
+    for (uint64_t ln = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; ln < nlanes; ln += stride) {
+        BitReader r[S];
+        uint32_t cnt[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const uint64_t du = ln * S + s;
+            const uint64_t s0 = du * kDUSyms;
+            cnt[s] = du >= a.ndu ? 0u : (a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0));
+            br_init(r[s], a, (du < a.ndu ? a.index[du] : 0ull) + a.bit_adj);
+        }
+        uint8_t* o = a.out + 2 * (ln * S * kDUSyms);
+        for (uint32_t i = 0; i < (uint32_t)kDUSyms; i += 8) {
+            uint32_t pk[S][4];
+#pragma unroll
+            for (int s = 0; s < S; ++s) pk[s][0] = pk[s][1] = pk[s][2] = pk[s][3] = 0;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                uint32_t sym = 0, L = 0;
-                if (!WIDE) {
-                    if (r.nb <= 32) {
-                        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
-                        r.nb += 32;
-                        r.nxt = ld_word(a, r.wpos++);
+                uint32_t e[S];
+                uint64_t win[S];
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if (r[s].nb <= 32) {
+                        r[s].buf |= (uint64_t)r[s].nxt << (32 - r[s].nb);
+                        r[s].nb += 32;
+                        r[s].nxt = ld_word(a, r[s].wpos++);
                     }
-                    dec_lookup<MODE>(a, lds, r.buf, sym, L);
-                    r.buf <<= L;
-                    r.nb -= L;
+                    win[s] = WIDE ? br_window_wide(r[s]) : r[s].buf;
+                }
+                uint32_t sym[S], L[S];
+                if (MODE == DEC_DENSE) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) dec_lookup<MODE>(a, lds, win[s], sym[s], L[s]);
                 } else {
-                    if (r.nb <= 32) {
-                        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
-                        r.nb += 32;
-                        r.nxt = ld_word(a, r.wpos++);
+#pragma unroll
+                    for (int s = 0; s < S; ++s) e[s] = lds[(uint32_t)(win[s] >> (64 - a.k))];
+                    // first deeper level for every stream that needs it, all issued before the wait
+                    uint32_t e2[S];
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        e2[s] = e[s];
+                        if (!(e[s] >> 31)) {
+                            const uint32_t nb = (e[s] >> 26) & 31u;
+                            e2[s] = a.l2[(e[s] & 0x3ffffffu) + (uint32_t)((win[s] << a.k) >> (64 - nb))];
+                        }
                     }
-                    const uint64_t win = br_window_wide(r);
-                    dec_lookup<MODE>(a, lds, win, sym, L);
-                    if (L < r.nb) {
-                        r.buf <<= L;
-                        r.nb -= L;
-                    } else {
-                        const uint32_t rr = L - r.nb;  // bits taken from nxt
-                        r.buf = rr ? ((uint64_t)r.nxt << (32 + rr)) : ((uint64_t)r.nxt << 32);
-                        r.nb = 32 - rr;
-                        r.nxt = ld_word(a, r.wpos++);
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        uint32_t ee = e2[s];
+                        if (!(e[s] >> 31)) {
+                            uint32_t D = (uint32_t)a.k + ((e[s] >> 26) & 31u);
+                            while (!(ee >> 31)) {  // codes deeper than k + 8 bits: rare
+                                const uint32_t nb = (ee >> 26) & 31u;
+                                ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[s] << D) >> (64 - nb))];
+                                D += nb;
+                            }
+                        }
+                        L[s] = (ee >> 16) & 63u;
+                        sym[s] = ee & 0xffffu;
                     }
                 }
-                pk[q >> 1] |= sym << (16 * (q & 1));
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if (!WIDE || L[s] < r[s].nb) {
+                        r[s].buf <<= L[s];
+                        r[s].nb -= L[s];
+                    } else {
+                        const uint32_t rr = L[s] - r[s].nb;  // bits taken from nxt
+                        r[s].buf = (uint64_t)r[s].nxt << (32 + rr);
+                        r[s].nb = 32 - rr;
+                        r[s].nxt = ld_word(a, r[s].wpos++);
+                    }
+                    pk[s][q >> 1] |= sym[s] << (16 * (q & 1));
+                }
             }
-            if (i + 8 <= cnt) {
-                *reinterpret_cast<uint4*>(o + 2 * i) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            } else {
-                for (uint32_t q = 0; q < cnt - i; ++q) {
-                    const uint32_t sym = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-                    o[2 * (i + q)] = (uint8_t)sym;
-                    o[2 * (i + q) + 1] = (uint8_t)(sym >> 8);
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                uint8_t* os = o + 2 * (s * kDUSyms + i);
+                if (i + 8 <= cnt[s]) {
+                    *reinterpret_cast<uint4*>(os) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
+                } else if (i < cnt[s]) {
+                    for (uint32_t q = 0; q < cnt[s] - i; ++q) {
+                        const uint32_t v = (pk[s][q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                        os[2 * q] = (uint8_t)v;
+                        os[2 * q + 1] = (uint8_t)(v >> 8);
+                    }
                 }
             }
         }
@@ -634,8 +761,8 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
         if (e != hipSuccess) return e;
         attr[variant] = true;
     }
-    uint64_t wgs = (a.ndu + 1023) / 1024;
-    const uint64_t cap = (uint64_t)ncu * 8;
+    uint64_t wgs = ((a.ndu + kDecStreams - 1) / kDecStreams + 1023) / 1024;
+    const uint64_t cap = (uint64_t)ncu * 4;
     if (wgs > cap) wgs = cap;
     const uint32_t lds = t.dec_lds_bytes;
     switch (variant) {

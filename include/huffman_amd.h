@@ -38,7 +38,7 @@ enum {
     HZ_ETOOLONG = -4,  /* a code longer than HZ_MAXLEN bits */
     HZ_EFORMAT = -5,   /* malformed or truncated .compressed stream */
     HZ_ECAP = -6,      /* output capacity too small */
-    HZ_ETIMEOUT = -7,  /* a device-side wait exceeded its bound (look-back) */
+    HZ_ETIMEOUT = -7,  /* a device-side wait exceeded its bound (reserved) */
     HZ_EIO = -8,       /* file I/O error */
     HZ_ENODEV = -9     /* no usable gfx950 device */
 };
