@@ -253,14 +253,38 @@ std::vector<uint32_t> build_enc_dense(const hz_codebook* cb) {
     return img;
 }
 
-// HOT: slot (s & 0x7fff) holds the shorter-coded of {slot, slot | 0x8000} when its
-// code fits 25 bits: valid << 31 | (s >> 15) << 30 | L << 25 | code.
-std::vector<uint32_t> build_enc_hot(const hz_codebook* cb) {
+// HOT: 32768 slots; symbols s and s ^ m share slot hot_slot(s, m). The slot
+// holds the shorter-coded (more frequent) of the pair when its code fits 25
+// bits: valid << 31 | (s >> 15) << 30 | L << 25 | code. m is chosen per
+// codebook to minimise the escaped probability mass (weight 2^-L).
+uint32_t choose_hot_mask(const hz_codebook* cb) {
+    static const uint32_t cand[] = {0x8000, 0xffff, 0x8080, 0xc0c0, 0x80ff, 0xff80, 0xa0a0, 0xf0f0,
+                                    0x8888, 0xcccc, 0xaaaa, 0x8001, 0xff00, 0x80c0, 0xe0e0, 0x9999};
+    uint32_t best = 0x8000;
+    double best_miss = 1e300;
+    for (uint32_t m : cand) {
+        double miss = 0.0;
+        for (uint32_t s = 0; s < 32768; ++s) {
+            const uint32_t t = s ^ (m & 0x7fffu) ^ 0x8000u;  // the partner with bit 15 set
+            const uint32_t a = cb->len[s], b = cb->len[t];
+            const double wa = a ? ldexp(1.0, -(int)a) : 0.0, wb = b ? ldexp(1.0, -(int)b) : 0.0;
+            const bool a_ok = a && a <= (uint32_t)kHotMaxLen, b_ok = b && b <= (uint32_t)kHotMaxLen;
+            // the slot keeps the better eligible one; everything else escapes
+            if (a_ok && (!b_ok || a <= b)) miss += wb;
+            else if (b_ok) miss += wa;
+            else miss += wa + wb;
+        }
+        if (miss < best_miss) { best_miss = miss; best = m; }
+    }
+    return best;
+}
+
+std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m) {
     std::vector<uint32_t> img(kHotLdsBytes / 4, 0u);
     for (uint32_t slot = 0; slot < 32768; ++slot) {
+        const uint32_t cands[2] = {slot, slot ^ (m & 0x7fffu) ^ 0x8000u};
         int best = -1;
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t s = slot | (h << 15);
+        for (uint32_t s : cands) {
             const uint32_t L = cb->len[s];
             if (!L || L > (uint32_t)kHotMaxLen) continue;
             if (best < 0 || L < cb->len[best]) best = (int)s;
@@ -270,6 +294,20 @@ std::vector<uint32_t> build_enc_hot(const hz_codebook* cb) {
             img[slot] = (1u << 31) | ((s >> 15) << 30) | ((uint32_t)cb->len[s] << 25) | (uint32_t)cb->code[s];
         }
     }
+    return img;
+}
+
+std::vector<uint32_t> build_enc_esc(const hz_codebook* cb) {
+    std::vector<uint32_t> t(HZ_NSYM, 0u);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s] && cb->len[s] <= (uint32_t)kNarrowMaxLen) t[s] = ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
+    return t;
+}
+
+std::vector<uint32_t> build_len8(const hz_codebook* cb) {
+    std::vector<uint32_t> img(kLen8LdsBytes / 4, 0u);
+    uint8_t* b = reinterpret_cast<uint8_t*>(img.data());
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) b[len8_index(s)] = cb->len[s];
     return img;
 }
 

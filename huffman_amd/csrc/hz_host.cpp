@@ -21,7 +21,10 @@
 namespace hz {
 int select_enc_mode(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_dense(const hz_codebook* cb);
-std::vector<uint32_t> build_enc_hot(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m);
+uint32_t choose_hot_mask(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_esc(const hz_codebook* cb);
+std::vector<uint32_t> build_len8(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
@@ -69,6 +72,8 @@ extern "C" int hz_version(void) { return 1; }
 static void free_tables(Tables& t) {
     (void)hipFree(t.d_enc_lds);
     (void)hipFree(t.d_enc_wide);
+    (void)hipFree(t.d_enc_esc);
+    (void)hipFree(t.d_len8);
     (void)hipFree(t.d_dec_lds);
     (void)hipFree(t.d_dec_l2);
     t = Tables();
@@ -191,11 +196,14 @@ extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
         if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
     } else if (t.enc_mode == ENC_HOT) {
-        std::vector<uint32_t> img = build_enc_hot(cb);
+        t.hot_mask = choose_hot_mask(cb);
+        std::vector<uint32_t> img = build_enc_hot(cb, t.hot_mask);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
         if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
+        if ((rc = upload(&t.d_enc_esc, build_enc_esc(cb), c->stream))) return rc;
     }
     if ((rc = upload(&t.d_enc_wide, build_enc_wide(cb), c->stream))) return rc;
+    if ((rc = upload(&t.d_len8, build_len8(cb), c->stream))) return rc;
     t.dec_mode = select_dec_mode(cb);
     std::vector<uint32_t> dimg, l2;
     if (t.dec_mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);

@@ -23,6 +23,7 @@ enum EncMode : int {
 };
 constexpr uint32_t kDenseLdsBytes = 65536u * 17u / 8u;   // 139 264
 constexpr uint32_t kHotLdsBytes = 32768u * 4u;           // 131 072
+constexpr uint32_t kLen8LdsBytes = 65536u;               // u8 code length per symbol (count pass)
 constexpr int kHotMaxLen = 25;                           // codes in a HOT slot
 constexpr int kNarrowMaxLen = 26;                        // u32 register entries
 
@@ -45,10 +46,20 @@ struct Tables {
     uint32_t dec_lds_bytes = 0;
     uint32_t* d_enc_lds = nullptr; // LDS image for the pack kernel
     uint64_t* d_enc_wide = nullptr;// 65536 x u64: len << 56 | code
+    uint32_t* d_enc_esc = nullptr; // 65536 x u32: len << 26 | code (HOT escapes, len <= 26)
+    uint32_t* d_len8 = nullptr;    // LDS image: u8 length at len8_index(s)
+    uint32_t hot_mask = 0x8000;    // HOT pairing: s and s ^ hot_mask share slot
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
     uint64_t dec_l2_entries = 0;
 };
+
+// Count-pass length table layout: the high byte is XORed into the bank bits
+// so skewed symbol sets (small high and low bytes) spread over LDS banks.
+__host__ __device__ inline uint32_t len8_index(uint32_t s) { return s ^ (((s >> 8) & 0x3fu) << 2); }
+
+// HOT slot of symbol s under pairing mask m (bit 15 of m set).
+__host__ __device__ inline uint32_t hot_slot(uint32_t s, uint32_t m) { return (s & 0x8000u) ? (s ^ m) : s; }
 
 // Launchers (hz_kernels.hip). All stream ordered; return hipError_t.
 hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu,

@@ -218,10 +218,13 @@ struct PackArgs {
     const uint32_t* lds_img;
     uint32_t lds_words;
     const unsigned long long* wide;
+    const uint32_t* esc;         // HOT escapes: len << 26 | code
+    const uint32_t* len8_img;    // count pass: u8 lengths (LDS image, 64 KiB)
+    uint32_t hot_mask;
     uint32_t* out;
     uint64_t out_words;          // stores beyond this are dropped and flagged
     uint32_t lead;               // bits before the stream's first bit (header pending bits)
-    unsigned long long* blk;     // per block: tail32 << 32 | bits (count) -> start bit (after scan)
+    unsigned long long* blk;     // per block bit count (k_pack_count)
     const unsigned long long* blk_start;
     unsigned long long* index;   // decode-unit start bits (optional)
     uint32_t* err;
@@ -272,19 +275,23 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            const uint32_t v = lds[s & 0x7fffu];
+            const uint32_t v = lds[hot_slot(s, a.hot_mask)];
             const bool hit = (v >> 30) == (2u | (s >> 15));
             e[k] = k < nvalid ? (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu)) : (T)0;
             if (!hit && k < nvalid) miss |= 1u << k;
         }
-        if (miss) {  // rare for skewed data: slot collisions and codes > 25 bits
+        if (miss) {
+            // Escapes (slot collisions, codes > 25 bits): all 32 loads issued
+            // before one wait; unneeded ones read entry 0 (one cached line).
+            uint32_t w[kSPT];
 #pragma unroll
             for (int k = 0; k < kSPT; ++k) {
-                if (miss & (1u << k)) {
-                    const unsigned long long wv = a.wide[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
-                    e[k] = (T)(((wv >> 56) << SH) | (wv & CMASK));
-                }
+                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                w[k] = a.esc[((miss >> k) & 1u) ? s : 0u];
             }
+#pragma unroll
+            for (int k = 0; k < kSPT; ++k)
+                if ((miss >> k) & 1u) e[k] = (T)(((w[k] >> 26) << SH) | (w[k] & 0x3ffffffu));
         }
     } else {
 #pragma unroll
@@ -332,21 +339,88 @@ HZ_DEV void load_lds_table(uint32_t* lds, const uint32_t* img, uint32_t words) {
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(pack_threads(MODE)) void k_pack_count(PackArgs a) {
-    using T = typename PackEnt<MODE>::T;
+// Bit count per block from a 64 KiB u8 length table (one LDS read per symbol).
+constexpr int kCountThreads = 1024;
+constexpr int kCountUnroll = 2;  // blocks in flight per wave
+
+__global__ __launch_bounds__(kCountThreads) void k_pack_count(PackArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.len8_img);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = threadIdx.x; i < kLen8LdsBytes / 16; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const uint8_t* l8 = reinterpret_cast<const uint8_t*>(lds);
     const int lane = threadIdx.x & 63;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
+    const uint64_t full = a.nsym / kBlockSyms;  // blocks without a tail
+    uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (; blk + (kCountUnroll - 1) * W < full; blk += kCountUnroll * W) {
+        uint4 v[kCountUnroll][kSPT / 8];
+#pragma unroll
+        for (int u = 0; u < kCountUnroll; ++u) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ((blk + u * W) * kBlockSyms + (uint64_t)lane * kSPT));
+#pragma unroll
+            for (int q = 0; q < kSPT / 8; ++q) v[u][q] = p[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kCountUnroll; ++u) {
+            uint32_t n = 0;
+#pragma unroll
+            for (int q = 0; q < kSPT / 8; ++q) {
+                const uint32_t wd[4] = {v[u][q].x, v[u][q].y, v[u][q].z, v[u][q].w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) n += l8[len8_index((wd[k >> 1] >> (16 * (k & 1))) & 0xffffu)];
+            }
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) n += shfl_xor_u32(n, m);
+            if (lane == 0) a.blk[blk + u * W] = n;
+        }
+    }
+    for (; blk < a.nblocks; blk += W) {
         const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
-        const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
-        T e[kSPT];
-        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e);
-        uint32_t n, sn, st;
-        pack_lane_scan<MODE>(e, lane, n, sn, st);
-        if (lane == 63) a.blk[blk] = ((unsigned long long)st << 32) | sn;
+        uint32_t n = 0;
+        if (blk < full) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
+#pragma unroll
+            for (int q = 0; q < kSPT / 8; ++q) {
+                const uint4 v = p[q];
+                const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) n += l8[len8_index((wd[k >> 1] >> (16 * (k & 1))) & 0xffffu)];
+            }
+        } else {
+            for (int k = 0; k < kSPT; ++k) {
+                const uint64_t i = sym0 + k;
+                if (i < a.nsym) n += l8[len8_index((uint32_t)a.in[2 * i] | ((uint32_t)a.in[2 * i + 1] << 8))];
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) n += shfl_xor_u32(n, m);
+        if (lane == 0) a.blk[blk] = n;
+    }
+}
+
+// Lookup of one symbol (used for the 32 symbols before a block).
+template <int MODE>
+HZ_DEV typename PackEnt<MODE>::T pack_lookup_one(const PackArgs& a, const uint32_t* lds, uint32_t s) {
+    using T = typename PackEnt<MODE>::T;
+    constexpr int SH = PackEnt<MODE>::kShift;
+    if (MODE == ENC_DENSE) {
+        const uint32_t bit = s * 17u;
+        const uint32_t w = bit >> 5;
+        const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
+        const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
+        const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
+        return f ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
+    } else if (MODE == ENC_HOT) {
+        const uint32_t v = lds[hot_slot(s, a.hot_mask)];
+        if ((v >> 30) == (2u | (s >> 15))) return (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu));
+        const uint32_t w = a.esc[s];
+        return (T)(((w >> 26) << SH) | (w & 0x3ffffffu));
+    } else {
+        return (T)a.wide[s];
     }
 }
 
@@ -370,7 +444,25 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
         if (lane == 0) { ex_n = 0; ex_t = 0; }
         const uint64_t bstart = a.blk_start[blk];
         const uint64_t bend = bstart + shfl_u32(sn, 63);
-        const uint32_t ptail = blk ? (uint32_t)(a.blk[blk - 1] >> 32) : a.lead;
+        // The 32 bits before the block: codes of the previous block's last 32
+        // symbols (each code >= 1 bit), combined across lanes 0..31.
+        uint32_t ptail = a.lead;
+        if (blk > 0) {
+            const uint64_t ps = blk * kBlockSyms - 32 + (uint64_t)(lane & 31);
+            const uint32_t s = (uint32_t)a.in[2 * ps] | ((uint32_t)a.in[2 * ps + 1] << 8);
+            const T ent = pack_lookup_one<MODE>(a, lds, s);
+            uint32_t pn = (uint32_t)(ent >> SH);
+            uint32_t pt = (uint32_t)(ent & CMASK);  // low 32 bits of the code
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                const uint32_t on = shfl_up_u32(pn, d), ot = shfl_up_u32(pt, d);
+                if ((lane & 31) >= d) {
+                    pt = pn >= 32 ? pt : ((ot << pn) | pt);
+                    pn += on;
+                }
+            }
+            ptail = shfl_u32(pt, 31);
+        }
         const uint64_t o = bstart + ex_n;
         const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
         uint32_t na = (uint32_t)(o & 31);
@@ -495,6 +587,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     a.in = d_in; a.nsym = nsym; a.nblocks = nblocks;
     a.lds_img = t.d_enc_lds; a.lds_words = t.enc_lds_bytes / 4;
     a.wide = reinterpret_cast<const unsigned long long*>(t.d_enc_wide);
+    a.esc = t.d_enc_esc; a.len8_img = t.d_len8; a.hot_mask = t.hot_mask;
     a.out = d_out; a.out_words = out_words; a.lead = lead;
     a.blk = d_scratch;
     unsigned long long* blk_start = d_scratch + nblocks;
@@ -507,21 +600,25 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     if (wgs > cap) wgs = cap;
     const uint32_t lds = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes;
     static bool attr[3] = {false, false, false};
+    static bool attr_count = false;
+    if (!attr_count) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_pack_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           kLen8LdsBytes);
+        if (e != hipSuccess) return e;
+        attr_count = true;
+    }
     if (!attr[t.enc_mode]) {
-        const void* fc[3] = {(const void*)k_pack_count<ENC_DENSE>, (const void*)k_pack_count<ENC_HOT>,
-                             (const void*)k_pack_count<ENC_WIDE>};
         const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE>, (const void*)k_pack_write<ENC_HOT>,
                              (const void*)k_pack_write<ENC_WIDE>};
-        hipError_t e = hipFuncSetAttribute(fc[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(fw[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipError_t e = hipFuncSetAttribute(fw[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr[t.enc_mode] = true;
     }
-    switch (t.enc_mode) {
-        case ENC_DENSE: hipLaunchKernelGGL(k_pack_count<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a); break;
-        case ENC_HOT: hipLaunchKernelGGL(k_pack_count<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a); break;
-        default: hipLaunchKernelGGL(k_pack_count<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+    {
+        const uint64_t cw = kCountThreads / 64;
+        uint64_t cg = (nblocks + cw - 1) / cw;
+        if (cg > (uint64_t)ncu * 2) cg = (uint64_t)ncu * 2;  // two 64 KiB-LDS workgroups per CU
+        hipLaunchKernelGGL(k_pack_count, dim3(cg), dim3(kCountThreads), kLen8LdsBytes, s, a);
     }
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
                        nblocks, tiles);
@@ -561,7 +658,7 @@ struct DecArgs {
 };
 
 HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) {
-    return w < a.nwords ? bswap32(__builtin_nontemporal_load(a.words + w)) : 0u;
+    return w < a.nwords ? bswap32(a.words[w]) : 0u;
 }
 
 template <int MODE>
@@ -623,7 +720,7 @@ HZ_DEV uint64_t br_window_wide(BitReader& r) {
 // global (deeper-level) lookups and its bit-stream refills are all issued
 // before one wait, and a wave's stall on a long-code lookup is paid once per
 // kDecStreams x 64 symbols instead of once per 64.
-constexpr int kDecStreams = 4;
+constexpr int kDecStreams = 2;
 
 template <int MODE, bool WIDE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
