@@ -235,9 +235,22 @@ template <> struct PackEnt<ENC_WIDE> { using T = uint64_t; static constexpr int 
 
 constexpr int pack_threads(int mode) { return mode == ENC_WIDE ? 512 : kPackThreads; }
 
+template <typename T, int SH>
+HZ_DEV T pack_dense_one(const uint32_t* lds, uint32_t s) {
+    const uint32_t bit = s * 17u;
+    const uint32_t w = bit >> 5;
+    const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
+    const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
+    const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
+    return f ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
+}
+
+// Loads the lane's 32 symbols and looks up their (len, code). `xs` is one more
+// symbol whose entry is returned in `xe` from the same batch (the previous
+// block's tail symbols); all global loads of a block are issued before one wait.
 template <int MODE>
 HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid,
-                             typename PackEnt<MODE>::T (&e)[kSPT]) {
+                             typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
@@ -270,6 +283,7 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
             const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
             e[k] = (k < nvalid && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
         }
+        xe = pack_dense_one<T, SH>(lds, xs);
     } else if (MODE == ENC_HOT) {
         uint32_t miss = 0;
 #pragma unroll
@@ -280,18 +294,17 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
             e[k] = k < nvalid ? (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu)) : (T)0;
             if (!hit && k < nvalid) miss |= 1u << k;
         }
-        if (miss) {
-            // Escapes (slot collisions, codes > 25 bits): all 32 loads issued
-            // before one wait; unneeded ones read entry 0 (one cached line).
-            uint32_t w[kSPT];
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k) {
-                const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                w[k] = a.esc[((miss >> k) & 1u) ? s : 0u];
-            }
+        const uint32_t xv = lds[hot_slot(xs, a.hot_mask)];
+        const bool xmiss = (xv >> 30) != (2u | (xs >> 15));
+        xe = (T)((((xv >> 25) & 31u) << SH) | (xv & 0x1ffffffu));
+        if (miss | (uint32_t)xmiss) {
+            // Escapes (slot collisions, codes > 25 bits). The escape table holds
+            // entries in the register format, so each load lands in its e[k]
+            // directly and the single wait falls at the first use (the scan).
 #pragma unroll
             for (int k = 0; k < kSPT; ++k)
-                if ((miss >> k) & 1u) e[k] = (T)(((w[k] >> 26) << SH) | (w[k] & 0x3ffffffu));
+                if ((miss >> k) & 1u) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
+            if (xmiss) xe = (T)a.esc[xs];
         }
     } else {
 #pragma unroll
@@ -299,6 +312,7 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
             e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
         }
+        xe = (T)a.wide[xs];
     }
 }
 
@@ -402,28 +416,6 @@ __global__ __launch_bounds__(kCountThreads) void k_pack_count(PackArgs a) {
     }
 }
 
-// Lookup of one symbol (used for the 32 symbols before a block).
-template <int MODE>
-HZ_DEV typename PackEnt<MODE>::T pack_lookup_one(const PackArgs& a, const uint32_t* lds, uint32_t s) {
-    using T = typename PackEnt<MODE>::T;
-    constexpr int SH = PackEnt<MODE>::kShift;
-    if (MODE == ENC_DENSE) {
-        const uint32_t bit = s * 17u;
-        const uint32_t w = bit >> 5;
-        const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
-        const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
-        const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
-        return f ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
-    } else if (MODE == ENC_HOT) {
-        const uint32_t v = lds[hot_slot(s, a.hot_mask)];
-        if ((v >> 30) == (2u | (s >> 15))) return (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu));
-        const uint32_t w = a.esc[s];
-        return (T)(((w >> 26) << SH) | (w & 0x3ffffffu));
-    } else {
-        return (T)a.wide[s];
-    }
-}
-
 template <int MODE>
 __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
     using T = typename PackEnt<MODE>::T;
@@ -436,23 +428,24 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
     for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
         const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
         const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
+        // independent loads first: block start, previous block's last 32 symbols
+        const uint64_t bstart = a.blk_start[blk];
+        const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
+        const uint32_t psym = (uint32_t)a.in[2 * ps] | ((uint32_t)a.in[2 * ps + 1] << 8);
         T e[kSPT];
-        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e);
+        T pe;
+        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e, psym, pe);
         uint32_t n, sn, st;
         pack_lane_scan<MODE>(e, lane, n, sn, st);
         uint32_t ex_n = shfl_up_u32(sn, 1), ex_t = shfl_up_u32(st, 1);
         if (lane == 0) { ex_n = 0; ex_t = 0; }
-        const uint64_t bstart = a.blk_start[blk];
         const uint64_t bend = bstart + shfl_u32(sn, 63);
         // The 32 bits before the block: codes of the previous block's last 32
         // symbols (each code >= 1 bit), combined across lanes 0..31.
         uint32_t ptail = a.lead;
         if (blk > 0) {
-            const uint64_t ps = blk * kBlockSyms - 32 + (uint64_t)(lane & 31);
-            const uint32_t s = (uint32_t)a.in[2 * ps] | ((uint32_t)a.in[2 * ps + 1] << 8);
-            const T ent = pack_lookup_one<MODE>(a, lds, s);
-            uint32_t pn = (uint32_t)(ent >> SH);
-            uint32_t pt = (uint32_t)(ent & CMASK);  // low 32 bits of the code
+            uint32_t pn = (uint32_t)(pe >> SH);
+            uint32_t pt = (uint32_t)(pe & CMASK);  // low 32 bits of the code
 #pragma unroll
             for (int d = 1; d < 32; d <<= 1) {
                 const uint32_t on = shfl_up_u32(pn, d), ot = shfl_up_u32(pt, d);
