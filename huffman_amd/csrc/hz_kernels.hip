@@ -708,16 +708,71 @@ HZ_DEV uint64_t br_window_wide(BitReader& r) {
     return r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
 }
 
-// Each lane decodes kDecStreams consecutive decode units interleaved: one
-// symbol of every stream per step, so the step's LDS lookups, its rare
-// global (deeper-level) lookups and its bit-stream refills are all issued
-// before one wait, and a wave's stall on a long-code lookup is paid once per
-// kDecStreams x 64 symbols instead of once per 64.
-constexpr int kDecStreams = 2;
+// One lane decodes one decode unit (512 symbols). Input arrives as whole
+// 64-byte chunks (4 x dwordx4 per lane, the next chunk prefetched while the
+// current one drains), so every compressed byte is fetched from HBM once
+// however many units are in flight; output leaves as 64-byte bursts (32
+// symbols, 4 aligned dwordx4 stores), so output lines are written whole.
+struct ChunkReader {
+    uint64_t win;      // next bits, MSB first
+    uint32_t nb;       // valid bits in win
+    uint32_t qn;       // valid words left in c[] (consumed from c[0])
+    uint32_t c[16];    // current chunk (big-endian words)
+    uint32_t n[16];    // next chunk (in flight)
+    uint64_t next;     // index of the chunk after n
+};
+
+HZ_DEV void chunk_load(const DecArgs& a, uint64_t ci, uint32_t (&d)[16]) {
+    const uint64_t w0 = ci * 16;
+    if (w0 + 16 <= a.nwords) {
+        const uint4* p = reinterpret_cast<const uint4*>(a.words + w0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = p[k];
+            d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = w0 + k < a.nwords ? a.words[w0 + k] : 0u;
+    }
+}
+
+HZ_DEV void chunk_shift(ChunkReader& r) {
+#pragma unroll
+    for (int k = 0; k < 15; ++k) r.c[k] = r.c[k + 1];
+}
+
+// Pull the next 32-bit word of the stream out of the chunk queue.
+HZ_DEV uint32_t chunk_pop(ChunkReader& r, const DecArgs& a) {
+    if (r.qn == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r.c[k] = r.n[k];
+        r.qn = 16;
+        chunk_load(a, r.next++, r.n);
+    }
+    const uint32_t w = bswap32(r.c[0]);
+    chunk_shift(r);
+    r.qn--;
+    return w;
+}
+
+HZ_DEV void chunk_init(ChunkReader& r, const DecArgs& a, uint64_t p) {
+    const uint64_t ci = p >> 9;
+    chunk_load(a, ci, r.c);
+    chunk_load(a, ci + 1, r.n);
+    r.next = ci + 2;
+    r.qn = 16;
+    const uint32_t skip = (uint32_t)((p >> 5) & 15);
+    for (uint32_t k = 0; k < skip; ++k) { chunk_shift(r); r.qn--; }
+    const uint32_t sh = (uint32_t)(p & 31);
+    const uint32_t w0 = chunk_pop(r, a);
+    const uint32_t w1 = chunk_pop(r, a);
+    r.win = ((((uint64_t)w0) << 32) | w1) << sh;
+    r.nb = 64 - sh;
+}
 
 template <int MODE, bool WIDE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
-    constexpr int S = kDecStreams;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
@@ -725,93 +780,48 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
         for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
-    const uint64_t nlanes = (a.ndu + S - 1) / S;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t ln = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; ln < nlanes; ln += stride) {
-        BitReader r[S];
-        uint32_t cnt[S];
+    for (uint64_t du = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; du < a.ndu; du += stride) {
+        const uint64_t s0 = du * kDUSyms;
+        const uint32_t cnt = a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0);
+        ChunkReader r;
+        chunk_init(r, a, a.index[du] + a.bit_adj);
+        uint4* o = reinterpret_cast<uint4*>(a.out + 2 * s0);
+        for (uint32_t g = 0; g < cnt; g += 32) {
+            uint32_t pk[16];
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const uint64_t du = ln * S + s;
-            const uint64_t s0 = du * kDUSyms;
-            cnt[s] = du >= a.ndu ? 0u : (a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0));
-            br_init(r[s], a, (du < a.ndu ? a.index[du] : 0ull) + a.bit_adj);
-        }
-        uint8_t* o = a.out + 2 * (ln * S * kDUSyms);
-        for (uint32_t i = 0; i < (uint32_t)kDUSyms; i += 8) {
-            uint32_t pk[S][4];
+            for (int q = 0; q < 16; ++q) pk[q] = 0;
 #pragma unroll
-            for (int s = 0; s < S; ++s) pk[s][0] = pk[s][1] = pk[s][2] = pk[s][3] = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                uint32_t e[S];
-                uint64_t win[S];
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (r[s].nb <= 32) {
-                        r[s].buf |= (uint64_t)r[s].nxt << (32 - r[s].nb);
-                        r[s].nb += 32;
-                        r[s].nxt = ld_word(a, r[s].wpos++);
-                    }
-                    win[s] = WIDE ? br_window_wide(r[s]) : r[s].buf;
+            for (int q = 0; q < 32; ++q) {
+                if (r.nb <= 32) {
+                    r.win |= (uint64_t)chunk_pop(r, a) << (32 - r.nb);
+                    r.nb += 32;
                 }
-                uint32_t sym[S], L[S];
-                if (MODE == DEC_DENSE) {
-#pragma unroll
-                    for (int s = 0; s < S; ++s) dec_lookup<MODE>(a, lds, win[s], sym[s], L[s]);
+                uint64_t win = r.win;
+                if (WIDE && r.nb < 56) win |= (uint64_t)bswap32(r.qn ? r.c[0] : r.n[0]) >> (r.nb - 32);
+                uint32_t sym, L;
+                dec_lookup<MODE>(a, lds, win, sym, L);
+                if (!WIDE || L < r.nb) {
+                    r.win <<= L;
+                    r.nb -= L;
                 } else {
-#pragma unroll
-                    for (int s = 0; s < S; ++s) e[s] = lds[(uint32_t)(win[s] >> (64 - a.k))];
-                    // first deeper level for every stream that needs it, all issued before the wait
-                    uint32_t e2[S];
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        e2[s] = e[s];
-                        if (!(e[s] >> 31)) {
-                            const uint32_t nb = (e[s] >> 26) & 31u;
-                            e2[s] = a.l2[(e[s] & 0x3ffffffu) + (uint32_t)((win[s] << a.k) >> (64 - nb))];
-                        }
-                    }
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        uint32_t ee = e2[s];
-                        if (!(e[s] >> 31)) {
-                            uint32_t D = (uint32_t)a.k + ((e[s] >> 26) & 31u);
-                            while (!(ee >> 31)) {  // codes deeper than k + 8 bits: rare
-                                const uint32_t nb = (ee >> 26) & 31u;
-                                ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[s] << D) >> (64 - nb))];
-                                D += nb;
-                            }
-                        }
-                        L[s] = (ee >> 16) & 63u;
-                        sym[s] = ee & 0xffffu;
-                    }
+                    const uint32_t rr = L - r.nb;  // bits taken from the next word
+                    const uint32_t w = chunk_pop(r, a);
+                    r.win = (uint64_t)w << (32 + rr);
+                    r.nb = 32 - rr;
                 }
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (!WIDE || L[s] < r[s].nb) {
-                        r[s].buf <<= L[s];
-                        r[s].nb -= L[s];
-                    } else {
-                        const uint32_t rr = L[s] - r[s].nb;  // bits taken from nxt
-                        r[s].buf = (uint64_t)r[s].nxt << (32 + rr);
-                        r[s].nb = 32 - rr;
-                        r[s].nxt = ld_word(a, r[s].wpos++);
-                    }
-                    pk[s][q >> 1] |= sym[s] << (16 * (q & 1));
-                }
+                pk[q >> 1] |= sym << (16 * (q & 1));
             }
+            if (g + 32 <= cnt) {
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                uint8_t* os = o + 2 * (s * kDUSyms + i);
-                if (i + 8 <= cnt[s]) {
-                    *reinterpret_cast<uint4*>(os) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
-                } else if (i < cnt[s]) {
-                    for (uint32_t q = 0; q < cnt[s] - i; ++q) {
-                        const uint32_t v = (pk[s][q >> 1] >> (16 * (q & 1))) & 0xffffu;
-                        os[2 * q] = (uint8_t)v;
-                        os[2 * q + 1] = (uint8_t)(v >> 8);
-                    }
+                for (int k = 0; k < 4; ++k)
+                    o[g / 8 + k] = make_uint4(pk[4 * k], pk[4 * k + 1], pk[4 * k + 2], pk[4 * k + 3]);
+            } else {
+                uint8_t* ob = a.out + 2 * (s0 + g);
+                for (uint32_t q = 0; q < cnt - g; ++q) {
+                    const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                    ob[2 * q] = (uint8_t)v;
+                    ob[2 * q + 1] = (uint8_t)(v >> 8);
                 }
             }
         }
@@ -820,10 +830,14 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
 
 static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                           uint64_t nsym) {
-    const uintptr_t base = (uintptr_t)d_payload & ~(uintptr_t)3;
+    // Chunk reads are 64-byte aligned: view the payload from the 64-byte
+    // boundary at or below it (inside the same allocation: device allocations
+    // are 256-byte aligned). The last word may extend up to 3 bytes past
+    // payload_bytes (include/huffman_amd.h: hz_decode).
+    const uintptr_t base = (uintptr_t)d_payload & ~(uintptr_t)63;
     a.words = reinterpret_cast<const uint32_t*>(base);
-    a.bit_adj = (uint32_t)(((uintptr_t)d_payload & 3) * 8);
-    a.nwords = (payload_bytes + ((uintptr_t)d_payload & 3) + 3) / 4;
+    a.bit_adj = (uint32_t)(((uintptr_t)d_payload & 63) * 8);
+    a.nwords = (payload_bytes + ((uintptr_t)d_payload & 63) + 3) / 4;
     a.nsym = nsym;
     a.ndu = (nsym + kDUSyms - 1) / kDUSyms;
     a.lds_img = t.d_dec_lds;
@@ -851,7 +865,7 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
         if (e != hipSuccess) return e;
         attr[variant] = true;
     }
-    uint64_t wgs = ((a.ndu + kDecStreams - 1) / kDecStreams + 1023) / 1024;
+    uint64_t wgs = (a.ndu + 1023) / 1024;
     const uint64_t cap = (uint64_t)ncu * 4;
     if (wgs > cap) wgs = cap;
     const uint32_t lds = t.dec_lds_bytes;

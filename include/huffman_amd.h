@@ -126,9 +126,10 @@ int hz_pack(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t start_bit, ui
             uint8_t *d_out, uint64_t out_cap, uint64_t *d_index);
 
 /* Decode nsym symbols from d_payload (bit stream as hz_pack writes it) into
- * d_out (2*nsym bytes). d_index: start bit of every decode unit (from hz_pack,
- * or hz_index_build for an index-less stream). Replaces translateFile
- * (Decompressor.cu:259-291). */
+ * d_out (2*nsym bytes, 16-byte aligned). d_index: start bit of every decode
+ * unit (from hz_pack, or hz_index_build for an index-less stream). d_payload
+ * must stay readable up to the next 4-byte boundary after payload_bytes.
+ * Replaces translateFile (Decompressor.cu:259-291). */
 int hz_decode(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t nsym,
               const uint64_t *d_index, uint8_t *d_out);
 
