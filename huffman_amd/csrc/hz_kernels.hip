@@ -7,6 +7,8 @@
 //   k_generate synthetic Zipf / uniform byte streams (this build's generator)
 //
 // Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
+#include <stdlib.h>
+
 #include "hz_internal.h"
 
 namespace hz {
@@ -708,70 +710,75 @@ HZ_DEV uint64_t br_window_wide(BitReader& r) {
     return r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
 }
 
-// One lane decodes one decode unit (512 symbols). Input arrives as whole
-// 64-byte chunks (4 x dwordx4 per lane, the next chunk prefetched while the
-// current one drains), so every compressed byte is fetched from HBM once
-// however many units are in flight; output leaves as 64-byte bursts (32
-// symbols, 4 aligned dwordx4 stores), so output lines are written whole.
+// One lane decodes S decode units (512 symbols each) interleaved: one symbol of
+// every unit per step, so a wave's stall on a long-code lookup in global
+// memory is paid once per 64*S symbols. Input arrives as whole CHW-word chunks
+// (the next chunk prefetched while the current one drains); output leaves in
+// OB-symbol bursts of aligned 16-byte stores.
+template <int CHW>
 struct ChunkReader {
     uint64_t win;      // next bits, MSB first
     uint32_t nb;       // valid bits in win
     uint32_t qn;       // valid words left in c[] (consumed from c[0])
-    uint32_t c[16];    // current chunk (big-endian words)
-    uint32_t n[16];    // next chunk (in flight)
+    uint32_t c[CHW];   // current chunk (big-endian words)
+    uint32_t n[CHW];   // next chunk (in flight)
     uint64_t next;     // index of the chunk after n
 };
 
-HZ_DEV void chunk_load(const DecArgs& a, uint64_t ci, uint32_t (&d)[16]) {
-    const uint64_t w0 = ci * 16;
-    if (w0 + 16 <= a.nwords) {
+template <int CHW>
+HZ_DEV void chunk_load(const DecArgs& a, uint64_t ci, uint32_t (&d)[CHW]) {
+    const uint64_t w0 = ci * CHW;
+    if (w0 + CHW <= a.nwords) {
         const uint4* p = reinterpret_cast<const uint4*>(a.words + w0);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < CHW / 4; ++k) {
             const uint4 v = p[k];
             d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = w0 + k < a.nwords ? a.words[w0 + k] : 0u;
+        for (int k = 0; k < CHW; ++k) d[k] = w0 + k < a.nwords ? a.words[w0 + k] : 0u;
     }
 }
 
-HZ_DEV void chunk_shift(ChunkReader& r) {
+template <int CHW>
+HZ_DEV void chunk_shift(ChunkReader<CHW>& r) {
 #pragma unroll
-    for (int k = 0; k < 15; ++k) r.c[k] = r.c[k + 1];
+    for (int k = 0; k < CHW - 1; ++k) r.c[k] = r.c[k + 1];
 }
 
-// Pull the next 32-bit word of the stream out of the chunk queue.
-HZ_DEV uint32_t chunk_pop(ChunkReader& r, const DecArgs& a) {
+template <int CHW>
+HZ_DEV uint32_t chunk_pop(ChunkReader<CHW>& r, const DecArgs& a) {
     if (r.qn == 0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) r.c[k] = r.n[k];
-        r.qn = 16;
-        chunk_load(a, r.next++, r.n);
+        for (int k = 0; k < CHW; ++k) r.c[k] = r.n[k];
+        r.qn = CHW;
+        chunk_load<CHW>(a, r.next++, r.n);
     }
     const uint32_t w = bswap32(r.c[0]);
-    chunk_shift(r);
+    chunk_shift<CHW>(r);
     r.qn--;
     return w;
 }
 
-HZ_DEV void chunk_init(ChunkReader& r, const DecArgs& a, uint64_t p) {
-    const uint64_t ci = p >> 9;
-    chunk_load(a, ci, r.c);
-    chunk_load(a, ci + 1, r.n);
+template <int CHW>
+HZ_DEV void chunk_init(ChunkReader<CHW>& r, const DecArgs& a, uint64_t p) {
+    constexpr int CB = CHW * 32;  // bits per chunk
+    const uint64_t ci = p / CB;
+    chunk_load<CHW>(a, ci, r.c);
+    chunk_load<CHW>(a, ci + 1, r.n);
     r.next = ci + 2;
-    r.qn = 16;
-    const uint32_t skip = (uint32_t)((p >> 5) & 15);
-    for (uint32_t k = 0; k < skip; ++k) { chunk_shift(r); r.qn--; }
+    r.qn = CHW;
+    const uint32_t skip = (uint32_t)((p % CB) >> 5);
+    for (uint32_t k = 0; k < skip; ++k) { chunk_shift<CHW>(r); r.qn--; }
     const uint32_t sh = (uint32_t)(p & 31);
-    const uint32_t w0 = chunk_pop(r, a);
-    const uint32_t w1 = chunk_pop(r, a);
+    const uint32_t w0 = chunk_pop<CHW>(r, a);
+    const uint32_t w1 = chunk_pop<CHW>(r, a);
     r.win = ((((uint64_t)w0) << 32) | w1) << sh;
     r.nb = 64 - sh;
 }
 
-template <int MODE, bool WIDE>
+template <int MODE, bool WIDE, int S, int CHW, int OB>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     {
@@ -780,48 +787,98 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
         for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
+    const uint64_t nlanes = (a.ndu + S - 1) / S;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t du = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; du < a.ndu; du += stride) {
-        const uint64_t s0 = du * kDUSyms;
-        const uint32_t cnt = a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0);
-        ChunkReader r;
-        chunk_init(r, a, a.index[du] + a.bit_adj);
-        uint4* o = reinterpret_cast<uint4*>(a.out + 2 * s0);
-        for (uint32_t g = 0; g < cnt; g += 32) {
-            uint32_t pk[16];
+    for (uint64_t ln = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; ln < nlanes; ln += stride) {
+        ChunkReader<CHW> r[S];
+        uint32_t cnt[S];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) pk[q] = 0;
+        for (int s = 0; s < S; ++s) {
+            const uint64_t du = ln * S + s;
+            const uint64_t s0 = du * kDUSyms;
+            cnt[s] = du >= a.ndu ? 0u : (a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0));
+            chunk_init<CHW>(r[s], a, (du < a.ndu ? a.index[du] : 0ull) + a.bit_adj);
+        }
+        const uint32_t cmax = cnt[0];
+        for (uint32_t g = 0; g < cmax; g += OB) {
+            uint32_t pk[S][OB / 2];
 #pragma unroll
-            for (int q = 0; q < 32; ++q) {
-                if (r.nb <= 32) {
-                    r.win |= (uint64_t)chunk_pop(r, a) << (32 - r.nb);
-                    r.nb += 32;
+            for (int s = 0; s < S; ++s)
+#pragma unroll
+                for (int q = 0; q < OB / 2; ++q) pk[s][q] = 0;
+#pragma unroll
+            for (int q = 0; q < OB; ++q) {
+                uint64_t win[S];
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if (r[s].nb <= 32) {
+                        r[s].win |= (uint64_t)chunk_pop<CHW>(r[s], a) << (32 - r[s].nb);
+                        r[s].nb += 32;
+                    }
+                    win[s] = r[s].win;
+                    if (WIDE && r[s].nb < 56)
+                        win[s] |= (uint64_t)bswap32(r[s].qn ? r[s].c[0] : r[s].n[0]) >> (r[s].nb - 32);
                 }
-                uint64_t win = r.win;
-                if (WIDE && r.nb < 56) win |= (uint64_t)bswap32(r.qn ? r.c[0] : r.n[0]) >> (r.nb - 32);
-                uint32_t sym, L;
-                dec_lookup<MODE>(a, lds, win, sym, L);
-                if (!WIDE || L < r.nb) {
-                    r.win <<= L;
-                    r.nb -= L;
+                uint32_t sym[S], L[S];
+                if (MODE == DEC_DENSE) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) dec_lookup<MODE>(a, lds, win[s], sym[s], L[s]);
                 } else {
-                    const uint32_t rr = L - r.nb;  // bits taken from the next word
-                    const uint32_t w = chunk_pop(r, a);
-                    r.win = (uint64_t)w << (32 + rr);
-                    r.nb = 32 - rr;
-                }
-                pk[q >> 1] |= sym << (16 * (q & 1));
-            }
-            if (g + 32 <= cnt) {
+                    uint32_t e[S], e2[S];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    o[g / 8 + k] = make_uint4(pk[4 * k], pk[4 * k + 1], pk[4 * k + 2], pk[4 * k + 3]);
-            } else {
-                uint8_t* ob = a.out + 2 * (s0 + g);
-                for (uint32_t q = 0; q < cnt - g; ++q) {
-                    const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-                    ob[2 * q] = (uint8_t)v;
-                    ob[2 * q + 1] = (uint8_t)(v >> 8);
+                    for (int s = 0; s < S; ++s) e[s] = lds[(uint32_t)(win[s] >> (64 - a.k))];
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {  // first deeper level: all issued before the wait
+                        e2[s] = e[s];
+                        if (!(e[s] >> 31)) {
+                            const uint32_t nb = (e[s] >> 26) & 31u;
+                            e2[s] = a.l2[(e[s] & 0x3ffffffu) + (uint32_t)((win[s] << a.k) >> (64 - nb))];
+                        }
+                    }
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        uint32_t ee = e2[s];
+                        if (!(e[s] >> 31)) {
+                            uint32_t D = (uint32_t)a.k + ((e[s] >> 26) & 31u);
+                            while (!(ee >> 31)) {  // deeper than k + 8 bits: rare
+                                const uint32_t nb = (ee >> 26) & 31u;
+                                ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[s] << D) >> (64 - nb))];
+                                D += nb;
+                            }
+                        }
+                        L[s] = (ee >> 16) & 63u;
+                        sym[s] = ee & 0xffffu;
+                    }
+                }
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if (!WIDE || L[s] < r[s].nb) {
+                        r[s].win <<= L[s];
+                        r[s].nb -= L[s];
+                    } else {
+                        const uint32_t rr = L[s] - r[s].nb;  // bits taken from the next word
+                        const uint32_t w = chunk_pop<CHW>(r[s], a);
+                        r[s].win = (uint64_t)w << (32 + rr);
+                        r[s].nb = 32 - rr;
+                    }
+                    pk[s][q >> 1] |= sym[s] << (16 * (q & 1));
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const uint64_t s0 = (ln * S + s) * kDUSyms;
+                if (g + OB <= cnt[s]) {
+                    uint4* o = reinterpret_cast<uint4*>(a.out + 2 * (s0 + g));
+#pragma unroll
+                    for (int k = 0; k < OB / 8; ++k)
+                        o[k] = make_uint4(pk[s][4 * k], pk[s][4 * k + 1], pk[s][4 * k + 2], pk[s][4 * k + 3]);
+                } else if (g < cnt[s]) {
+                    uint8_t* ob = a.out + 2 * (s0 + g);
+                    for (uint32_t q = 0; q < cnt[s] - g; ++q) {
+                        const uint32_t v = (pk[s][q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                        ob[2 * q] = (uint8_t)v;
+                        ob[2 * q + 1] = (uint8_t)(v >> 8);
+                    }
                 }
             }
         }
@@ -848,6 +905,36 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
     a.l2 = t.d_dec_l2;
 }
 
+// Decode variants (S streams per lane, CHW-word chunks, OB-symbol bursts),
+// selectable with HZ_DEC_VARIANT for A/B measurements; DESIGN.md records why
+// the default was chosen.
+template <int MODE, bool WIDE, int S, int CHW, int OB>
+static hipError_t run_decode(const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, S, CHW, OB>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const uint64_t nlanes = (a.ndu + S - 1) / S;
+    uint64_t wgs = (nlanes + 1023) / 1024;
+    const uint64_t cap = (uint64_t)ncu * 4;
+    if (wgs > cap) wgs = cap;
+    hipLaunchKernelGGL((k_decode<MODE, WIDE, S, CHW, OB>), dim3(wgs), dim3(1024), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int MODE, bool WIDE>
+static hipError_t run_decode_variant(int v, const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
+    switch (v) {
+        case 1: return run_decode<MODE, WIDE, 1, 16, 32>(a, lds, ncu, s);
+        case 2: return run_decode<MODE, WIDE, 2, 8, 16>(a, lds, ncu, s);
+        case 3: return run_decode<MODE, WIDE, 1, 8, 16>(a, lds, ncu, s);
+        default: return run_decode<MODE, WIDE, 2, 8, 16>(a, lds, ncu, s);
+    }
+}
+
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
                          const unsigned long long* d_index, uint8_t* d_out, uint32_t* d_err, int ncu,
                          hipStream_t s) {
@@ -855,27 +942,18 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.index = d_index; a.out = d_out; a.err = d_err;
+    static int variant = -1;
+    if (variant < 0) {
+        const char* ev = getenv("HZ_DEC_VARIANT");
+        variant = ev ? atoi(ev) : 0;
+    }
     const bool wide = t.max_len > 32;
-    const int variant = (t.dec_mode == DEC_DENSE ? 0 : 2) + (wide ? 1 : 0);
-    const void* fns[4] = {(const void*)k_decode<DEC_DENSE, false>, (const void*)k_decode<DEC_DENSE, true>,
-                          (const void*)k_decode<DEC_LUT, false>, (const void*)k_decode<DEC_LUT, true>};
-    static bool attr[4] = {false, false, false, false};
-    if (!attr[variant]) {
-        hipError_t e = hipFuncSetAttribute(fns[variant], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr[variant] = true;
-    }
-    uint64_t wgs = (a.ndu + 1023) / 1024;
-    const uint64_t cap = (uint64_t)ncu * 4;
-    if (wgs > cap) wgs = cap;
     const uint32_t lds = t.dec_lds_bytes;
-    switch (variant) {
-        case 0: hipLaunchKernelGGL((k_decode<DEC_DENSE, false>), dim3(wgs), dim3(1024), lds, s, a); break;
-        case 1: hipLaunchKernelGGL((k_decode<DEC_DENSE, true>), dim3(wgs), dim3(1024), lds, s, a); break;
-        case 2: hipLaunchKernelGGL((k_decode<DEC_LUT, false>), dim3(wgs), dim3(1024), lds, s, a); break;
-        default: hipLaunchKernelGGL((k_decode<DEC_LUT, true>), dim3(wgs), dim3(1024), lds, s, a); break;
-    }
-    return hipGetLastError();
+    if (t.dec_mode == DEC_DENSE)
+        return wide ? run_decode_variant<DEC_DENSE, true>(variant, a, lds, ncu, s)
+                    : run_decode_variant<DEC_DENSE, false>(variant, a, lds, ncu, s);
+    return wide ? run_decode_variant<DEC_LUT, true>(variant, a, lds, ncu, s)
+                : run_decode_variant<DEC_LUT, false>(variant, a, lds, ncu, s);
 }
 
 // Serial index build for an index-less stream: one lane walks the stream and
