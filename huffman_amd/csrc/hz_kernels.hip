@@ -723,6 +723,7 @@ struct ChunkReader {
     uint32_t c[CHW];   // current chunk (big-endian words)
     uint32_t n[CHW];   // next chunk (in flight)
     uint64_t next;     // index of the chunk after n
+    bool n_ok;         // n holds (or is loading) chunk next-1
 };
 
 template <int CHW>
@@ -747,13 +748,19 @@ HZ_DEV void chunk_shift(ChunkReader<CHW>& r) {
     for (int k = 0; k < CHW - 1; ++k) r.c[k] = r.c[k + 1];
 }
 
-template <int CHW>
+// GP (group prefetch): the next chunk is requested only at output-group
+// boundaries, so every lane's prefetch of a group is issued in the same step
+// and the wave's in-order vmcnt waits expose HBM latency once per group, not
+// on every step that a long-code lookup waits on (DESIGN.md "Decode").
+template <int CHW, bool GP = false>
 HZ_DEV uint32_t chunk_pop(ChunkReader<CHW>& r, const DecArgs& a) {
     if (r.qn == 0) {
+        if (!r.n_ok) chunk_load<CHW>(a, r.next++, r.n);  // GP fallback: group consumed > 1 chunk
 #pragma unroll
         for (int k = 0; k < CHW; ++k) r.c[k] = r.n[k];
         r.qn = CHW;
-        chunk_load<CHW>(a, r.next++, r.n);
+        if (GP) r.n_ok = false;
+        else chunk_load<CHW>(a, r.next++, r.n);
     }
     const uint32_t w = bswap32(r.c[0]);
     chunk_shift<CHW>(r);
@@ -769,6 +776,7 @@ HZ_DEV void chunk_init(ChunkReader<CHW>& r, const DecArgs& a, uint64_t p) {
     chunk_load<CHW>(a, ci + 1, r.n);
     r.next = ci + 2;
     r.qn = CHW;
+    r.n_ok = true;
     const uint32_t skip = (uint32_t)((p % CB) >> 5);
     for (uint32_t k = 0; k < skip; ++k) { chunk_shift<CHW>(r); r.qn--; }
     const uint32_t sh = (uint32_t)(p & 31);
@@ -778,7 +786,7 @@ HZ_DEV void chunk_init(ChunkReader<CHW>& r, const DecArgs& a, uint64_t p) {
     r.nb = 64 - sh;
 }
 
-template <int MODE, bool WIDE, int S, int CHW, int OB>
+template <int MODE, bool WIDE, int S, int CHW, int OB, bool GP>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     {
@@ -801,6 +809,11 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
         }
         const uint32_t cmax = cnt[0];
         for (uint32_t g = 0; g < cmax; g += OB) {
+            if (GP) {
+#pragma unroll
+                for (int s = 0; s < S; ++s)
+                    if (!r[s].n_ok) { chunk_load<CHW>(a, r[s].next++, r[s].n); r[s].n_ok = true; }
+            }
             uint32_t pk[S][OB / 2];
 #pragma unroll
             for (int s = 0; s < S; ++s)
@@ -812,12 +825,17 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     if (r[s].nb <= 32) {
-                        r[s].win |= (uint64_t)chunk_pop<CHW>(r[s], a) << (32 - r[s].nb);
+                        r[s].win |= (uint64_t)chunk_pop<CHW, GP>(r[s], a) << (32 - r[s].nb);
                         r[s].nb += 32;
                     }
                     win[s] = r[s].win;
-                    if (WIDE && r[s].nb < 56)
+                    if (WIDE && r[s].nb < 56) {
+                        if (GP && !r[s].qn && !r[s].n_ok) {
+                            chunk_load<CHW>(a, r[s].next++, r[s].n);
+                            r[s].n_ok = true;
+                        }
                         win[s] |= (uint64_t)bswap32(r[s].qn ? r[s].c[0] : r[s].n[0]) >> (r[s].nb - 32);
+                    }
                 }
                 uint32_t sym[S], L[S];
                 if (MODE == DEC_DENSE) {
@@ -857,7 +875,7 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
                         r[s].nb -= L[s];
                     } else {
                         const uint32_t rr = L[s] - r[s].nb;  // bits taken from the next word
-                        const uint32_t w = chunk_pop<CHW>(r[s], a);
+                        const uint32_t w = chunk_pop<CHW, GP>(r[s], a);
                         r[s].win = (uint64_t)w << (32 + rr);
                         r[s].nb = 32 - rr;
                     }
@@ -908,11 +926,11 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
 // Decode variants (S streams per lane, CHW-word chunks, OB-symbol bursts),
 // selectable with HZ_DEC_VARIANT for A/B measurements; DESIGN.md records why
 // the default was chosen.
-template <int MODE, bool WIDE, int S, int CHW, int OB>
+template <int MODE, bool WIDE, int S, int CHW, int OB, bool GP>
 static hipError_t run_decode(const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, S, CHW, OB>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, S, CHW, OB, GP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
@@ -921,17 +939,20 @@ static hipError_t run_decode(const DecArgs& a, uint32_t lds, int ncu, hipStream_
     uint64_t wgs = (nlanes + 1023) / 1024;
     const uint64_t cap = (uint64_t)ncu * 4;
     if (wgs > cap) wgs = cap;
-    hipLaunchKernelGGL((k_decode<MODE, WIDE, S, CHW, OB>), dim3(wgs), dim3(1024), lds, s, a);
+    hipLaunchKernelGGL((k_decode<MODE, WIDE, S, CHW, OB, GP>), dim3(wgs), dim3(1024), lds, s, a);
     return hipGetLastError();
 }
 
 template <int MODE, bool WIDE>
 static hipError_t run_decode_variant(int v, const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
     switch (v) {
-        case 1: return run_decode<MODE, WIDE, 1, 16, 32>(a, lds, ncu, s);
-        case 2: return run_decode<MODE, WIDE, 2, 8, 16>(a, lds, ncu, s);
-        case 3: return run_decode<MODE, WIDE, 1, 8, 16>(a, lds, ncu, s);
-        default: return run_decode<MODE, WIDE, 2, 8, 16>(a, lds, ncu, s);
+        case 1: return run_decode<MODE, WIDE, 1, 16, 32, false>(a, lds, ncu, s);
+        case 2: return run_decode<MODE, WIDE, 2, 8, 16, false>(a, lds, ncu, s);
+        case 3: return run_decode<MODE, WIDE, 1, 8, 16, false>(a, lds, ncu, s);
+        case 4: return run_decode<MODE, WIDE, 1, 16, 16, true>(a, lds, ncu, s);
+        case 5: return run_decode<MODE, WIDE, 1, 8, 8, true>(a, lds, ncu, s);
+        case 6: return run_decode<MODE, WIDE, 1, 16, 32, true>(a, lds, ncu, s);
+        default: return run_decode<MODE, WIDE, 1, 16, 16, true>(a, lds, ncu, s);
     }
 }
 
