@@ -70,6 +70,8 @@ PROTOTYPES = [
                              ctypes.POINTER(_U32), ctypes.POINTER(ctypes.c_uint8)]),
     ("hz_header_parse", _I, [_P, _U64, ctypes.POINTER(Codebook), ctypes.POINTER(HeaderInfo)]),
     ("hz_codebook_upload", _I, [_P, ctypes.POINTER(Codebook)]),
+    ("hz_codebook_upload_encode", _I, [_P, ctypes.POINTER(Codebook)]),
+    ("hz_codebook_upload_decode", _I, [_P, ctypes.POINTER(Codebook)]),
     ("hz_index_stride", _U64, []),
     ("hz_index_entries", _U64, [_U64]),
     ("hz_scratch_bytes", _U64, [_U64]),

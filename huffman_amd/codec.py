@@ -149,6 +149,12 @@ class Device:
     def upload(self, cb):
         check(self.lib.hz_codebook_upload(self.h, ctypes.byref(cb)), "hz_codebook_upload")
 
+    def upload_encode(self, cb):
+        check(self.lib.hz_codebook_upload_encode(self.h, ctypes.byref(cb)), "hz_codebook_upload_encode")
+
+    def upload_decode(self, cb):
+        check(self.lib.hz_codebook_upload_decode(self.h, ctypes.byref(cb)), "hz_codebook_upload_decode")
+
     def pack(self, d_in, n, start_bit, lead, d_out, out_cap, d_index=None):
         check(self.lib.hz_pack(self.h, d_in, n, start_bit, lead, d_out, out_cap, d_index), "hz_pack")
 

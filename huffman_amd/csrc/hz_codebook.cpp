@@ -260,19 +260,20 @@ std::vector<uint32_t> build_enc_dense(const hz_codebook* cb) {
 uint32_t choose_hot_mask(const hz_codebook* cb) {
     static const uint32_t cand[] = {0x8000, 0xffff, 0x8080, 0xc0c0, 0x80ff, 0xff80, 0xa0a0, 0xf0f0,
                                     0x8888, 0xcccc, 0xaaaa, 0x8001, 0xff00, 0x80c0, 0xe0e0, 0x9999};
+    // weight 2^-L in fixed point (2^-56 units); ineligible (absent or > 25 bits)
+    // symbols escape whatever the pairing, so they do not rank the masks
+    static thread_local std::vector<uint64_t> w(HZ_NSYM);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const uint32_t L = cb->len[s];
+        w[s] = (L && L <= (uint32_t)kHotMaxLen) ? (1ull << (HZ_MAXLEN - L)) : 0ull;
+    }
     uint32_t best = 0x8000;
-    double best_miss = 1e300;
+    uint64_t best_miss = ~0ull;
     for (uint32_t m : cand) {
-        double miss = 0.0;
+        uint64_t miss = 0;
         for (uint32_t s = 0; s < 32768; ++s) {
-            const uint32_t t = s ^ (m & 0x7fffu) ^ 0x8000u;  // the partner with bit 15 set
-            const uint32_t a = cb->len[s], b = cb->len[t];
-            const double wa = a ? ldexp(1.0, -(int)a) : 0.0, wb = b ? ldexp(1.0, -(int)b) : 0.0;
-            const bool a_ok = a && a <= (uint32_t)kHotMaxLen, b_ok = b && b <= (uint32_t)kHotMaxLen;
-            // the slot keeps the better eligible one; everything else escapes
-            if (a_ok && (!b_ok || a <= b)) miss += wb;
-            else if (b_ok) miss += wa;
-            else miss += wa + wb;
+            const uint64_t wa = w[s], wb = w[s ^ m];  // s ^ m: the partner with bit 15 set
+            miss += wa < wb ? wa : wb;                // the slot keeps the heavier one
         }
         if (miss < best_miss) { best_miss = miss; best = m; }
     }
@@ -348,61 +349,77 @@ int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K) {
 }
 
 namespace {
-struct CodeRec { uint64_t code; uint32_t len; uint32_t sym; };
-
 constexpr uint32_t kLeafBit = 1u << 31;
 inline uint32_t leaf(uint32_t L, uint32_t sym) { return kLeafBit | (L << 16) | sym; }
+}  // namespace
 
-// Fill a table of 2^nb entries for codes whose first D bits are consumed.
-int fill_level(std::vector<uint32_t>& tab, size_t base, int nb, int D, const std::vector<CodeRec>& recs,
-               std::vector<uint32_t>& l2) {
-    // group codes longer than D + nb by their next nb bits
-    std::vector<std::vector<CodeRec>> deeper;
-    std::vector<int> deeper_idx(1u << nb, -1);
-    for (const CodeRec& c : recs) {
-        const uint32_t rem = c.len - D;  // bits after the consumed prefix
-        const uint64_t r = c.code & ((rem >= 64) ? ~0ull : ((1ull << rem) - 1));
-        if ((int)rem <= nb) {
-            const uint64_t lo = r << (nb - rem), hi = (r + 1) << (nb - rem);
-            for (uint64_t i = lo; i < hi; ++i) {
-                if (tab[base + i]) return HZ_EFORMAT;
-                tab[base + i] = leaf(c.len, c.sym);
+// Fill one table level. `syms` are the symbols whose codes pass through this
+// table: their first D bits are consumed, the table is (1 << nb) entries at
+// tab[base...]. Codes ending within nb bits fill their ranges with leaves;
+// longer ones are grouped by their next nb bits (counting sort) and each
+// group gets a subtable of its own, appended to l2, at most kDecLevelBits wide.
+static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t base, uint32_t nb, uint32_t D,
+                      const uint32_t* syms, size_t nsyms, std::vector<uint32_t>& l2) {
+    const uint32_t E = 1u << nb;
+    std::vector<uint32_t> cnt(E + 1, 0u), maxd(E, 0u);
+    size_t ndeep = 0;
+    for (size_t i = 0; i < nsyms; ++i) {
+        const uint32_t s = syms[i];
+        const uint32_t rem = cb->len[s] - D;
+        const uint64_t bits = cb->code[s] & ((1ull << rem) - 1);
+        if (rem <= nb) {
+            const uint64_t lo = bits << (nb - rem), hi = (bits + 1) << (nb - rem);
+            uint32_t* t = tab.data() + base;
+            for (uint64_t k = lo; k < hi; ++k) {
+                if (t[k]) return HZ_EFORMAT;
+                t[k] = leaf(cb->len[s], s);
             }
         } else {
-            const uint32_t q = (uint32_t)(r >> (rem - nb));
-            if (deeper_idx[q] < 0) { deeper_idx[q] = (int)deeper.size(); deeper.emplace_back(); }
-            deeper[deeper_idx[q]].push_back(c);
+            const uint32_t q = (uint32_t)(bits >> (rem - nb));
+            cnt[q + 1]++;
+            maxd[q] = std::max(maxd[q], rem - nb);
+            ++ndeep;
         }
     }
-    for (uint32_t q = 0; q < (1u << nb); ++q) {
-        if (deeper_idx[q] < 0) continue;
+    if (!ndeep) return HZ_OK;
+    for (uint32_t q = 0; q < E; ++q) cnt[q + 1] += cnt[q];
+    std::vector<uint32_t> order(ndeep);
+    {
+        std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+        for (size_t i = 0; i < nsyms; ++i) {
+            const uint32_t s = syms[i];
+            const uint32_t rem = cb->len[s] - D;
+            if (rem <= nb) continue;
+            const uint64_t bits = cb->code[s] & ((1ull << rem) - 1);
+            order[pos[(uint32_t)(bits >> (rem - nb))]++] = s;
+        }
+    }
+    for (uint32_t q = 0; q < E; ++q) {
+        if (cnt[q + 1] == cnt[q]) continue;
         if (tab[base + q]) return HZ_EFORMAT;
-        const std::vector<CodeRec>& sub = deeper[deeper_idx[q]];
-        uint32_t mx = 0;
-        for (const CodeRec& c : sub) mx = std::max(mx, c.len);
-        const int D2 = D + nb;
-        const int nb2 = std::min<int>((int)mx - D2, kDecLevelBits);
+        const uint32_t nb2 = std::min<uint32_t>(maxd[q], (uint32_t)kDecLevelBits);
         const size_t off = l2.size();
         if (off + (1ull << nb2) >= (1ull << 26)) return HZ_ENOMEM;
         l2.resize(off + (1ull << nb2), 0u);
-        tab[base + q] = ((uint32_t)nb2 << 26) | (uint32_t)off;
-        int rc = fill_level(l2, off, nb2, D2, sub, l2);
+        tab[base + q] = (nb2 << 26) | (uint32_t)off;  // (tab may alias l2: index, not pointer)
+        const int rc = fill_level(cb, l2, off, nb2, D + nb, order.data() + cnt[q], cnt[q + 1] - cnt[q], l2);
         if (rc) return rc;
     }
     return HZ_OK;
 }
-}  // namespace
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
     K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
-    std::vector<CodeRec> recs;
-    for (uint32_t s = 0; s < HZ_NSYM; ++s)
-        if (cb->len[s]) recs.push_back({cb->code[s], cb->len[s], s});
     img.assign(1u << K1, 0u);
     l2.clear();
-    int rc = fill_level(img, 0, K1, 0, recs, l2);
+    l2.reserve(1u << 19);
+    std::vector<uint32_t> syms;
+    syms.reserve(HZ_NSYM);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) syms.push_back(s);
+    const int rc = fill_level(cb, img, 0, (uint32_t)K1, 0, syms.data(), syms.size(), l2);
     if (rc) return rc;
     // Unused windows (incomplete codes) decode as a 1-bit filler so a lane
     // that runs past its unit's end never stalls.

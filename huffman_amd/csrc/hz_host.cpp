@@ -35,6 +35,13 @@ using namespace hz;
 
 #define HZ_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return HZ_EHIP; } while (0)
 
+// Pinned host staging for table uploads (see hz_codebook_upload_encode).
+struct Staging {
+    uint8_t* p = nullptr;
+    size_t cap = 0, used = 0;
+    hipEvent_t done = nullptr;
+};
+
 struct hz_ctx {
     int device = 0;
     int ncu = 0;
@@ -49,6 +56,8 @@ struct hz_ctx {
     double thr_alpha = -1.0;
     hipEvent_t ev[4][2] = {};
     bool ev_used[4] = {false, false, false, false};
+    Staging stage_enc, stage_dec;
+    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0;
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -111,6 +120,10 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_tables(c->t);
+    for (Staging* st : {&c->stage_enc, &c->stage_dec}) {
+        if (st->done) (void)hipEventDestroy(st->done);
+        (void)hipHostFree(st->p);
+    }
     (void)hipFree(c->d_desc);
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_thr);
@@ -169,53 +182,106 @@ extern "C" int hz_hist16(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d
     return HZ_OK;
 }
 
-template <typename T>
-static int upload(T** dptr, const std::vector<T>& v, hipStream_t s) {
-    if (*dptr) { (void)hipFree(*dptr); *dptr = nullptr; }
-    if (v.empty()) return HZ_OK;
-    HZ_TRY(hipMalloc(dptr, v.size() * sizeof(T)));
-    HZ_TRY(hipMemcpyAsync(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
-    HZ_TRY(hipStreamSynchronize(s));  // v may be a temporary
+// Device tables live in per-context buffers that only grow; host images are
+// staged in pinned memory and copied asynchronously on the context stream, so
+// an upload never synchronises and the decode tables can be built on the host
+// while the pack kernel runs (bench step: upload_encode -> pack ->
+// upload_decode -> decode). Stream order keeps in-flight kernels on the
+// previous tables; a staging buffer is reused only after its last copy's event.
+static int staging_begin(Staging& st) {
+    if (!st.done) HZ_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+    else HZ_TRY(hipEventSynchronize(st.done));
+    st.used = 0;
     return HZ_OK;
 }
 
-extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
+template <typename T>
+static int stage_copy(hz_ctx* c, Staging& st, T** dptr, size_t* dcap, const std::vector<T>& v) {
+    const size_t bytes = v.size() * sizeof(T);
+    if (*dcap < bytes) {
+        HZ_TRY(hipStreamSynchronize(c->stream));
+        (void)hipFree(*dptr);
+        *dptr = nullptr;
+        HZ_TRY(hipMalloc(dptr, bytes));
+        *dcap = bytes;
+    }
+    if (st.used + bytes > st.cap) {
+        // grow (rare): earlier copies of this batch must land first
+        HZ_TRY(hipStreamSynchronize(c->stream));
+        uint8_t* np = nullptr;
+        const size_t ncap = std::max(st.cap * 2, st.used + bytes + (1u << 20));
+        HZ_TRY(hipHostMalloc(&np, ncap, hipHostMallocDefault));
+        (void)hipHostFree(st.p);
+        st.p = np;
+        st.cap = ncap;
+        st.used = 0;
+    }
+    memcpy(st.p + st.used, v.data(), bytes);
+    HZ_TRY(hipMemcpyAsync(*dptr, st.p + st.used, bytes, hipMemcpyHostToDevice, c->stream));
+    st.used += (bytes + 255) & ~(size_t)255;
+    return HZ_OK;
+}
+
+extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
     if (!c || !cb) return HZ_EINVAL;
     if (cb->max_len > HZ_MAXLEN) return HZ_ETOOLONG;
     HZ_TRY(hipSetDevice(c->device));
-    HZ_TRY(hipStreamSynchronize(c->stream));  // previous tables may still be in use
     Tables& t = c->t;
-    free_tables(t);
+    t.enc_mode = -1;
     if (cb->nsym == 0) return HZ_OK;
+    int rc;
+    if ((rc = staging_begin(c->stage_enc))) return rc;
     t.max_len = (int)cb->max_len;
     t.min_len = (int)cb->min_len;
-    t.enc_mode = select_enc_mode(cb);
-    int rc;
-    if (t.enc_mode == ENC_DENSE) {
+    const int mode = select_enc_mode(cb);
+    if (mode == ENC_DENSE) {
         std::vector<uint32_t> img = build_enc_dense(cb);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
-        if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
-    } else if (t.enc_mode == ENC_HOT) {
+        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
+    } else if (mode == ENC_HOT) {
         t.hot_mask = choose_hot_mask(cb);
         std::vector<uint32_t> img = build_enc_hot(cb, t.hot_mask);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
-        if ((rc = upload(&t.d_enc_lds, img, c->stream))) return rc;
-        if ((rc = upload(&t.d_enc_esc, build_enc_esc(cb), c->stream))) return rc;
+        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
+        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_esc, &c->cap_enc_esc, build_enc_esc(cb)))) return rc;
     }
-    if ((rc = upload(&t.d_enc_wide, build_enc_wide(cb), c->stream))) return rc;
-    if ((rc = upload(&t.d_len8, build_len8(cb), c->stream))) return rc;
-    t.dec_mode = select_dec_mode(cb);
+    if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_wide, &c->cap_enc_wide, build_enc_wide(cb)))) return rc;
+    if ((rc = stage_copy(c, c->stage_enc, &t.d_len8, &c->cap_len8, build_len8(cb)))) return rc;
+    HZ_TRY(hipEventRecord(c->stage_enc.done, c->stream));
+    t.enc_mode = mode;
+    return HZ_OK;
+}
+
+extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
+    if (!c || !cb) return HZ_EINVAL;
+    if (cb->max_len > HZ_MAXLEN) return HZ_ETOOLONG;
+    HZ_TRY(hipSetDevice(c->device));
+    Tables& t = c->t;
+    t.dec_mode = -1;
+    if (cb->nsym == 0) return HZ_OK;
+    int rc;
+    if ((rc = staging_begin(c->stage_dec))) return rc;
+    t.max_len = (int)cb->max_len;
+    t.min_len = (int)cb->min_len;
+    const int mode = select_dec_mode(cb);
     std::vector<uint32_t> dimg, l2;
-    if (t.dec_mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
+    if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
     else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
-    if ((rc = upload(&t.d_dec_lds, dimg, c->stream))) return rc;
+    if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_lds, &c->cap_dec_lds, dimg))) return rc;
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();
-    if ((rc = upload(&t.d_dec_l2, l2, c->stream))) return rc;
+    if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
+    HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
+    t.dec_mode = mode;
     return HZ_OK;
+}
+
+extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
+    int rc = hz_codebook_upload_encode(c, cb);
+    return rc ? rc : hz_codebook_upload_decode(c, cb);
 }
 
 extern "C" uint64_t hz_index_stride(void) { return kDUSyms; }

@@ -952,7 +952,7 @@ static hipError_t run_decode_variant(int v, const DecArgs& a, uint32_t lds, int 
         case 4: return run_decode<MODE, WIDE, 1, 16, 16, true>(a, lds, ncu, s);
         case 5: return run_decode<MODE, WIDE, 1, 8, 8, true>(a, lds, ncu, s);
         case 6: return run_decode<MODE, WIDE, 1, 16, 32, true>(a, lds, ncu, s);
-        default: return run_decode<MODE, WIDE, 1, 16, 16, true>(a, lds, ncu, s);
+        default: return run_decode<MODE, WIDE, 1, 16, 32, true>(a, lds, ncu, s);
     }
 }
 

@@ -4,8 +4,9 @@ This is the flow `archive` runs, kept on the device end to end so it can be
 timed with inputs already resident in HBM (bench.py) and sharded across ranks
 (huffman_amd/dist.py):
 
-    hist16 (GPU) -> host codebook + header (reference semantics) -> table
-    upload -> pack (GPU, one bit stream + decode-unit index) -> decode (GPU)
+    hist16 (GPU) -> host codebook + header (reference semantics) -> encode
+    table upload -> pack (GPU, one bit stream + decode-unit index) -> decode
+    table upload (host build overlaps the pack kernel) -> decode (GPU)
 
 PyTorch provides device memory and the stream; every compute stage is a
 gfx950 kernel of libhuffman_amd.so.
@@ -62,11 +63,17 @@ class StreamCodec:
         plan = Plan(cb, n_total, hist_host if hist_local is None else hist_local, first_shard, shard_bit_offset,
                     last_byte)
         t1 = time.perf_counter()
-        self.dev.upload(cb)
+        self.dev.upload_encode(cb)   # decode tables follow the pack launch (upload_decode)
         t2 = time.perf_counter()
         self.timings["codebook_ms"] = (t1 - t0) * 1e3
         self.timings["upload_ms"] = (t2 - t1) * 1e3
         return plan
+
+    def upload_decode(self, plan):
+        """Decode tables; call after launching pack so the host build overlaps it."""
+        t0 = time.perf_counter()
+        self.dev.upload_decode(plan.cb)
+        self.timings["upload_decode_ms"] = (time.perf_counter() - t0) * 1e3
 
     def alloc_payload(self, plan, nsym):
         out = torch.empty(max(plan.words, 1) * 4 + 16, dtype=torch.uint8, device=self.device)
@@ -103,6 +110,7 @@ class StreamCodec:
         out, index = self.alloc_payload(plan, n // 2)
         if n // 2:
             self.pack(x, plan, out, index)
+        self.upload_decode(plan)
         return plan, out, index
 
     def file_image(self, plan, payload):

@@ -106,8 +106,13 @@ int hz_header_write(const hz_codebook *cb, uint64_t n, uint8_t last_byte, uint8_
  * Replaces Decompressor.cu:65-103 (U 0 => 65536 :69-71; L 0 => 65536 :94-95). */
 int hz_header_parse(const uint8_t *file, uint64_t len, hz_codebook *cb, hz_header_info *info);
 
-/* Upload a codebook's device tables (encode + decode) to the context. */
+/* Upload a codebook's device tables to the context: encode tables (needed by
+ * hz_pack), decode tables (needed by hz_decode / hz_index_build), or both.
+ * Asynchronous on the context stream; the decode half can be built on the
+ * host while a hz_pack launched before it runs. */
 int hz_codebook_upload(hz_ctx *ctx, const hz_codebook *cb);
+int hz_codebook_upload_encode(hz_ctx *ctx, const hz_codebook *cb);
+int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
 
 /* Index granularity used by hz_pack / hz_decode (symbols per decode unit). */
 uint64_t hz_index_stride(void);
