@@ -73,7 +73,7 @@ PROTOTYPES = [
     ("hz_codebook_upload_encode", _I, [_P, ctypes.POINTER(Codebook)]),
     ("hz_codebook_upload_decode", _I, [_P, ctypes.POINTER(Codebook)]),
     ("hz_index_stride", _U64, []),
-    ("hz_index_entries", _U64, [_U64]),
+    ("hz_index_bytes", _U64, [_U64]),
     ("hz_scratch_bytes", _U64, [_U64]),
     ("hz_pack", _I, [_P, _P, _U64, _U64, _U32, _P, _U64, _P]),
     ("hz_decode", _I, [_P, _P, _U64, _U64, _P, _P]),

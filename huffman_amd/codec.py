@@ -112,8 +112,15 @@ def parse_header(blob):
     return cb, info
 
 
-def index_entries(nsym):
-    return load().hz_index_entries(nsym)
+def index_bytes(nsym):
+    """Bytes of the block index hz_pack writes for nsym symbols (include/huffman_amd.h)."""
+    return load().hz_index_bytes(nsym)
+
+
+def index_starts(index, nsym):
+    """The u64 start[] part of a block index (numpy or torch int64 view)."""
+    nb = (nsym + load().hz_index_stride() - 1) // load().hz_index_stride()
+    return index[:nb + 1]
 
 
 class Device:

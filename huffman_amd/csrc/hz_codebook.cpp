@@ -232,9 +232,18 @@ extern "C" int hz_header_parse(const uint8_t* f, uint64_t len, hz_codebook* cb, 
 namespace hz {
 
 int select_enc_mode(const hz_codebook* cb) {
+    if (cb->min_len == 16 && cb->max_len == 16) return ENC_FIXED16;  // U = 65 536, a complete 16-bit code
     if (cb->max_len <= 16) return ENC_DENSE;
     if (cb->max_len <= kNarrowMaxLen) return ENC_HOT;
     return ENC_WIDE;
+}
+
+// FIXED16: u16 code per symbol.
+std::vector<uint32_t> build_enc_fixed16(const hz_codebook* cb) {
+    std::vector<uint32_t> img(kFixed16LdsBytes / 4, 0u);
+    uint16_t* c16 = reinterpret_cast<uint16_t*>(img.data());
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) c16[s] = (uint16_t)cb->code[s];
+    return img;
 }
 
 // DENSE: entry s = (code << 1 | 1) << (16 - L), 17 bits at bit 17*s (LE bit order).
@@ -319,9 +328,28 @@ std::vector<uint64_t> build_enc_wide(const hz_codebook* cb) {
     return t;
 }
 
+static uint32_t dense_dec_bytes(uint32_t K) {
+    const uint32_t ent = 1u << K;
+    const uint32_t words = (ent / 2 ? ent / 2 : 1) + (ent / 16 ? ent / 16 : 1);
+    return 4 * ((words + 3) & ~3u);
+}
+
+// FIXED16 when every code is 16 bits; DENSE when the lengths span <= 4 values
+// and the table leaves room for kDecMinWaves staging slots; LUT otherwise.
 int select_dec_mode(const hz_codebook* cb) {
-    if (cb->max_len <= 16 && cb->max_len - cb->min_len <= 3) return DEC_DENSE;
+    if (cb->min_len == 16 && cb->max_len == 16) return DEC_FIXED16;
+    if (cb->max_len <= 16 && cb->max_len - cb->min_len <= 3 &&
+        dec_waves(dense_dec_bytes(cb->max_len), (int)cb->max_len) >= kDecMinWaves)
+        return DEC_DENSE;
     return DEC_LUT;
+}
+
+// FIXED16 decode: u16 symbol per 16-bit code.
+std::vector<uint32_t> build_dec_fixed16(const hz_codebook* cb) {
+    std::vector<uint32_t> img(kFixed16LdsBytes / 4, 0u);
+    uint16_t* t16 = reinterpret_cast<uint16_t*>(img.data());
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) t16[cb->code[s] & 0xffffu] = (uint16_t)s;
+    return img;
 }
 
 // DENSE decode: u16 symbol per K-bit window, then 2-bit (L - min_len) per window.

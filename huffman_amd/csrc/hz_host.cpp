@@ -21,6 +21,8 @@
 namespace hz {
 int select_enc_mode(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_dense(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_fixed16(const hz_codebook* cb);
+std::vector<uint32_t> build_dec_fixed16(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m);
 uint32_t choose_hot_mask(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_esc(const hz_codebook* cb);
@@ -234,7 +236,11 @@ extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
     t.max_len = (int)cb->max_len;
     t.min_len = (int)cb->min_len;
     const int mode = select_enc_mode(cb);
-    if (mode == ENC_DENSE) {
+    if (mode == ENC_FIXED16) {
+        std::vector<uint32_t> img = build_enc_fixed16(cb);
+        t.enc_lds_bytes = (uint32_t)(img.size() * 4);
+        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
+    } else if (mode == ENC_DENSE) {
         std::vector<uint32_t> img = build_enc_dense(cb);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
         if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
@@ -245,8 +251,11 @@ extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
         if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
         if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_esc, &c->cap_enc_esc, build_enc_esc(cb)))) return rc;
     }
-    if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_wide, &c->cap_enc_wide, build_enc_wide(cb)))) return rc;
-    if ((rc = stage_copy(c, c->stage_enc, &t.d_len8, &c->cap_len8, build_len8(cb)))) return rc;
+    if (mode == ENC_WIDE &&
+        (rc = stage_copy(c, c->stage_enc, &t.d_enc_wide, &c->cap_enc_wide, build_enc_wide(cb))))
+        return rc;
+    if (mode != ENC_FIXED16 && (rc = stage_copy(c, c->stage_enc, &t.d_len8, &c->cap_len8, build_len8(cb))))
+        return rc;
     HZ_TRY(hipEventRecord(c->stage_enc.done, c->stream));
     t.enc_mode = mode;
     return HZ_OK;
@@ -261,15 +270,18 @@ extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
     if (cb->nsym == 0) return HZ_OK;
     int rc;
     if ((rc = staging_begin(c->stage_dec))) return rc;
-    t.max_len = (int)cb->max_len;
-    t.min_len = (int)cb->min_len;
+    t.dec_max_len = (int)cb->max_len;
+    t.dec_min_len = (int)cb->min_len;
     const int mode = select_dec_mode(cb);
     std::vector<uint32_t> dimg, l2;
-    if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
+    if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
+    else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
     else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
+    t.dec_waves = mode == DEC_FIXED16 ? kDecMaxWaves : dec_waves(t.dec_lds_bytes, t.dec_max_len);
+    if (t.dec_waves <= 0) return HZ_ENOMEM;  // cannot happen for K1 <= 14 and codes <= 56 bits
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_lds, &c->cap_dec_lds, dimg))) return rc;
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();
@@ -284,8 +296,8 @@ extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
     return rc ? rc : hz_codebook_upload_decode(c, cb);
 }
 
-extern "C" uint64_t hz_index_stride(void) { return kDUSyms; }
-extern "C" uint64_t hz_index_entries(uint64_t nsym) { return (nsym + kDUSyms - 1) / kDUSyms; }
+extern "C" uint64_t hz_index_stride(void) { return kBlockSyms; }
+extern "C" uint64_t hz_index_bytes(uint64_t nsym) { return index_bytes(nsym); }
 extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) { return pack_scratch_words(nsym) * sizeof(uint64_t); }
 
 static int ensure_scratch(hz_ctx* c, uint64_t words) {
@@ -482,7 +494,7 @@ int decode_image(const uint8_t* f, uint64_t len, std::vector<uint8_t>& out) {
         if ((rc = dpay.alloc(pay + 16))) return rc;
         HZ_TRY(hipMemsetAsync(dpay.p, 0, pay + 16, c->stream));
         HZ_TRY(hipMemcpyAsync(dpay.p, f + info.payload_byte, pay, hipMemcpyHostToDevice, c->stream));
-        if ((rc = didx.alloc(hz_index_entries(nsym) * 8))) return rc;
+        if ((rc = didx.alloc(hz_index_bytes(nsym)))) return rc;
         if ((rc = dout.alloc(2 * nsym + 16))) return rc;
         if ((rc = hz_index_build(c, (const uint8_t*)dpay.p, pay, info.payload_bit, nsym, (uint64_t*)didx.p))) return rc;
         if ((rc = hz_decode(c, (const uint8_t*)dpay.p, pay, nsym, (const uint64_t*)didx.p, (uint8_t*)dout.p))) return rc;

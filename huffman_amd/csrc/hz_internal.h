@@ -10,17 +10,32 @@ namespace hz {
 constexpr int kWave = 64;
 constexpr int kSPT = 32;                       // symbols per lane (64 input bytes)
 constexpr int kBlockSyms = kWave * kSPT;       // 2048 symbols = 4 KiB of input
-constexpr int kDUSyms = 512;                   // decode unit: one decode lane's run
-constexpr int kLanesPerDU = kDUSyms / kSPT;    // 16 pack lanes per decode unit
-constexpr int kDUPerBlock = kBlockSyms / kDUSyms;
+constexpr int kChainSyms = 16;                 // decode chain: index granularity
+constexpr int kChainsPerBlock = kBlockSyms / kChainSyms;  // 128 (two per lane)
 constexpr int kPackThreads = 1024;             // 16 waves per CU share one LDS table
+constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
+
+// Block index written by hz_pack / hz_index_build (DESIGN.md "Decode"):
+//   u64 start[nblocks + 1]      absolute start bit of every 2048-symbol block
+//                               (start[nblocks] = end of the stream)
+//   u32 sub[nblocks][64]        per lane: the start bits of its two 16-symbol
+//                               chains relative to start[b], mod 2^16 (low,
+//                               high half); exact when block bits < 2^16,
+//                               otherwise recovered by a prefix over deltas.
+__host__ __device__ inline uint64_t index_blocks(uint64_t nsym) { return (nsym + kBlockSyms - 1) / kBlockSyms; }
+__host__ __device__ inline uint64_t index_bytes(uint64_t nsym) {
+    const uint64_t nb = index_blocks(nsym);
+    return nsym ? 8 * (nb + 1) + 4ull * kWave * nb : 0;
+}
 
 // Encode table modes (selected on the host per codebook, DESIGN.md "Pack").
 enum EncMode : int {
     ENC_DENSE = 0,  // max_len <= 16: 65536 x 17-bit sentinel entries, 139 264 B LDS
     ENC_HOT = 1,    // max_len <= 26: 32768 u32 slots (tag,len,code) + u64 escapes
-    ENC_WIDE = 2    // anything up to 56 bits: u64 table in global memory
+    ENC_WIDE = 2,   // anything up to 56 bits: u64 table in global memory
+    ENC_FIXED16 = 3 // every code 16 bits (U = 65536, min_len = max_len): u16 codes in LDS, no scan
 };
+constexpr uint32_t kFixed16LdsBytes = 65536u * 2u;       // 131 072
 constexpr uint32_t kDenseLdsBytes = 65536u * 17u / 8u;   // 139 264
 constexpr uint32_t kHotLdsBytes = 32768u * 4u;           // 131 072
 constexpr uint32_t kLen8LdsBytes = 65536u;               // u8 code length per symbol (count pass)
@@ -29,11 +44,28 @@ constexpr int kNarrowMaxLen = 26;                        // u32 register entries
 
 // Decode table modes.
 enum DecMode : int {
-    DEC_DENSE = 0,  // max_len <= 16, max-min <= 3: 2^K u16 symbols + 2-bit lengths in LDS
-    DEC_LUT = 1     // 2^K1 u32 level-1 entries in LDS, deeper levels in global
+    DEC_DENSE = 0,  // max-min <= 3 and the table fits beside 8 staging slots: 2^K u16 symbols + 2-bit lengths
+    DEC_LUT = 1,    // 2^K1 u32 level-1 entries in LDS, deeper levels in global
+    DEC_FIXED16 = 2 // every code 16 bits: u16 symbol per code in LDS, positions are arithmetic
 };
 constexpr int kDecLutMaxK1 = 14;
 constexpr int kDecLevelBits = 8;
+constexpr int kDecMaxWaves = 16;
+constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
+
+// Per-wave LDS staging of one block's payload (u32 words): the block's bits,
+// chains past the end of a tail block (16 codes each), the 16-byte alignment
+// of the first word and the words a window reads past the last bit.
+__host__ __device__ inline uint32_t dec_stage_words(int max_len) {
+    const uint32_t bits = (uint32_t)(kBlockSyms + kChainSyms) * (uint32_t)max_len;
+    return (((bits + 31) / 32 + 4 + 3) + 3) & ~3u;
+}
+__host__ __device__ inline int dec_waves(uint32_t table_bytes, int max_len) {
+    const uint32_t slot = 4 * dec_stage_words(max_len);
+    if (table_bytes + slot > kLdsBytes) return 0;
+    const uint32_t w = (kLdsBytes - table_bytes) / slot;
+    return w > (uint32_t)kDecMaxWaves ? kDecMaxWaves : (int)w;
+}
 
 
 struct Tables {
@@ -42,6 +74,9 @@ struct Tables {
     int max_len = 0;
     int min_len = 0;
     int dec_k = 0;                 // DENSE window bits / LUT level-1 bits
+    int dec_waves = 0;             // waves per decode workgroup (LDS staging slots)
+    int dec_max_len = 0;           // of the codebook the decode tables were built for
+    int dec_min_len = 0;
     uint32_t enc_lds_bytes = 0;
     uint32_t dec_lds_bytes = 0;
     uint32_t* d_enc_lds = nullptr; // LDS image for the pack kernel

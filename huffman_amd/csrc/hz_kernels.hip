@@ -228,7 +228,8 @@ struct PackArgs {
     uint32_t lead;               // bits before the stream's first bit (header pending bits)
     unsigned long long* blk;     // per block bit count (k_pack_count)
     const unsigned long long* blk_start;
-    unsigned long long* index;   // decode-unit start bits (optional)
+    unsigned long long* index;   // block index start[] (optional, hz_internal.h)
+    uint32_t* index_sub;         // block index sub[] (chain offsets)
     uint32_t* err;
 };
 
@@ -320,8 +321,8 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
 
 // Lane bit count + last 32 bits, then the wave's inclusive scan of (bits, tail).
 template <int MODE>
-HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane, uint32_t& n, uint32_t& sn,
-                           uint32_t& st) {
+HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane, uint32_t& n, uint32_t& nA,
+                           uint32_t& sn, uint32_t& st) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
@@ -331,6 +332,7 @@ HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane,
     for (int k = 0; k < kSPT; ++k) {
         const uint32_t L = (uint32_t)(e[k] >> SH);
         n += L;
+        if (k == kChainSyms - 1) nA = n;  // bits of the lane's first decode chain
         t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
     }
     sn = n;
@@ -346,7 +348,7 @@ HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane,
 }
 
 template <int MODE>
-HZ_DEV void load_lds_table(uint32_t* lds, const uint32_t* img, uint32_t words) {
+HZ_DEV void load_lds_table(uint32_t* lds, const uint32_t* img, uint32_t words) {  // all but WIDE
     if (MODE != ENC_WIDE) {
         const uint4* src = reinterpret_cast<const uint4*>(img);
         uint4* dst = reinterpret_cast<uint4*>(lds);
@@ -437,8 +439,8 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
         T e[kSPT];
         T pe;
         pack_load_lookup<MODE>(a, lds, sym0, nvalid, e, psym, pe);
-        uint32_t n, sn, st;
-        pack_lane_scan<MODE>(e, lane, n, sn, st);
+        uint32_t n, nA, sn, st;
+        pack_lane_scan<MODE>(e, lane, n, nA, sn, st);
         uint32_t ex_n = shfl_up_u32(sn, 1), ex_t = shfl_up_u32(st, 1);
         if (lane == 0) { ex_n = 0; ex_t = 0; }
         const uint64_t bend = bstart + shfl_u32(sn, 63);
@@ -486,8 +488,92 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
         }
         if (fits && nvalid > 0 && sym0 + (uint64_t)nvalid == a.nsym && na > 0)
             *dst = bswap32((uint32_t)(acc << (32 - na)));
-        if (a.index && (lane % kLanesPerDU) == 0 && nvalid > 0)
-            a.index[sym0 / kDUSyms] = o;
+        if (a.index) {  // block index (hz_internal.h): start bits + the lane's two chain offsets
+            a.index_sub[blk * kWave + lane] = (ex_n & 0xffffu) | (((ex_n + nA) & 0xffffu) << 16);
+            if (lane == 0) a.index[blk] = bstart;
+            if (lane == 0 && blk + 1 == a.nblocks) a.index[a.nblocks] = bend;
+        }
+    }
+}
+
+// ---- every code 16 bits (U = 65 536, min_len = max_len = 16) ---------------
+// Symbol i starts at bit start_bit + 16 i: no count pass and no scan. Lane j
+// packs symbols [32 j, 32 j + 32) into the 16 words whose last bit lies in its
+// run; word t is a funnel shift of code pairs t-1 and t by start_bit % 32.
+__global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint64_t start_bit) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<ENC_FIXED16>(lds, a.lds_img, a.lds_words);
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(lds);
+    const uint32_t sb = (uint32_t)(start_bit & 31);
+    const uint64_t W0 = start_bit >> 5;
+    const uint64_t nl = (a.nsym + kSPT - 1) / kSPT;
+    const uint64_t end_word = (start_bit + 16 * a.nsym + 31) >> 5;  // words holding stream bits
+    const bool fits = end_word <= a.out_words;
+    if (!fits && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, 4u);
+    const bool vec_out = (W0 & 3) == 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += stride) {
+        const uint64_t sym0 = j * kSPT;
+        const int nvalid = a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0);
+        uint32_t raw[kSPT / 2];
+        if (nvalid == kSPT) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
+#pragma unroll
+            for (int q = 0; q < kSPT / 8; ++q) {
+                const uint4 v = p[q];
+                raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSPT / 2; ++k) raw[k] = 0;
+            for (int k = 0; k < nvalid; ++k)
+                raw[k >> 1] |= ((uint32_t)a.in[2 * (sym0 + k)] | ((uint32_t)a.in[2 * (sym0 + k) + 1] << 8)) << (16 * (k & 1));
+        }
+        // the previous lane's last code pair (or the header's pending bits)
+        uint32_t prev = a.lead;
+        if (j > 0) {
+            const uint32_t pr = *reinterpret_cast<const uint32_t*>(a.in + 2 * (sym0 - 2));
+            prev = ((uint32_t)c16[pr & 0xffffu] << 16) | c16[pr >> 16];
+        }
+        uint32_t v[kSPT / 2];
+#pragma unroll
+        for (int t = 0; t < kSPT / 2; ++t) {
+            const uint32_t lo = (uint32_t)c16[raw[t] & 0xffffu], hi = (uint32_t)c16[raw[t] >> 16];
+            v[t] = (2 * t < nvalid ? lo << 16 : 0u) | (2 * t + 1 < nvalid ? hi : 0u);
+        }
+        uint32_t o[kSPT / 2];
+#pragma unroll
+        for (int t = 0; t < kSPT / 2; ++t) {
+            const uint32_t p = t ? v[t - 1] : prev;
+            o[t] = sb ? (uint32_t)(((((uint64_t)p) << 32) | v[t]) >> sb) : v[t];
+        }
+        const uint64_t wj = W0 + 16 * j;
+        if (fits) {
+            if (nvalid == kSPT && j + 1 < nl && vec_out) {
+                uint4* d = reinterpret_cast<uint4*>(a.out + wj);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    d[q] = make_uint4(bswap32(o[4 * q]), bswap32(o[4 * q + 1]), bswap32(o[4 * q + 2]), bswap32(o[4 * q + 3]));
+            } else {
+                // words whose first bit is a stream bit; the last lane also
+                // writes the word its final bits spill into
+#pragma unroll
+                for (int t = 0; t < kSPT / 2; ++t)
+                    if (wj + t < end_word) a.out[wj + t] = bswap32(o[t]);
+                if (j + 1 == nl && wj + 16 < end_word)
+                    a.out[wj + 16] = bswap32((uint32_t)(((uint64_t)v[15] << 32) >> sb));
+            }
+        }
+        if (a.index) {
+            const uint64_t blk = j / kWave;
+            const uint32_t lane = (uint32_t)(j % kWave);
+            const uint32_t cnt = (uint32_t)(a.nsym - blk * kBlockSyms < (uint64_t)kBlockSyms ? a.nsym - blk * kBlockSyms
+                                                                                        : (uint64_t)kBlockSyms);
+            const uint32_t ca = 32 * lane < cnt ? 32 * lane : cnt, cb = 32 * lane + 16 < cnt ? 32 * lane + 16 : cnt;
+            a.index_sub[j] = ((16 * ca) & 0xffffu) | (((16 * cb) & 0xffffu) << 16);
+            if (lane == 0) a.index[blk] = start_bit + (uint64_t)blk * kBlockSyms * 16;
+            if (j + 1 == nl) a.index[a.nblocks] = start_bit + 16 * a.nsym;
+        }
     }
 }
 
@@ -588,6 +674,21 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     unsigned long long* blk_start = d_scratch + nblocks;
     unsigned long long* tiles = d_scratch + 2 * nblocks;
     a.blk_start = blk_start; a.index = d_index; a.err = d_err;
+    a.index_sub = d_index ? reinterpret_cast<uint32_t*>(d_index + nblocks + 1) : nullptr;
+    if (t.enc_mode == ENC_FIXED16) {
+        static bool attr_fixed = false;
+        if (!attr_fixed) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_pack_fixed16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kFixed16LdsBytes);
+            if (e != hipSuccess) return e;
+            attr_fixed = true;
+        }
+        const uint64_t nl = (nsym + kSPT - 1) / kSPT;
+        uint64_t wgs = (nl + kPackThreads - 1) / kPackThreads;
+        if (wgs > (uint64_t)ncu) wgs = ncu;  // 128 KiB table: one workgroup per CU
+        hipLaunchKernelGGL(k_pack_fixed16, dim3(wgs), dim3(kPackThreads), kFixed16LdsBytes, s, a, start_bit);
+        return hipGetLastError();
+    }
     const int threads = t.enc_mode == ENC_WIDE ? pack_threads(ENC_WIDE) : kPackThreads;
     const uint64_t waves = (uint64_t)threads / 64;
     uint64_t wgs = (nblocks + waves - 1) / waves;
@@ -629,21 +730,32 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 }
 
 // ===========================================================================
-// Decode. One lane decodes one decode unit (512 symbols) from the start bit
-// the index gives, through an LDS table:
-//   DENSE: 2^K u16 symbols + 2-bit (len - min_len), K = max_len <= 16;
-//   LUT:   2^K1 u32 level-1 entries (leaf: 1|len<<16|sym; link: nbits<<26|offset)
-//          with deeper levels in global memory (L2 resident).
+// Decode (replaces translateFile, Decompressor.cu:259-291).
+//
+// Block decoder: one wave per 2048-symbol pack block. The block's payload
+// bits [start[b], start[b+1]) are staged into the wave's LDS slot with
+// coalesced 16-byte loads (byte-swapped once on the way in); then each lane
+// decodes its 32 symbols as two independent 16-symbol chains whose start bits
+// come from the block index, reading every window straight from LDS. There
+// is no per-lane refill state, so a symbol costs a window read, a table
+// lookup and an add. Tables (LDS, one copy per workgroup):
+//   DENSE: 2^K u16 symbols + 2-bit (len - min_len), K = max_len;
+//   LUT:   2^K1 u32 level-1 entries (leaf: 1<<31 | len<<16 | sym;
+//          link: nbits<<26 | offset), deeper levels in global memory.
+// Every code 16 bits (FIXED16): symbol i sits at bit start + 16 i, so that
+// decoder needs no index and no staging (k_decode_fixed16).
 // ===========================================================================
 struct DecArgs {
-    const uint32_t* words;   // payload, aligned down to 4 bytes
+    const uint32_t* words;   // payload view, 64-byte aligned
     uint64_t nwords;
     uint32_t bit_adj;        // payload bit 0 = bit bit_adj of words
     uint64_t nsym;
-    uint64_t ndu;
-    const unsigned long long* index;
+    uint64_t nblocks;
+    const unsigned long long* starts;  // block index (hz_internal.h)
+    const uint32_t* subs;
     const uint32_t* lds_img;
-    uint32_t lds_words;
+    uint32_t lds_words;      // table words; the staging slots follow
+    uint32_t stage_words;    // per wave
     int k;
     int min_len;
     int max_len;
@@ -652,16 +764,14 @@ struct DecArgs {
     uint32_t* err;
 };
 
-HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) {
-    return w < a.nwords ? bswap32(a.words[w]) : 0u;
-}
-
 template <int MODE>
 HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint32_t& sym, uint32_t& L) {
-    if (MODE == DEC_DENSE) {
+    if (MODE == DEC_FIXED16) {
+        sym = reinterpret_cast<const uint16_t*>(lds)[(uint32_t)(win >> 48)];
+        L = 16;
+    } else if (MODE == DEC_DENSE) {
         const uint32_t idx = (uint32_t)(win >> (64 - a.k));
-        const uint16_t* l16 = reinterpret_cast<const uint16_t*>(lds);
-        sym = l16[idx];
+        sym = reinterpret_cast<const uint16_t*>(lds)[idx];
         const uint32_t lw = lds[(1u << a.k) / 2 + (idx >> 4)];
         L = (uint32_t)a.min_len + ((lw >> ((idx & 15) * 2)) & 3u);
     } else {
@@ -669,8 +779,7 @@ HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint
         uint32_t D = (uint32_t)a.k;
         while (!(e >> 31)) {
             const uint32_t nb = (e >> 26) & 31u;
-            const uint32_t off = e & 0x3ffffffu;
-            e = a.l2[off + (uint32_t)((win << D) >> (64 - nb))];
+            e = a.l2[(e & 0x3ffffffu) + (uint32_t)((win << D) >> (64 - nb))];
             D += nb;
         }
         L = (e >> 16) & 63u;
@@ -678,226 +787,180 @@ HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint
     }
 }
 
-// Bit reader over big-endian words: `buf` holds `nb` valid bits at its top;
-// `nxt` is the following word. Supports codes up to 56 bits.
-struct BitReader {
-    uint64_t buf;
-    uint32_t nb;
-    uint32_t nxt;
-    uint64_t wpos;  // index of the word after nxt
-};
-
-HZ_DEV void br_init(BitReader& r, const DecArgs& a, uint64_t p) {
-    const uint64_t w = p >> 5;
-    const uint32_t sh = (uint32_t)(p & 31);
-    r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
-    r.nb = 64 - sh;
-    r.nxt = ld_word(a, w + 2);
-    r.wpos = w + 3;
+HZ_DEV void copy_lds_table(uint32_t* lds, const uint32_t* img, uint32_t words) {
+    const uint4* src = reinterpret_cast<const uint4*>(img);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (uint32_t i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
 }
 
-HZ_DEV uint64_t br_window(BitReader& r) {
-    if (r.nb <= 32) {
-        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
-        r.nb += 32;
-        r.nxt = 0;  // refilled by br_next
-    }
-    return r.buf;
+// MSB-first window at bit `pos` of a staged (byte-swapped) slot: the top 33+
+// bits are valid, or all 64 when WIDE (codes longer than 32 bits).
+template <bool WIDE>
+HZ_DEV uint64_t stage_window(const uint32_t* stg, uint32_t pos) {
+    const uint32_t wi = pos >> 5, sh = pos & 31;
+    const uint64_t two = (((uint64_t)stg[wi]) << 32) | stg[wi + 1];
+    if (!WIDE) return two << sh;
+    return (two << sh) | ((((uint64_t)stg[wi + 2]) << sh) >> 32);
 }
 
-HZ_DEV uint64_t br_window_wide(BitReader& r) {
-    // up to 64 valid bits in buf plus the next word for codes > 32 bits
-    return r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
-}
-
-// One lane decodes S decode units (512 symbols each) interleaved: one symbol of
-// every unit per step, so a wave's stall on a long-code lookup in global
-// memory is paid once per 64*S symbols. Input arrives as whole CHW-word chunks
-// (the next chunk prefetched while the current one drains); output leaves in
-// OB-symbol bursts of aligned 16-byte stores.
-template <int CHW>
-struct ChunkReader {
-    uint64_t win;      // next bits, MSB first
-    uint32_t nb;       // valid bits in win
-    uint32_t qn;       // valid words left in c[] (consumed from c[0])
-    uint32_t c[CHW];   // current chunk (big-endian words)
-    uint32_t n[CHW];   // next chunk (in flight)
-    uint64_t next;     // index of the chunk after n
-    bool n_ok;         // n holds (or is loading) chunk next-1
-};
-
-template <int CHW>
-HZ_DEV void chunk_load(const DecArgs& a, uint64_t ci, uint32_t (&d)[CHW]) {
-    const uint64_t w0 = ci * CHW;
-    if (w0 + CHW <= a.nwords) {
-        const uint4* p = reinterpret_cast<const uint4*>(a.words + w0);
-#pragma unroll
-        for (int k = 0; k < CHW / 4; ++k) {
-            const uint4 v = p[k];
-            d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < CHW; ++k) d[k] = w0 + k < a.nwords ? a.words[w0 + k] : 0u;
-    }
-}
-
-template <int CHW>
-HZ_DEV void chunk_shift(ChunkReader<CHW>& r) {
-#pragma unroll
-    for (int k = 0; k < CHW - 1; ++k) r.c[k] = r.c[k + 1];
-}
-
-// GP (group prefetch): the next chunk is requested only at output-group
-// boundaries, so every lane's prefetch of a group is issued in the same step
-// and the wave's in-order vmcnt waits expose HBM latency once per group, not
-// on every step that a long-code lookup waits on (DESIGN.md "Decode").
-template <int CHW, bool GP = false>
-HZ_DEV uint32_t chunk_pop(ChunkReader<CHW>& r, const DecArgs& a) {
-    if (r.qn == 0) {
-        if (!r.n_ok) chunk_load<CHW>(a, r.next++, r.n);  // GP fallback: group consumed > 1 chunk
-#pragma unroll
-        for (int k = 0; k < CHW; ++k) r.c[k] = r.n[k];
-        r.qn = CHW;
-        if (GP) r.n_ok = false;
-        else chunk_load<CHW>(a, r.next++, r.n);
-    }
-    const uint32_t w = bswap32(r.c[0]);
-    chunk_shift<CHW>(r);
-    r.qn--;
-    return w;
-}
-
-template <int CHW>
-HZ_DEV void chunk_init(ChunkReader<CHW>& r, const DecArgs& a, uint64_t p) {
-    constexpr int CB = CHW * 32;  // bits per chunk
-    const uint64_t ci = p / CB;
-    chunk_load<CHW>(a, ci, r.c);
-    chunk_load<CHW>(a, ci + 1, r.n);
-    r.next = ci + 2;
-    r.qn = CHW;
-    r.n_ok = true;
-    const uint32_t skip = (uint32_t)((p % CB) >> 5);
-    for (uint32_t k = 0; k < skip; ++k) { chunk_shift<CHW>(r); r.qn--; }
-    const uint32_t sh = (uint32_t)(p & 31);
-    const uint32_t w0 = chunk_pop<CHW>(r, a);
-    const uint32_t w1 = chunk_pop<CHW>(r, a);
-    r.win = ((((uint64_t)w0) << 32) | w1) << sh;
-    r.nb = 64 - sh;
-}
-
-template <int MODE, bool WIDE, int S, int CHW, int OB, bool GP>
+template <int MODE, bool WIDE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
-        uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
-    const uint64_t nlanes = (a.ndu + S - 1) / S;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t ln = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; ln < nlanes; ln += stride) {
-        ChunkReader<CHW> r[S];
-        uint32_t cnt[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const uint64_t du = ln * S + s;
-            const uint64_t s0 = du * kDUSyms;
-            cnt[s] = du >= a.ndu ? 0u : (a.nsym - s0 >= (uint64_t)kDUSyms ? (uint32_t)kDUSyms : (uint32_t)(a.nsym - s0));
-            chunk_init<CHW>(r[s], a, (du < a.ndu ? a.index[du] : 0ull) + a.bit_adj);
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = blockDim.x >> 6;
+    uint32_t* stg = lds + a.lds_words + (threadIdx.x >> 6) * a.stage_words;
+    const uint32_t npc_max = a.stage_words >> 2;
+    for (uint64_t b = (uint64_t)blockIdx.x * nw + (threadIdx.x >> 6); b < a.nblocks; b += (uint64_t)gridDim.x * nw) {
+        const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
+        const uint32_t sub = a.subs[b * kWave + lane];
+        // ---- stage words [w0, w0 + 4 npc) of the payload, byte-swapped
+        const uint64_t w0 = (b0 >> 5) & ~3ull;
+        const uint64_t wend = (b1 >> 5) + (WIDE ? 3 : 2);
+        uint32_t npc = (uint32_t)((wend - w0 + 3) >> 2);
+        npc = npc < npc_max ? npc : npc_max;
+        for (uint32_t p = lane; p < npc; p += kWave) {
+            const uint64_t w = w0 + 4ull * p;
+            uint4 v;
+            if (w + 4 <= a.nwords) {
+                v = *reinterpret_cast<const uint4*>(a.words + w);
+            } else {
+                v.x = w < a.nwords ? a.words[w] : 0u;
+                v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
+                v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
+                v.w = 0u;
+            }
+            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         }
-        const uint32_t cmax = cnt[0];
-        for (uint32_t g = 0; g < cmax; g += OB) {
-            if (GP) {
+        __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+        // ---- chain start bits, relative to the slot
+        uint32_t oA = sub & 0xffffu, oB = sub >> 16;
+        if (b1 - b0 >= 65536) {  // offsets are mod 2^16: rebuild them from deltas
+            uint32_t pv = shfl_up_u32(oB, 1);
+            if (lane == 0) pv = 0;
+            const uint32_t dA = (oA - pv) & 0xffffu, dB = (oB - oA) & 0xffffu;
+            uint32_t sc = dA + dB;
 #pragma unroll
-                for (int s = 0; s < S; ++s)
-                    if (!r[s].n_ok) { chunk_load<CHW>(a, r[s].next++, r[s].n); r[s].n_ok = true; }
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = shfl_up_u32(sc, d);
+                if (lane >= d) sc += o;
             }
-            uint32_t pk[S][OB / 2];
+            oB = sc;
+            oA = sc - dB;
+        }
+        const uint32_t base = (uint32_t)(b0 - (w0 << 5));
+        uint32_t pos[2] = {base + oA, base + oB};
+        uint32_t pk[kSPT / 2];
 #pragma unroll
-            for (int s = 0; s < S; ++s)
+        for (int q = 0; q < kChainSyms; ++q) {
+            uint64_t win[2];
+            uint32_t sym[2], L[2];
 #pragma unroll
-                for (int q = 0; q < OB / 2; ++q) pk[s][q] = 0;
+            for (int c = 0; c < 2; ++c) win[c] = stage_window<WIDE>(stg, pos[c]);
+            if (MODE == DEC_DENSE) {
 #pragma unroll
-            for (int q = 0; q < OB; ++q) {
-                uint64_t win[S];
+                for (int c = 0; c < 2; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
+            } else {
+                uint32_t e[2], e2[2];
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (r[s].nb <= 32) {
-                        r[s].win |= (uint64_t)chunk_pop<CHW, GP>(r[s], a) << (32 - r[s].nb);
-                        r[s].nb += 32;
-                    }
-                    win[s] = r[s].win;
-                    if (WIDE && r[s].nb < 56) {
-                        if (GP && !r[s].qn && !r[s].n_ok) {
-                            chunk_load<CHW>(a, r[s].next++, r[s].n);
-                            r[s].n_ok = true;
-                        }
-                        win[s] |= (uint64_t)bswap32(r[s].qn ? r[s].c[0] : r[s].n[0]) >> (r[s].nb - 32);
-                    }
-                }
-                uint32_t sym[S], L[S];
-                if (MODE == DEC_DENSE) {
+                for (int c = 0; c < 2; ++c) e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))];
 #pragma unroll
-                    for (int s = 0; s < S; ++s) dec_lookup<MODE>(a, lds, win[s], sym[s], L[s]);
-                } else {
-                    uint32_t e[S], e2[S];
-#pragma unroll
-                    for (int s = 0; s < S; ++s) e[s] = lds[(uint32_t)(win[s] >> (64 - a.k))];
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {  // first deeper level: all issued before the wait
-                        e2[s] = e[s];
-                        if (!(e[s] >> 31)) {
-                            const uint32_t nb = (e[s] >> 26) & 31u;
-                            e2[s] = a.l2[(e[s] & 0x3ffffffu) + (uint32_t)((win[s] << a.k) >> (64 - nb))];
-                        }
-                    }
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        uint32_t ee = e2[s];
-                        if (!(e[s] >> 31)) {
-                            uint32_t D = (uint32_t)a.k + ((e[s] >> 26) & 31u);
-                            while (!(ee >> 31)) {  // deeper than k + 8 bits: rare
-                                const uint32_t nb = (ee >> 26) & 31u;
-                                ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[s] << D) >> (64 - nb))];
-                                D += nb;
-                            }
-                        }
-                        L[s] = (ee >> 16) & 63u;
-                        sym[s] = ee & 0xffffu;
+                for (int c = 0; c < 2; ++c) {  // first deeper level of both chains before one wait
+                    e2[c] = e[c];
+                    if (!(e[c] >> 31)) {
+                        const uint32_t nb = (e[c] >> 26) & 31u;
+                        e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << a.k) >> (64 - nb))];
                     }
                 }
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (!WIDE || L[s] < r[s].nb) {
-                        r[s].win <<= L[s];
-                        r[s].nb -= L[s];
-                    } else {
-                        const uint32_t rr = L[s] - r[s].nb;  // bits taken from the next word
-                        const uint32_t w = chunk_pop<CHW, GP>(r[s], a);
-                        r[s].win = (uint64_t)w << (32 + rr);
-                        r[s].nb = 32 - rr;
+                for (int c = 0; c < 2; ++c) {
+                    uint32_t ee = e2[c];
+                    if (!(e[c] >> 31)) {
+                        uint32_t D = (uint32_t)a.k + ((e[c] >> 26) & 31u);
+                        while (!(ee >> 31)) {  // deeper than k1 + 8 bits: rare
+                            const uint32_t nb = (ee >> 26) & 31u;
+                            ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[c] << D) >> (64 - nb))];
+                            D += nb;
+                        }
                     }
-                    pk[s][q >> 1] |= sym[s] << (16 * (q & 1));
+                    L[c] = (ee >> 16) & 63u;
+                    sym[c] = ee & 0xffffu;
                 }
             }
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const uint64_t s0 = (ln * S + s) * kDUSyms;
-                if (g + OB <= cnt[s]) {
-                    uint4* o = reinterpret_cast<uint4*>(a.out + 2 * (s0 + g));
+            for (int c = 0; c < 2; ++c) {
+                pos[c] += L[c];
+                if (q & 1) pk[c * 8 + (q >> 1)] |= sym[c] << 16;
+                else pk[c * 8 + (q >> 1)] = sym[c];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // ---- 32 symbols = 64 contiguous output bytes per lane
+        const uint64_t sym0 = b * kBlockSyms + (uint64_t)lane * kSPT;
+        if (sym0 + kSPT <= a.nsym) {
+            uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0);
 #pragma unroll
-                    for (int k = 0; k < OB / 8; ++k)
-                        o[k] = make_uint4(pk[s][4 * k], pk[s][4 * k + 1], pk[s][4 * k + 2], pk[s][4 * k + 3]);
-                } else if (g < cnt[s]) {
-                    uint8_t* ob = a.out + 2 * (s0 + g);
-                    for (uint32_t q = 0; q < cnt[s] - g; ++q) {
-                        const uint32_t v = (pk[s][q >> 1] >> (16 * (q & 1))) & 0xffffu;
-                        ob[2 * q] = (uint8_t)v;
-                        ob[2 * q + 1] = (uint8_t)(v >> 8);
-                    }
-                }
+            for (int q = 0; q < 4; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+        } else if (sym0 < a.nsym) {
+            uint8_t* ob = a.out + 2 * sym0;
+            const uint32_t cnt = (uint32_t)(a.nsym - sym0);
+            for (uint32_t q = 0; q < cnt; ++q) {
+                const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                ob[2 * q] = (uint8_t)v;
+                ob[2 * q + 1] = (uint8_t)(v >> 8);
+            }
+        }
+    }
+}
+
+// Every code 16 bits: lane j decodes symbols [32 j, 32 j + 32) from the 17
+// words starting at stream word (p0 >> 5) + 16 j.
+__global__ __launch_bounds__(1024) void k_decode_fixed16(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t p0 = a.starts[0] + a.bit_adj;  // the stream's first bit (the index holds nothing else we need)
+    const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
+    const uint32_t sh = (uint32_t)(p0 & 31);
+    const uint64_t W0 = p0 >> 5;
+    const bool vec = (W0 & 3) == 0;
+    const uint64_t nl = (a.nsym + kSPT - 1) / kSPT;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += stride) {
+        const uint64_t ws = W0 + 16 * j;
+        uint32_t w[17];
+        if (vec && ws + 17 <= a.nwords) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.words + ws);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = p[q];
+                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+            }
+            w[16] = a.words[ws + 16];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 17; ++k) w[k] = ws + k < a.nwords ? a.words[ws + k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 17; ++k) w[k] = bswap32(w[k]);
+        uint32_t o[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t c = (uint32_t)(((((uint64_t)w[t]) << 32 | w[t + 1]) << sh) >> 32);
+            o[t] = (uint32_t)t16[c >> 16] | ((uint32_t)t16[c & 0xffffu] << 16);
+        }
+        const uint64_t sym0 = j * kSPT;
+        if (sym0 + kSPT <= a.nsym) {
+            uint4* d = reinterpret_cast<uint4*>(a.out + 2 * sym0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        } else {
+            uint8_t* ob = a.out + 2 * sym0;
+            const uint32_t cnt = (uint32_t)(a.nsym - sym0);
+            for (uint32_t q = 0; q < cnt; ++q) {
+                const uint32_t v = (o[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                ob[2 * q] = (uint8_t)v;
+                ob[2 * q + 1] = (uint8_t)(v >> 8);
             }
         }
     }
@@ -905,55 +968,40 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
 
 static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                           uint64_t nsym) {
-    // Chunk reads are 64-byte aligned: view the payload from the 64-byte
-    // boundary at or below it (inside the same allocation: device allocations
-    // are 256-byte aligned). The last word may extend up to 3 bytes past
-    // payload_bytes (include/huffman_amd.h: hz_decode).
+    // View the payload from the 64-byte boundary at or below it (inside the
+    // same allocation: device allocations are 256-byte aligned). The last word
+    // may extend up to 3 bytes past payload_bytes (include/huffman_amd.h).
     const uintptr_t base = (uintptr_t)d_payload & ~(uintptr_t)63;
     a.words = reinterpret_cast<const uint32_t*>(base);
     a.bit_adj = (uint32_t)(((uintptr_t)d_payload & 63) * 8);
     a.nwords = (payload_bytes + ((uintptr_t)d_payload & 63) + 3) / 4;
     a.nsym = nsym;
-    a.ndu = (nsym + kDUSyms - 1) / kDUSyms;
+    a.nblocks = index_blocks(nsym);
     a.lds_img = t.d_dec_lds;
     a.lds_words = t.dec_lds_bytes / 4;
+    a.stage_words = dec_stage_words(t.dec_max_len);
     a.k = t.dec_k;
-    a.min_len = t.min_len;
-    a.max_len = t.max_len;
+    a.min_len = t.dec_min_len;
+    a.max_len = t.dec_max_len;
     a.l2 = t.d_dec_l2;
 }
 
-// Decode variants (S streams per lane, CHW-word chunks, OB-symbol bursts),
-// selectable with HZ_DEC_VARIANT for A/B measurements; DESIGN.md records why
-// the default was chosen.
-template <int MODE, bool WIDE, int S, int CHW, int OB, bool GP>
-static hipError_t run_decode(const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
+template <int MODE, bool WIDE>
+static hipError_t run_decode(const DecArgs& a, int waves, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, S, CHW, OB, GP>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const uint64_t nlanes = (a.ndu + S - 1) / S;
-    uint64_t wgs = (nlanes + 1023) / 1024;
-    const uint64_t cap = (uint64_t)ncu * 4;
+    const uint32_t lds = 4 * (a.lds_words + (uint32_t)waves * a.stage_words);
+    const uint64_t per_cu = kLdsBytes / lds;
+    uint64_t wgs = (a.nblocks + waves - 1) / waves;
+    const uint64_t cap = (uint64_t)ncu * (per_cu ? per_cu : 1);
     if (wgs > cap) wgs = cap;
-    hipLaunchKernelGGL((k_decode<MODE, WIDE, S, CHW, OB, GP>), dim3(wgs), dim3(1024), lds, s, a);
+    hipLaunchKernelGGL((k_decode<MODE, WIDE>), dim3(wgs), dim3(64 * waves), lds, s, a);
     return hipGetLastError();
-}
-
-template <int MODE, bool WIDE>
-static hipError_t run_decode_variant(int v, const DecArgs& a, uint32_t lds, int ncu, hipStream_t s) {
-    switch (v) {
-        case 1: return run_decode<MODE, WIDE, 1, 16, 32, false>(a, lds, ncu, s);
-        case 2: return run_decode<MODE, WIDE, 2, 8, 16, false>(a, lds, ncu, s);
-        case 3: return run_decode<MODE, WIDE, 1, 8, 16, false>(a, lds, ncu, s);
-        case 4: return run_decode<MODE, WIDE, 1, 16, 16, true>(a, lds, ncu, s);
-        case 5: return run_decode<MODE, WIDE, 1, 8, 8, true>(a, lds, ncu, s);
-        case 6: return run_decode<MODE, WIDE, 1, 16, 32, true>(a, lds, ncu, s);
-        default: return run_decode<MODE, WIDE, 1, 16, 32, true>(a, lds, ncu, s);
-    }
 }
 
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
@@ -962,46 +1010,76 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     if (nsym == 0) return hipSuccess;
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
-    a.index = d_index; a.out = d_out; a.err = d_err;
-    static int variant = -1;
-    if (variant < 0) {
-        const char* ev = getenv("HZ_DEC_VARIANT");
-        variant = ev ? atoi(ev) : 0;
+    a.starts = d_index;
+    a.subs = reinterpret_cast<const uint32_t*>(d_index + a.nblocks + 1);
+    a.out = d_out; a.err = d_err;
+    if (t.dec_mode == DEC_FIXED16) {
+        static bool attr = false;
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_decode_fixed16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kFixed16LdsBytes);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        const uint64_t nl = (nsym + kSPT - 1) / kSPT;
+        uint64_t wgs = (nl + 1023) / 1024;
+        if (wgs > (uint64_t)ncu) wgs = ncu;
+        hipLaunchKernelGGL(k_decode_fixed16, dim3(wgs), dim3(1024), kFixed16LdsBytes, s, a);
+        return hipGetLastError();
     }
-    const bool wide = t.max_len > 32;
-    const uint32_t lds = t.dec_lds_bytes;
-    if (t.dec_mode == DEC_DENSE)
-        return wide ? run_decode_variant<DEC_DENSE, true>(variant, a, lds, ncu, s)
-                    : run_decode_variant<DEC_DENSE, false>(variant, a, lds, ncu, s);
-    return wide ? run_decode_variant<DEC_LUT, true>(variant, a, lds, ncu, s)
-                : run_decode_variant<DEC_LUT, false>(variant, a, lds, ncu, s);
+    const int waves = t.dec_waves;
+    if (waves <= 0) return hipErrorInvalidValue;
+    const bool wide = t.dec_max_len > 32;
+    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false>(a, waves, ncu, s);
+    return wide ? run_decode<DEC_LUT, true>(a, waves, ncu, s) : run_decode<DEC_LUT, false>(a, waves, ncu, s);
 }
 
 // Serial index build for an index-less stream: one lane walks the stream and
-// records the start bit of every decode unit. Correct for any stream; used for
-// reference-produced files (the parallel self-synchronising builder is the
-// next step).
+// records the start bit of every block and the offset of every 16-symbol
+// chain. Correct for any stream; used for reference-produced files (the
+// parallel self-synchronising builder is the next step).
+struct BitReader {
+    uint64_t buf;
+    uint32_t nb;
+    uint32_t nxt;
+    uint64_t wpos;  // index of the word after nxt
+};
+
+HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) { return w < a.nwords ? bswap32(a.words[w]) : 0u; }
+
 template <int MODE>
-__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* index) {
+__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* starts, uint32_t* subs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.lds_img);
-        uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (uint32_t i = threadIdx.x; i < a.lds_words / 4; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
+    copy_lds_table(lds, a.lds_img, a.lds_words);
     if (threadIdx.x != 0) return;
     uint64_t pos = start_bit;
+    const uint64_t p = pos + a.bit_adj;
     BitReader r;
-    br_init(r, a, pos + a.bit_adj);
+    {
+        const uint64_t w = p >> 5;
+        const uint32_t sh = (uint32_t)(p & 31);
+        r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
+        r.nb = 64 - sh;
+        r.nxt = ld_word(a, w + 2);
+        r.wpos = w + 3;
+    }
+    uint64_t bstart = 0;
+    uint32_t lo = 0;
     for (uint64_t i = 0; i < a.nsym; ++i) {
-        if (i % kDUSyms == 0) index[i / kDUSyms] = pos;
+        const uint32_t in_blk = (uint32_t)(i % kBlockSyms);
+        if (in_blk == 0) { starts[i / kBlockSyms] = pos; bstart = pos; }
+        if (in_blk % kChainSyms == 0) {
+            const uint32_t off = (uint32_t)(pos - bstart) & 0xffffu;
+            uint32_t& w = subs[(i / kBlockSyms) * kWave + in_blk / kSPT];
+            if ((in_blk / kChainSyms) & 1) w = lo | (off << 16);
+            else { lo = off; w = off; }
+        }
         if (r.nb <= 32) {
             r.buf |= (uint64_t)r.nxt << (32 - r.nb);
             r.nb += 32;
             r.nxt = ld_word(a, r.wpos++);
         }
-        const uint64_t win = br_window_wide(r);
+        const uint64_t win = r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
         uint32_t sym, L;
         dec_lookup<MODE>(a, lds, win, sym, L);
         if (L == 0) { atomicOr(a.err, 2u); return; }
@@ -1011,11 +1089,21 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
             r.nb -= L;
         } else {
             const uint32_t rr = L - r.nb;
-            r.buf = rr ? ((uint64_t)r.nxt << (32 + rr)) : ((uint64_t)r.nxt << 32);
+            r.buf = (uint64_t)r.nxt << (32 + rr);
             r.nb = 32 - rr;
             r.nxt = ld_word(a, r.wpos++);
         }
     }
+    // chains past the end of a tail block start at the end
+    const uint64_t nb = a.nblocks;
+    const uint32_t tail = (uint32_t)(a.nsym - (nb - 1) * kBlockSyms);
+    const uint32_t endoff = (uint32_t)(pos - bstart) & 0xffffu;
+    for (uint32_t c = (tail + kChainSyms - 1) / kChainSyms; c < (uint32_t)kChainsPerBlock; ++c) {
+        uint32_t& w = subs[(nb - 1) * kWave + c / 2];
+        if (c & 1) w = (w & 0xffffu) | (endoff << 16);
+        else w = endoff;
+    }
+    starts[nb] = pos;
 }
 
 hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
@@ -1024,18 +1112,23 @@ hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64
     if (nsym == 0) return hipSuccess;
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
-    a.index = nullptr; a.out = nullptr; a.err = d_err;
-    const void* fn = t.dec_mode == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE> : (const void*)k_index_serial<DEC_LUT>;
-    static bool attr[2] = {false, false};
-    if (!attr[t.dec_mode]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    a.starts = nullptr; a.subs = nullptr; a.out = nullptr; a.err = d_err;
+    uint32_t* subs = reinterpret_cast<uint32_t*>(d_index + a.nblocks + 1);
+    const int m = t.dec_mode;
+    const void* fn = m == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE>
+                   : m == DEC_FIXED16 ? (const void*)k_index_serial<DEC_FIXED16> : (const void*)k_index_serial<DEC_LUT>;
+    static bool attr[3] = {false, false, false};
+    if (!attr[m]) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
         if (e != hipSuccess) return e;
-        attr[t.dec_mode] = true;
+        attr[m] = true;
     }
-    if (t.dec_mode == DEC_DENSE)
-        hipLaunchKernelGGL(k_index_serial<DEC_DENSE>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index);
+    if (m == DEC_DENSE)
+        hipLaunchKernelGGL(k_index_serial<DEC_DENSE>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
+    else if (m == DEC_FIXED16)
+        hipLaunchKernelGGL(k_index_serial<DEC_FIXED16>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
     else
-        hipLaunchKernelGGL(k_index_serial<DEC_LUT>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index);
+        hipLaunchKernelGGL(k_index_serial<DEC_LUT>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .codec import Device, build_codebook, header_bits, index_entries, payload_bits, write_header
+from .codec import Device, build_codebook, header_bits, index_bytes, payload_bits, write_header
 
 
 class Plan:
@@ -77,7 +77,7 @@ class StreamCodec:
 
     def alloc_payload(self, plan, nsym):
         out = torch.empty(max(plan.words, 1) * 4 + 16, dtype=torch.uint8, device=self.device)
-        index = torch.empty(max(index_entries(nsym), 1), dtype=torch.int64, device=self.device)
+        index = torch.empty(max((index_bytes(nsym) + 7) // 8, 1), dtype=torch.int64, device=self.device)
         return out, index
 
     def pack(self, x, plan, out, index):

@@ -114,31 +114,37 @@ int hz_codebook_upload(hz_ctx *ctx, const hz_codebook *cb);
 int hz_codebook_upload_encode(hz_ctx *ctx, const hz_codebook *cb);
 int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
 
-/* Index granularity used by hz_pack / hz_decode (symbols per decode unit). */
+/* Block index written by hz_pack / hz_index_build and read by hz_decode
+ * (hz_index_bytes(nsym) bytes, 8-byte aligned): u64 start[nblocks + 1] -- the
+ * absolute start bit of every hz_index_stride() = 2048-symbol block, then the
+ * stream's end bit -- followed by u32 sub[nblocks][64]: the start bits of the
+ * 16-symbol chains 2l and 2l+1 of the block relative to start[b], mod 2^16
+ * (low and high half). The reference has no index (its decoder is serial,
+ * Decompressor.cu:259-291); this is the side band that makes decode parallel. */
 uint64_t hz_index_stride(void);
-uint64_t hz_index_entries(uint64_t nsym);
+uint64_t hz_index_bytes(uint64_t nsym);
 uint64_t hz_scratch_bytes(uint64_t nsym);
 
 /* Pack the n/2 symbols of d_in with the uploaded codebook into d_out as one
  * MSB-first bit stream beginning at bit `start_bit` of d_out (d_out 4-byte
  * aligned; bits of d_out's first word before start_bit are taken from `lead`,
  * right aligned, i.e. the header's pending bits). Bits after the stream's end
- * up to the next 32-bit word are zero. d_index (optional, hz_index_entries()
- * u64) receives the absolute start bit of every decode unit. Replaces
+ * up to the next 32-bit word are zero. d_index (optional, hz_index_bytes())
+ * receives the block index. Replaces
  * populateCWLength + transform_inclusive_scan + encodeFromCW
  * (Compressor.cu:50-61,541-576,182-313) and writeFileContent (:673-684,597-601). */
 int hz_pack(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t start_bit, uint32_t lead,
             uint8_t *d_out, uint64_t out_cap, uint64_t *d_index);
 
 /* Decode nsym symbols from d_payload (bit stream as hz_pack writes it) into
- * d_out (2*nsym bytes, 16-byte aligned). d_index: start bit of every decode
- * unit (from hz_pack, or hz_index_build for an index-less stream). d_payload
+ * d_out (2*nsym bytes, 16-byte aligned). d_index: the block index (from
+ * hz_pack, or hz_index_build for an index-less stream). d_payload
  * must stay readable up to the next 4-byte boundary after payload_bytes.
  * Replaces translateFile (Decompressor.cu:259-291). */
 int hz_decode(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t nsym,
               const uint64_t *d_index, uint8_t *d_out);
 
-/* Build the decode-unit index of an index-less stream (a .compressed file from
+/* Build the block index of an index-less stream (a .compressed file from
  * the reference encoder) on the device. */
 int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                    uint64_t nsym, uint64_t *d_index);

@@ -210,8 +210,10 @@ def test_pipeline_4gib_roundtrip_properties(codec):
     from huffman_amd import codebook_arrays
     _, ln, _ = codebook_arrays(plan.cb)
     assert plan.payload_bits == int(np.sum(h * ln.astype(np.uint64)))
-    idx = index.cpu().numpy()
+    from huffman_amd import index_starts
+    idx = index_starts(index.cpu().numpy(), n // 2)
     assert idx[0] == plan.start_bit and np.all(np.diff(idx) > 0)
+    assert int(idx[-1]) == plan.start_bit + plan.payload_bits
     out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
     codec.decode(payload, n // 2, index, out)
     codec.sync()

@@ -118,6 +118,9 @@ def test_header_parse_empty_conventions(built_lib):
 
 
 def test_index_geometry(built_lib):
-    assert built_lib.hz_index_stride() == 512
-    assert built_lib.hz_index_entries(0) == 0
-    assert built_lib.hz_index_entries(513) == 2
+    """Block index: u64 start[nblocks + 1] + u32 sub[nblocks][64] (include/huffman_amd.h)."""
+    assert built_lib.hz_index_stride() == 2048
+    assert built_lib.hz_index_bytes(0) == 0
+    assert built_lib.hz_index_bytes(1) == 8 * 2 + 256
+    assert built_lib.hz_index_bytes(2049) == 8 * 3 + 2 * 256
+    assert built_lib.hz_index_bytes(1 << 33) == 8 * ((1 << 22) + 1) + 256 * (1 << 22)
