@@ -339,7 +339,7 @@ static uint32_t dense_dec_bytes(uint32_t K) {
 int select_dec_mode(const hz_codebook* cb) {
     if (cb->min_len == 16 && cb->max_len == 16) return DEC_FIXED16;
     if (cb->max_len <= 16 && cb->max_len - cb->min_len <= 3 &&
-        dec_waves(dense_dec_bytes(cb->max_len), (int)cb->max_len) >= kDecMinWaves)
+        dense_dec_bytes(cb->max_len) + 4 * kDecMinWaves * dec_slot_words_max((int)cb->max_len) <= kLdsBytes)
         return DEC_DENSE;
     return DEC_LUT;
 }
@@ -438,7 +438,8 @@ static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t 
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
-    K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
+    static const int k1_env = getenv("HZ_DEC_K1") ? atoi(getenv("HZ_DEC_K1")) : 0;  // tuning experiments
+    K1 = std::min<int>((int)cb->max_len, k1_env > 0 && k1_env <= kDecLutMaxK1 ? k1_env : kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
     img.assign(1u << K1, 0u);
     l2.clear();

@@ -280,8 +280,8 @@ extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
-    t.dec_waves = mode == DEC_FIXED16 ? kDecMaxWaves : dec_waves(t.dec_lds_bytes, t.dec_max_len);
-    if (t.dec_waves <= 0) return HZ_ENOMEM;  // cannot happen for K1 <= 14 and codes <= 56 bits
+    if (mode != DEC_FIXED16 && t.dec_lds_bytes + 4 * dec_slot_words_max(t.dec_max_len) > kLdsBytes)
+        return HZ_ENOMEM;  // cannot happen for K1 <= 14 and codes <= 56 bits
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_lds, &c->cap_dec_lds, dimg))) return rc;
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();

@@ -18,6 +18,7 @@ constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
 // Block index written by hz_pack / hz_index_build (DESIGN.md "Decode"):
 //   u64 start[nblocks + 1]      absolute start bit of every 2048-symbol block
 //                               (start[nblocks] = end of the stream)
+//   u64 max_bits                largest block (bits): sizes the decoder's LDS slots
 //   u32 sub[nblocks][64]        per lane: the start bits of its two 16-symbol
 //                               chains relative to start[b], mod 2^16 (low,
 //                               high half); exact when block bits < 2^16,
@@ -25,8 +26,9 @@ constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
 __host__ __device__ inline uint64_t index_blocks(uint64_t nsym) { return (nsym + kBlockSyms - 1) / kBlockSyms; }
 __host__ __device__ inline uint64_t index_bytes(uint64_t nsym) {
     const uint64_t nb = index_blocks(nsym);
-    return nsym ? 8 * (nb + 1) + 4ull * kWave * nb : 0;
+    return nsym ? 8 * (nb + 2) + 4ull * kWave * nb : 0;
 }
+__host__ __device__ inline uint64_t index_sub_offset(uint64_t nblocks) { return nblocks + 2; }  // in u64 words
 
 // Encode table modes (selected on the host per codebook, DESIGN.md "Pack").
 enum EncMode : int {
@@ -53,20 +55,19 @@ constexpr int kDecLevelBits = 8;
 constexpr int kDecMaxWaves = 16;
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
 
-// Per-wave LDS staging of one block's payload (u32 words): the block's bits,
-// chains past the end of a tail block (16 codes each), the 16-byte alignment
-// of the first word and the words a window reads past the last bit.
-__host__ __device__ inline uint32_t dec_stage_words(int max_len) {
-    const uint32_t bits = (uint32_t)(kBlockSyms + kChainSyms) * (uint32_t)max_len;
-    return (((bits + 31) / 32 + 4 + 3) + 3) & ~3u;
+// Per-wave LDS slot for one block's payload (u32 words), from the largest
+// block of the stream: its bits, chains past the end of a tail block (16 codes
+// each), the 16-byte alignment of the first word and the words a window reads
+// past the last bit.
+__host__ __device__ inline uint32_t dec_slot_words(uint64_t max_bits, int max_len) {
+    const uint64_t bits = max_bits + (uint64_t)kChainSyms * (uint32_t)max_len;
+    const uint64_t w = (bits + 31) / 32 + 4 + 3;
+    return (uint32_t)((w + 3) & ~3ull);
 }
-__host__ __device__ inline int dec_waves(uint32_t table_bytes, int max_len) {
-    const uint32_t slot = 4 * dec_stage_words(max_len);
-    if (table_bytes + slot > kLdsBytes) return 0;
-    const uint32_t w = (kLdsBytes - table_bytes) / slot;
-    return w > (uint32_t)kDecMaxWaves ? kDecMaxWaves : (int)w;
+// Worst case: every symbol of a block at max_len bits.
+__host__ __device__ inline uint32_t dec_slot_words_max(int max_len) {
+    return dec_slot_words((uint64_t)kBlockSyms * (uint32_t)max_len, max_len);
 }
-
 
 struct Tables {
     int enc_mode = -1;
@@ -74,7 +75,6 @@ struct Tables {
     int max_len = 0;
     int min_len = 0;
     int dec_k = 0;                 // DENSE window bits / LUT level-1 bits
-    int dec_waves = 0;             // waves per decode workgroup (LDS staging slots)
     int dec_max_len = 0;           // of the codebook the decode tables were built for
     int dec_min_len = 0;
     uint32_t enc_lds_bytes = 0;

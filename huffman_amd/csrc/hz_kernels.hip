@@ -429,6 +429,7 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t max_bits = 0;  // largest block of this wave (index max_bits: one atomic per wave)
     for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
         const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
         const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
@@ -490,10 +491,14 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
             *dst = bswap32((uint32_t)(acc << (32 - na)));
         if (a.index) {  // block index (hz_internal.h): start bits + the lane's two chain offsets
             a.index_sub[blk * kWave + lane] = (ex_n & 0xffffu) | (((ex_n + nA) & 0xffffu) << 16);
-            if (lane == 0) a.index[blk] = bstart;
-            if (lane == 0 && blk + 1 == a.nblocks) a.index[a.nblocks] = bend;
+            if (lane == 0) {
+                a.index[blk] = bstart;
+                if (blk + 1 == a.nblocks) a.index[a.nblocks] = bend;
+            }
+            max_bits = bend - bstart > max_bits ? bend - bstart : max_bits;
         }
     }
+    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
 // ---- every code 16 bits (U = 65 536, min_len = max_len = 16) ---------------
@@ -573,6 +578,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
             a.index_sub[j] = ((16 * ca) & 0xffffu) | (((16 * cb) & 0xffffu) << 16);
             if (lane == 0) a.index[blk] = start_bit + (uint64_t)blk * kBlockSyms * 16;
             if (j + 1 == nl) a.index[a.nblocks] = start_bit + 16 * a.nsym;
+            if (j == 0) a.index[a.nblocks + 1] = 16ull * (a.nsym < (uint64_t)kBlockSyms ? a.nsym : (uint64_t)kBlockSyms);
         }
     }
 }
@@ -674,7 +680,11 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     unsigned long long* blk_start = d_scratch + nblocks;
     unsigned long long* tiles = d_scratch + 2 * nblocks;
     a.blk_start = blk_start; a.index = d_index; a.err = d_err;
-    a.index_sub = d_index ? reinterpret_cast<uint32_t*>(d_index + nblocks + 1) : nullptr;
+    a.index_sub = d_index ? reinterpret_cast<uint32_t*>(d_index + index_sub_offset(nblocks)) : nullptr;
+    if (d_index && t.enc_mode != ENC_FIXED16) {
+        hipError_t e = hipMemsetAsync(d_index + nblocks + 1, 0, 8, s);  // max_bits, raised per block
+        if (e != hipSuccess) return e;
+    }
     if (t.enc_mode == ENC_FIXED16) {
         static bool attr_fixed = false;
         if (!attr_fixed) {
@@ -754,8 +764,8 @@ struct DecArgs {
     const unsigned long long* starts;  // block index (hz_internal.h)
     const uint32_t* subs;
     const uint32_t* lds_img;
-    uint32_t lds_words;      // table words; the staging slots follow
-    uint32_t stage_words;    // per wave
+    uint32_t lds_words;      // table words; the staging region follows
+    uint32_t region_words;   // staging region per workgroup (slots sized in-kernel from max_bits)
     int k;
     int min_len;
     int max_len;
@@ -809,10 +819,15 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
-    const uint32_t nw = blockDim.x >> 6;
-    uint32_t* stg = lds + a.lds_words + (threadIdx.x >> 6) * a.stage_words;
-    const uint32_t npc_max = a.stage_words >> 2;
-    for (uint64_t b = (uint64_t)blockIdx.x * nw + (threadIdx.x >> 6); b < a.nblocks; b += (uint64_t)gridDim.x * nw) {
+    const uint32_t wid = threadIdx.x >> 6;
+    // slots fit the stream's largest block; waves without a slot have nothing to do
+    const uint32_t slot = dec_slot_words(a.starts[a.nblocks + 1], a.max_len);
+    uint32_t nw = a.region_words / slot;
+    nw = nw < (blockDim.x >> 6) ? nw : (blockDim.x >> 6);
+    if (wid >= nw) return;
+    uint32_t* stg = lds + a.lds_words + wid * slot;
+    const uint32_t npc_max = slot >> 2;
+    for (uint64_t b = (uint64_t)blockIdx.x * nw + wid; b < a.nblocks; b += (uint64_t)gridDim.x * nw) {
         const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
         const uint32_t sub = a.subs[b * kWave + lane];
         // ---- stage words [w0, w0 + 4 npc) of the payload, byte-swapped
@@ -979,15 +994,19 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
     a.nblocks = index_blocks(nsym);
     a.lds_img = t.d_dec_lds;
     a.lds_words = t.dec_lds_bytes / 4;
-    a.stage_words = dec_stage_words(t.dec_max_len);
     a.k = t.dec_k;
     a.min_len = t.dec_min_len;
     a.max_len = t.dec_max_len;
     a.l2 = t.d_dec_l2;
 }
 
+// Launch shape: slots are sized for the average block (estimated from the
+// payload size) with headroom; the kernel sizes the real slots from the
+// index's max_bits and idles the waves that do not get one. Up to two
+// workgroups per CU (each holds its own table copy): whichever shape runs
+// more waves.
 template <int MODE, bool WIDE>
-static hipError_t run_decode(const DecArgs& a, int waves, int ncu, hipStream_t s) {
+static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE>,
@@ -995,12 +1014,29 @@ static hipError_t run_decode(const DecArgs& a, int waves, int ncu, hipStream_t s
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const uint32_t lds = 4 * (a.lds_words + (uint32_t)waves * a.stage_words);
-    const uint64_t per_cu = kLdsBytes / lds;
-    uint64_t wgs = (a.nblocks + waves - 1) / waves;
-    const uint64_t cap = (uint64_t)ncu * (per_cu ? per_cu : 1);
+    const uint64_t avg = (payload_bits + a.nblocks - 1) / a.nblocks;
+    const uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
+    const uint32_t worst = dec_slot_words_max(a.max_len);
+    const uint32_t table = a.lds_words;
+    int best_w = 0, best_g = 1;
+    for (int g = 1; g <= 2; ++g) {
+        const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
+        if (room <= table + est) continue;
+        int w = (int)((room - table) / est);
+        w = w > kDecMaxWaves ? kDecMaxWaves : w;
+        if (g * w > best_g * best_w) { best_w = w; best_g = g; }
+    }
+    if (best_w == 0) return hipErrorInvalidValue;
+    DecArgs b = a;
+    b.region_words = (uint32_t)best_w * est;
+    if (b.region_words < worst && table + worst <= kLdsBytes / 4) b.region_words = worst;  // any stream decodes
+    if (table + b.region_words > kLdsBytes / 4 / (uint32_t)best_g) best_g = 1;
+    if (table + b.region_words > kLdsBytes / 4) return hipErrorInvalidValue;
+    const uint32_t lds = 4 * (table + b.region_words);
+    uint64_t wgs = (a.nblocks + best_w - 1) / best_w;
+    const uint64_t cap = (uint64_t)ncu * best_g;
     if (wgs > cap) wgs = cap;
-    hipLaunchKernelGGL((k_decode<MODE, WIDE>), dim3(wgs), dim3(64 * waves), lds, s, a);
+    hipLaunchKernelGGL((k_decode<MODE, WIDE>), dim3(wgs), dim3(64 * best_w), lds, s, b);
     return hipGetLastError();
 }
 
@@ -1011,7 +1047,7 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = d_index;
-    a.subs = reinterpret_cast<const uint32_t*>(d_index + a.nblocks + 1);
+    a.subs = reinterpret_cast<const uint32_t*>(d_index + index_sub_offset(a.nblocks));
     a.out = d_out; a.err = d_err;
     if (t.dec_mode == DEC_FIXED16) {
         static bool attr = false;
@@ -1027,11 +1063,10 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
         hipLaunchKernelGGL(k_decode_fixed16, dim3(wgs), dim3(1024), kFixed16LdsBytes, s, a);
         return hipGetLastError();
     }
-    const int waves = t.dec_waves;
-    if (waves <= 0) return hipErrorInvalidValue;
+    const uint64_t pbits = payload_bytes * 8;
     const bool wide = t.dec_max_len > 32;
-    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false>(a, waves, ncu, s);
-    return wide ? run_decode<DEC_LUT, true>(a, waves, ncu, s) : run_decode<DEC_LUT, false>(a, waves, ncu, s);
+    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false>(a, pbits, ncu, s);
+    return wide ? run_decode<DEC_LUT, true>(a, pbits, ncu, s) : run_decode<DEC_LUT, false>(a, pbits, ncu, s);
 }
 
 // Serial index build for an index-less stream: one lane walks the stream and
@@ -1063,11 +1098,15 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
         r.nxt = ld_word(a, w + 2);
         r.wpos = w + 3;
     }
-    uint64_t bstart = 0;
+    uint64_t bstart = 0, maxb = 0;
     uint32_t lo = 0;
     for (uint64_t i = 0; i < a.nsym; ++i) {
         const uint32_t in_blk = (uint32_t)(i % kBlockSyms);
-        if (in_blk == 0) { starts[i / kBlockSyms] = pos; bstart = pos; }
+        if (in_blk == 0) {
+            if (i) maxb = pos - bstart > maxb ? pos - bstart : maxb;
+            starts[i / kBlockSyms] = pos;
+            bstart = pos;
+        }
         if (in_blk % kChainSyms == 0) {
             const uint32_t off = (uint32_t)(pos - bstart) & 0xffffu;
             uint32_t& w = subs[(i / kBlockSyms) * kWave + in_blk / kSPT];
@@ -1104,6 +1143,7 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
         else w = endoff;
     }
     starts[nb] = pos;
+    starts[nb + 1] = pos - bstart > maxb ? pos - bstart : maxb;
 }
 
 hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
@@ -1113,7 +1153,7 @@ hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = nullptr; a.subs = nullptr; a.out = nullptr; a.err = d_err;
-    uint32_t* subs = reinterpret_cast<uint32_t*>(d_index + a.nblocks + 1);
+    uint32_t* subs = reinterpret_cast<uint32_t*>(d_index + index_sub_offset(a.nblocks));
     const int m = t.dec_mode;
     const void* fn = m == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE>
                    : m == DEC_FIXED16 ? (const void*)k_index_serial<DEC_FIXED16> : (const void*)k_index_serial<DEC_LUT>;

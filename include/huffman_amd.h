@@ -117,7 +117,8 @@ int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
 /* Block index written by hz_pack / hz_index_build and read by hz_decode
  * (hz_index_bytes(nsym) bytes, 8-byte aligned): u64 start[nblocks + 1] -- the
  * absolute start bit of every hz_index_stride() = 2048-symbol block, then the
- * stream's end bit -- followed by u32 sub[nblocks][64]: the start bits of the
+ * stream's end bit -- then u64 max_bits, the largest block in bits (sizes the
+ * decoder's LDS slots), then u32 sub[nblocks][64]: the start bits of the
  * 16-symbol chains 2l and 2l+1 of the block relative to start[b], mod 2^16
  * (low and high half). The reference has no index (its decoder is serial,
  * Decompressor.cu:259-291); this is the side band that makes decode parallel. */
