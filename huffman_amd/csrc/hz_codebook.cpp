@@ -264,7 +264,7 @@ std::vector<uint32_t> build_enc_dense(const hz_codebook* cb) {
 
 // HOT: 32768 slots; symbols s and s ^ m share slot hot_slot(s, m). The slot
 // holds the shorter-coded (more frequent) of the pair when its code fits 25
-// bits: valid << 31 | (s >> 15) << 30 | L << 25 | code. m is chosen per
+// bits: (s >> 15) << 31 | L << 26 | code (L = 0: empty). m is chosen per
 // codebook to minimise the escaped probability mass (weight 2^-L).
 uint32_t choose_hot_mask(const hz_codebook* cb) {
     static const uint32_t cand[] = {0x8000, 0xffff, 0x8080, 0xc0c0, 0x80ff, 0xff80, 0xa0a0, 0xf0f0,
@@ -301,7 +301,7 @@ std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m) {
         }
         if (best >= 0) {
             const uint32_t s = (uint32_t)best;
-            img[slot] = (1u << 31) | ((s >> 15) << 30) | ((uint32_t)cb->len[s] << 25) | (uint32_t)cb->code[s];
+            img[slot] = ((s >> 15) << 31) | ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
         }
     }
     return img;

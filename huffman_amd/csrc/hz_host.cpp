@@ -236,6 +236,12 @@ extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
     t.max_len = (int)cb->max_len;
     t.min_len = (int)cb->min_len;
     const int mode = select_enc_mode(cb);
+    {
+        double avg = 0.0;
+        for (uint32_t s = 0; s < HZ_NSYM; ++s)
+            if (cb->len[s]) avg += ldexp(1.0, -(int)cb->len[s]) * cb->len[s];
+        t.enc_avg_bits = avg > 0.0 ? avg : 1.0;
+    }
     if (mode == ENC_FIXED16) {
         std::vector<uint32_t> img = build_enc_fixed16(cb);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);

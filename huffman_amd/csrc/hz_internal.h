@@ -10,8 +10,9 @@ namespace hz {
 constexpr int kWave = 64;
 constexpr int kSPT = 32;                       // symbols per lane (64 input bytes)
 constexpr int kBlockSyms = kWave * kSPT;       // 2048 symbols = 4 KiB of input
-constexpr int kChainSyms = 16;                 // decode chain: index granularity
-constexpr int kChainsPerBlock = kBlockSyms / kChainSyms;  // 128 (two per lane)
+constexpr int kChainsPerLane = 4;              // decode: independent chains per lane
+constexpr int kChainSyms = kSPT / kChainsPerLane;         // 8 symbols: index granularity
+constexpr int kChainsPerBlock = kBlockSyms / kChainSyms;  // 256
 constexpr int kPackThreads = 1024;             // 16 waves per CU share one LDS table
 constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
 
@@ -19,14 +20,14 @@ constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
 //   u64 start[nblocks + 1]      absolute start bit of every 2048-symbol block
 //                               (start[nblocks] = end of the stream)
 //   u64 max_bits                largest block (bits): sizes the decoder's LDS slots
-//   u32 sub[nblocks][64]        per lane: the start bits of its two 16-symbol
-//                               chains relative to start[b], mod 2^16 (low,
-//                               high half); exact when block bits < 2^16,
+//   u16 sub[nblocks][256]       start bit of every 8-symbol chain relative to
+//                               start[b], mod 2^16 (a lane's four chains are
+//                               one u64); exact when block bits < 2^16,
 //                               otherwise recovered by a prefix over deltas.
 __host__ __device__ inline uint64_t index_blocks(uint64_t nsym) { return (nsym + kBlockSyms - 1) / kBlockSyms; }
 __host__ __device__ inline uint64_t index_bytes(uint64_t nsym) {
     const uint64_t nb = index_blocks(nsym);
-    return nsym ? 8 * (nb + 2) + 4ull * kWave * nb : 0;
+    return nsym ? 8 * (nb + 2) + 2ull * kChainsPerBlock * nb : 0;
 }
 __host__ __device__ inline uint64_t index_sub_offset(uint64_t nblocks) { return nblocks + 2; }  // in u64 words
 
@@ -78,6 +79,7 @@ struct Tables {
     int dec_max_len = 0;           // of the codebook the decode tables were built for
     int dec_min_len = 0;
     uint32_t enc_lds_bytes = 0;
+    double enc_avg_bits = 16.0;    // Kraft estimate of bits per symbol: sum 2^-L * L
     uint32_t dec_lds_bytes = 0;
     uint32_t* d_enc_lds = nullptr; // LDS image for the pack kernel
     uint64_t* d_enc_wide = nullptr;// 65536 x u64: len << 56 | code

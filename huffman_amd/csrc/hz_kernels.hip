@@ -229,14 +229,13 @@ struct PackArgs {
     unsigned long long* blk;     // per block bit count (k_pack_count)
     const unsigned long long* blk_start;
     unsigned long long* index;   // block index start[] (optional, hz_internal.h)
-    uint32_t* index_sub;         // block index sub[] (chain offsets)
+    unsigned long long* index_sub;  // block index sub[] (four u16 chain offsets per lane)
     uint32_t* err;
+    uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
 };
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
 template <> struct PackEnt<ENC_WIDE> { using T = uint64_t; static constexpr int kShift = 56; };
-
-constexpr int pack_threads(int mode) { return mode == ENC_WIDE ? 512 : kPackThreads; }
 
 template <typename T, int SH>
 HZ_DEV T pack_dense_one(const uint32_t* lds, uint32_t s) {
@@ -248,24 +247,42 @@ HZ_DEV T pack_dense_one(const uint32_t* lds, uint32_t s) {
     return f ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
 }
 
-// Loads the lane's 32 symbols and looks up their (len, code). `xs` is one more
-// symbol whose entry is returned in `xe` from the same batch (the previous
-// block's tail symbols); all global loads of a block are issued before one wait.
+// The lane's 32 input symbols (64 bytes) of block `blk` and, for lanes 0..31,
+// one of the previous block's last 32 symbols. Issued one block ahead of use
+// (k_pack_write); lanes past a full run load from the buffer start and are
+// re-read byte by byte in pack_lookup.
+struct PackIn {
+    uint32_t raw[kSPT / 2];
+    uint32_t psym;
+    uint64_t bstart;
+};
+
+HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) {
+    const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+    const uint64_t ls = sym0 + kSPT <= a.nsym ? sym0 : 0;
+    const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ls);
+#pragma unroll
+    for (int q = 0; q < kSPT / 8; ++q) {
+        const uint4 v = p[q];
+        x.raw[4 * q] = v.x; x.raw[4 * q + 1] = v.y; x.raw[4 * q + 2] = v.z; x.raw[4 * q + 3] = v.w;
+    }
+    const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
+    x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
+    x.bstart = a.blk_start[blk];
+}
+
+// (len, code) of the lane's 32 symbols in register format (len << SH | code),
+// plus the entry of one more symbol `xs` (the previous block's tail). HOT
+// slots hold tag << 31 | len << 26 | code: the entry is a hit when the tag
+// matches bit 15 of the symbol and len != 0; misses (slot taken by the
+// partner symbol, or codes > 25 bits) come from the escape table, all issued
+// before one wait.
 template <int MODE>
-HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid,
-                             typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe) {
+HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid, uint32_t (&raw)[kSPT / 2],
+                        typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
-    constexpr T CMASK = (T(1) << SH) - 1;
-    uint32_t raw[kSPT / 2];
-    if (nvalid == kSPT) {
-        const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
-#pragma unroll
-        for (int q = 0; q < kSPT / 8; ++q) {
-            const uint4 v = p[q];
-            raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
-        }
-    } else {
+    if (nvalid < kSPT) {
 #pragma unroll
         for (int k = 0; k < kSPT / 2; ++k) {
             uint32_t w = 0;
@@ -288,22 +305,25 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
         }
         xe = pack_dense_one<T, SH>(lds, xs);
     } else if (MODE == ENC_HOT) {
+        const uint32_t m = a.hot_mask;
         uint32_t miss = 0;
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            const uint32_t v = lds[hot_slot(s, a.hot_mask)];
-            const bool hit = (v >> 30) == (2u | (s >> 15));
-            e[k] = k < nvalid ? (T)((((v >> 25) & 31u) << SH) | (v & 0x1ffffffu)) : (T)0;
+            const uint32_t slot = s ^ (m & (uint32_t)((int32_t)(s << 16) >> 31));
+            const uint32_t x = lds[slot] ^ ((s << 16) & 0x80000000u);
+            const bool hit = x - 0x04000000u < 0x7c000000u;  // tag matches and len != 0
+            e[k] = k < nvalid ? (T)x : (T)0;
             if (!hit && k < nvalid) miss |= 1u << k;
         }
-        const uint32_t xv = lds[hot_slot(xs, a.hot_mask)];
-        const bool xmiss = (xv >> 30) != (2u | (xs >> 15));
-        xe = (T)((((xv >> 25) & 31u) << SH) | (xv & 0x1ffffffu));
+        const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
+        const uint32_t xx = lds[xslot] ^ ((xs << 16) & 0x80000000u);
+        const bool xmiss = !(xx - 0x04000000u < 0x7c000000u);
+        xe = (T)xx;
         if (miss | (uint32_t)xmiss) {
-            // Escapes (slot collisions, codes > 25 bits). The escape table holds
-            // entries in the register format, so each load lands in its e[k]
-            // directly and the single wait falls at the first use (the scan).
+            // The escape table holds entries in the register format, so each
+            // load lands in its e[k] directly and the single wait falls at the
+            // first use.
 #pragma unroll
             for (int k = 0; k < kSPT; ++k)
                 if ((miss >> k) & 1u) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
@@ -316,34 +336,6 @@ HZ_DEV void pack_load_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sy
             e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
         }
         xe = (T)a.wide[xs];
-    }
-}
-
-// Lane bit count + last 32 bits, then the wave's inclusive scan of (bits, tail).
-template <int MODE>
-HZ_DEV void pack_lane_scan(const typename PackEnt<MODE>::T (&e)[kSPT], int lane, uint32_t& n, uint32_t& nA,
-                           uint32_t& sn, uint32_t& st) {
-    using T = typename PackEnt<MODE>::T;
-    constexpr int SH = PackEnt<MODE>::kShift;
-    constexpr T CMASK = (T(1) << SH) - 1;
-    n = 0;
-    uint64_t t64 = 0;
-#pragma unroll
-    for (int k = 0; k < kSPT; ++k) {
-        const uint32_t L = (uint32_t)(e[k] >> SH);
-        n += L;
-        if (k == kChainSyms - 1) nA = n;  // bits of the lane's first decode chain
-        t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
-    }
-    sn = n;
-    st = (uint32_t)t64;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t on = shfl_up_u32(sn, d), ot = shfl_up_u32(st, d);
-        if (lane >= d) {
-            st = sn >= 32 ? st : (sn == 0 ? ot : ((ot << sn) | st));
-            sn += on;
-        }
     }
 }
 
@@ -420,30 +412,76 @@ __global__ __launch_bounds__(kCountThreads) void k_pack_count(PackArgs a) {
     }
 }
 
+// Emits the lane's codes into `dst` (LDS slot or global words) starting with
+// `na` bits pending in `acc`; every completed 32-bit word is stored.
+template <int MODE, bool TO_LDS, typename P>
+HZ_DEV void pack_emit(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& acc, uint32_t& na, P dst, bool ok) {
+    using T = typename PackEnt<MODE>::T;
+    constexpr int SH = PackEnt<MODE>::kShift;
+    constexpr T CMASK = (T(1) << SH) - 1;
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        const uint32_t L = (uint32_t)(e[k] >> SH);
+        const uint64_t c = (uint64_t)(e[k] & CMASK);
+        if (MODE == ENC_WIDE && L > 32) {
+            const uint32_t Lh = L - 32;
+            acc = (acc << Lh) | (c >> 32);
+            na += Lh;
+            if (na >= 32) { na -= 32; const uint32_t w = (uint32_t)(acc >> na); if (ok) *dst = TO_LDS ? w : bswap32(w); ++dst; }
+            acc = (acc << 32) | (c & 0xffffffffull);
+            na += 32;
+            if (na >= 32) { na -= 32; const uint32_t w = (uint32_t)(acc >> na); if (ok) *dst = TO_LDS ? w : bswap32(w); ++dst; }
+        } else if (L) {
+            acc = (acc << L) | c;
+            na += L;
+            if (na >= 32) { na -= 32; const uint32_t w = (uint32_t)(acc >> na); if (ok) *dst = TO_LDS ? w : bswap32(w); ++dst; }
+        }
+    }
+}
+
+constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
+
 template <int MODE>
-__global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
+__global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
+    // Output slot of this wave: the block's words are assembled in LDS and
+    // leave as contiguous 256-byte stores (a block that does not fit, and the
+    // stream's last block, store straight from the lanes).
+    uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t max_bits = 0;  // largest block of this wave (index max_bits: one atomic per wave)
-    for (uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); blk < a.nblocks; blk += W) {
+    uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    PackIn nx;  // the next block's inputs, in flight while this block is packed
+    if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
+    for (; blk < a.nblocks; blk += W) {
         const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
         const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
-        // independent loads first: block start, previous block's last 32 symbols
-        const uint64_t bstart = a.blk_start[blk];
-        const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
-        const uint32_t psym = (uint32_t)a.in[2 * ps] | ((uint32_t)a.in[2 * ps + 1] << 8);
+        PackIn cur = nx;
+        const uint64_t bstart = cur.bstart;
         T e[kSPT];
         T pe;
-        pack_load_lookup<MODE>(a, lds, sym0, nvalid, e, psym, pe);
-        uint32_t n, nA, sn, st;
-        pack_lane_scan<MODE>(e, lane, n, nA, sn, st);
-        uint32_t ex_n = shfl_up_u32(sn, 1), ex_t = shfl_up_u32(st, 1);
-        if (lane == 0) { ex_n = 0; ex_t = 0; }
+        pack_lookup<MODE>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
+        // next block's loads: after this block's escapes, so no wait covers them early
+        pack_prefetch(a, blk + W < a.nblocks ? blk + W : blk, lane, nx);
+        // lane bits, decode-chain offsets, wave scan of the bit counts
+        uint32_t n = 0, nc[kChainsPerLane];
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            if (k % kChainSyms == 0) nc[k / kChainSyms] = n;
+            n += (uint32_t)(e[k] >> SH);
+        }
+        uint32_t sn = n;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = shfl_up_u32(sn, d);
+            if (lane >= d) sn += o;
+        }
+        const uint32_t ex_n = sn - n;
         const uint64_t bend = bstart + shfl_u32(sn, 63);
         // The 32 bits before the block: codes of the previous block's last 32
         // symbols (each code >= 1 bit), combined across lanes 0..31.
@@ -462,38 +500,64 @@ __global__ __launch_bounds__(pack_threads(MODE)) void k_pack_write(PackArgs a) {
             ptail = shfl_u32(pt, 31);
         }
         const uint64_t o = bstart + ex_n;
-        const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
-        uint32_t na = (uint32_t)(o & 31);
-        uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
         // every word this block writes lies below ceil(bend / 32)
         const bool fits = ((bend + 31) >> 5) <= a.out_words;
         if (!fits && lane == 0) atomicOr(a.err, 4u);
-        uint32_t* dst = a.out + (o >> 5);
+        const bool last = blk + 1 == a.nblocks;
+        const uint64_t wfirst = bstart >> 5;
+        const uint32_t nwords = (uint32_t)((bend >> 5) - wfirst);  // words completed inside the block
+        if (slot && !last && nwords <= a.slot_words) {
+            // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
+            // own: emit with the leading bits zero, then OR in the previous
+            // lane's tail once all lanes are done.
+            uint32_t na = (uint32_t)(o & 31);
+            uint64_t acc = 0;
+            pack_emit<MODE, true>(e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
+            uint32_t prev = shfl_up_u32((uint32_t)acc, 1);
+            if (lane == 0) prev = ptail;
+            const uint32_t h = (uint32_t)(o & 31);
+            if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
+            __builtin_amdgcn_wave_barrier();
+            if (fits)
+                for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            // direct path: each lane needs the 32 bits before its run from the
+            // (bits, tail) scan, since a lane of the last block may hold < 32 bits
+            uint64_t t64 = 0;
 #pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            const uint32_t L = (uint32_t)(e[k] >> SH);
-            const uint64_t c = (uint64_t)(e[k] & CMASK);
-            if (MODE == ENC_WIDE && L > 32) {
-                const uint32_t Lh = L - 32;
-                acc = (acc << Lh) | (c >> 32);
-                na += Lh;
-                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
-                acc = (acc << 32) | (c & 0xffffffffull);
-                na += 32;
-                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
-            } else if (L) {
-                acc = (acc << L) | c;
-                na += L;
-                if (na >= 32) { na -= 32; if (fits) *dst = bswap32((uint32_t)(acc >> na)); ++dst; }
+            for (int k = 0; k < kSPT; ++k) {
+                const uint32_t L = (uint32_t)(e[k] >> SH);
+                t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
             }
+            uint32_t tn = n, st = (uint32_t)t64;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t on = shfl_up_u32(tn, d), ot = shfl_up_u32(st, d);
+                if (lane >= d) {
+                    st = tn >= 32 ? st : (tn == 0 ? ot : ((ot << tn) | st));
+                    tn += on;
+                }
+            }
+            uint32_t ex_t = shfl_up_u32(st, 1);
+            if (lane == 0) ex_t = 0;
+            const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
+            uint32_t na = (uint32_t)(o & 31);
+            uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
+            uint32_t* dst = a.out + (o >> 5);
+            pack_emit<MODE, false>(e, acc, na, dst, fits);
+            dst += (uint32_t)(((o & 31) + n) >> 5);
+            if (fits && nvalid > 0 && sym0 + (uint64_t)nvalid == a.nsym && na > 0)
+                *dst = bswap32((uint32_t)(acc << (32 - na)));
         }
-        if (fits && nvalid > 0 && sym0 + (uint64_t)nvalid == a.nsym && na > 0)
-            *dst = bswap32((uint32_t)(acc << (32 - na)));
-        if (a.index) {  // block index (hz_internal.h): start bits + the lane's two chain offsets
-            a.index_sub[blk * kWave + lane] = (ex_n & 0xffffu) | (((ex_n + nA) & 0xffffu) << 16);
+        if (a.index) {  // block index (hz_internal.h): start bits + the lane's chain offsets
+            uint64_t sub = 0;
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c) sub |= (uint64_t)((ex_n + nc[c]) & 0xffffu) << (16 * c);
+            a.index_sub[blk * kWave + lane] = sub;
             if (lane == 0) {
                 a.index[blk] = bstart;
-                if (blk + 1 == a.nblocks) a.index[a.nblocks] = bend;
+                if (last) a.index[a.nblocks] = bend;
             }
             max_bits = bend - bstart > max_bits ? bend - bstart : max_bits;
         }
@@ -574,8 +638,13 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
             const uint32_t lane = (uint32_t)(j % kWave);
             const uint32_t cnt = (uint32_t)(a.nsym - blk * kBlockSyms < (uint64_t)kBlockSyms ? a.nsym - blk * kBlockSyms
                                                                                         : (uint64_t)kBlockSyms);
-            const uint32_t ca = 32 * lane < cnt ? 32 * lane : cnt, cb = 32 * lane + 16 < cnt ? 32 * lane + 16 : cnt;
-            a.index_sub[j] = ((16 * ca) & 0xffffu) | (((16 * cb) & 0xffffu) << 16);
+            uint64_t sub = 0;
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c) {
+                const uint32_t at = kSPT * lane + kChainSyms * c;
+                sub |= (uint64_t)((16 * (at < cnt ? at : cnt)) & 0xffffu) << (16 * c);
+            }
+            a.index_sub[j] = sub;
             if (lane == 0) a.index[blk] = start_bit + (uint64_t)blk * kBlockSyms * 16;
             if (j + 1 == nl) a.index[a.nblocks] = start_bit + 16 * a.nsym;
             if (j == 0) a.index[a.nblocks + 1] = 16ull * (a.nsym < (uint64_t)kBlockSyms ? a.nsym : (uint64_t)kBlockSyms);
@@ -680,7 +749,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     unsigned long long* blk_start = d_scratch + nblocks;
     unsigned long long* tiles = d_scratch + 2 * nblocks;
     a.blk_start = blk_start; a.index = d_index; a.err = d_err;
-    a.index_sub = d_index ? reinterpret_cast<uint32_t*>(d_index + index_sub_offset(nblocks)) : nullptr;
+    a.index_sub = d_index ? d_index + index_sub_offset(nblocks) : nullptr;
     if (d_index && t.enc_mode != ENC_FIXED16) {
         hipError_t e = hipMemsetAsync(d_index + nblocks + 1, 0, 8, s);  // max_bits, raised per block
         if (e != hipSuccess) return e;
@@ -699,12 +768,23 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
         hipLaunchKernelGGL(k_pack_fixed16, dim3(wgs), dim3(kPackThreads), kFixed16LdsBytes, s, a, start_bit);
         return hipGetLastError();
     }
-    const int threads = t.enc_mode == ENC_WIDE ? pack_threads(ENC_WIDE) : kPackThreads;
-    const uint64_t waves = (uint64_t)threads / 64;
+    // Waves per workgroup: as many output slots of the expected block size
+    // (Kraft estimate from the code lengths, +12 %) as fit beside the table.
+    const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
+    a.lds_words = table_words;
+    const uint32_t free_words = kLdsBytes / 4 - table_words;
+    const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * 1.12 / 32.0) + 4;
+    constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
+    uint32_t waves = free_words / est_words;
+    waves = waves > kMaxWaves ? kMaxWaves : waves;
+    a.slot_words = 0;
+    if (waves >= 6) a.slot_words = free_words / waves;
+    else waves = kMaxWaves;  // no room for slots: lanes store directly
+    const int threads = (int)waves * 64;
     uint64_t wgs = (nblocks + waves - 1) / waves;
-    const uint64_t cap = (uint64_t)ncu * (t.enc_mode == ENC_WIDE ? 4 : 1);  // LDS table: one WG per CU
+    const uint32_t lds = 4 * (table_words + waves * a.slot_words);
+    const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
-    const uint32_t lds = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes;
     static bool attr[3] = {false, false, false};
     static bool attr_count = false;
     if (!attr_count) {
@@ -762,7 +842,7 @@ struct DecArgs {
     uint64_t nsym;
     uint64_t nblocks;
     const unsigned long long* starts;  // block index (hz_internal.h)
-    const uint32_t* subs;
+    const unsigned long long* subs;    // four u16 chain offsets per lane
     const uint32_t* lds_img;
     uint32_t lds_words;      // table words; the staging region follows
     uint32_t region_words;   // staging region per workgroup (slots sized in-kernel from max_bits)
@@ -829,7 +909,7 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     const uint32_t npc_max = slot >> 2;
     for (uint64_t b = (uint64_t)blockIdx.x * nw + wid; b < a.nblocks; b += (uint64_t)gridDim.x * nw) {
         const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
-        const uint32_t sub = a.subs[b * kWave + lane];
+        const uint64_t sub = a.subs[b * kWave + lane];
         // ---- stage words [w0, w0 + 4 npc) of the payload, byte-swapped
         const uint64_t w0 = (b0 >> 5) & ~3ull;
         const uint64_t wend = (b1 >> 5) + (WIDE ? 3 : 2);
@@ -850,38 +930,44 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
         }
         __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
         // ---- chain start bits, relative to the slot
-        uint32_t oA = sub & 0xffffu, oB = sub >> 16;
-        if (b1 - b0 >= 65536) {  // offsets are mod 2^16: rebuild them from deltas
-            uint32_t pv = shfl_up_u32(oB, 1);
-            if (lane == 0) pv = 0;
-            const uint32_t dA = (oA - pv) & 0xffffu, dB = (oB - oA) & 0xffffu;
-            uint32_t sc = dA + dB;
+        constexpr int C = kChainsPerLane;
+        uint32_t off[C];
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = shfl_up_u32(sc, d);
-                if (lane >= d) sc += o;
+        for (int c = 0; c < C; ++c) off[c] = (uint32_t)(sub >> (16 * c)) & 0xffffu;
+        if (b1 - b0 >= 65536) {  // offsets are mod 2^16: rebuild them from deltas
+            uint32_t pv = shfl_up_u32(off[C - 1], 1);
+            if (lane == 0) pv = 0;
+            uint32_t d[C], sc = 0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) { d[c] = (off[c] - pv) & 0xffffu; pv = off[c]; sc += d[c]; }
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t o = shfl_up_u32(sc, dd);
+                if (lane >= dd) sc += o;
             }
-            oB = sc;
-            oA = sc - dB;
+#pragma unroll
+            for (int c = C - 1; c >= 0; --c) { off[c] = sc; sc -= d[c]; }
         }
         const uint32_t base = (uint32_t)(b0 - (w0 << 5));
-        uint32_t pos[2] = {base + oA, base + oB};
+        uint32_t pos[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) pos[c] = base + off[c];
         uint32_t pk[kSPT / 2];
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
-            uint64_t win[2];
-            uint32_t sym[2], L[2];
+            uint64_t win[C];
+            uint32_t sym[C], L[C];
 #pragma unroll
-            for (int c = 0; c < 2; ++c) win[c] = stage_window<WIDE>(stg, pos[c]);
+            for (int c = 0; c < C; ++c) win[c] = stage_window<WIDE>(stg, pos[c]);
             if (MODE == DEC_DENSE) {
 #pragma unroll
-                for (int c = 0; c < 2; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
+                for (int c = 0; c < C; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
             } else {
-                uint32_t e[2], e2[2];
+                uint32_t e[C], e2[C];
 #pragma unroll
-                for (int c = 0; c < 2; ++c) e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))];
+                for (int c = 0; c < C; ++c) e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))];
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {  // first deeper level of both chains before one wait
+                for (int c = 0; c < C; ++c) {  // first deeper level of every chain before one wait
                     e2[c] = e[c];
                     if (!(e[c] >> 31)) {
                         const uint32_t nb = (e[c] >> 26) & 31u;
@@ -889,7 +975,7 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
                     }
                 }
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {
+                for (int c = 0; c < C; ++c) {
                     uint32_t ee = e2[c];
                     if (!(e[c] >> 31)) {
                         uint32_t D = (uint32_t)a.k + ((e[c] >> 26) & 31u);
@@ -904,10 +990,11 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
                 }
             }
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
+            for (int c = 0; c < C; ++c) {
                 pos[c] += L[c];
-                if (q & 1) pk[c * 8 + (q >> 1)] |= sym[c] << 16;
-                else pk[c * 8 + (q >> 1)] = sym[c];
+                const int i = (c * kChainSyms + q) >> 1;  // symbol c*8+q of the lane
+                if (q & 1) pk[i] |= sym[c] << 16;
+                else pk[i] = sym[c];
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1047,7 +1134,7 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = d_index;
-    a.subs = reinterpret_cast<const uint32_t*>(d_index + index_sub_offset(a.nblocks));
+    a.subs = d_index + index_sub_offset(a.nblocks);
     a.out = d_out; a.err = d_err;
     if (t.dec_mode == DEC_FIXED16) {
         static bool attr = false;
@@ -1083,7 +1170,7 @@ struct BitReader {
 HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) { return w < a.nwords ? bswap32(a.words[w]) : 0u; }
 
 template <int MODE>
-__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* starts, uint32_t* subs) {
+__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* starts, uint16_t* subs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     if (threadIdx.x != 0) return;
@@ -1099,7 +1186,6 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
         r.wpos = w + 3;
     }
     uint64_t bstart = 0, maxb = 0;
-    uint32_t lo = 0;
     for (uint64_t i = 0; i < a.nsym; ++i) {
         const uint32_t in_blk = (uint32_t)(i % kBlockSyms);
         if (in_blk == 0) {
@@ -1107,12 +1193,8 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
             starts[i / kBlockSyms] = pos;
             bstart = pos;
         }
-        if (in_blk % kChainSyms == 0) {
-            const uint32_t off = (uint32_t)(pos - bstart) & 0xffffu;
-            uint32_t& w = subs[(i / kBlockSyms) * kWave + in_blk / kSPT];
-            if ((in_blk / kChainSyms) & 1) w = lo | (off << 16);
-            else { lo = off; w = off; }
-        }
+        if (in_blk % kChainSyms == 0)
+            subs[(i / kBlockSyms) * kChainsPerBlock + in_blk / kChainSyms] = (uint16_t)(pos - bstart);
         if (r.nb <= 32) {
             r.buf |= (uint64_t)r.nxt << (32 - r.nb);
             r.nb += 32;
@@ -1136,12 +1218,8 @@ __global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long
     // chains past the end of a tail block start at the end
     const uint64_t nb = a.nblocks;
     const uint32_t tail = (uint32_t)(a.nsym - (nb - 1) * kBlockSyms);
-    const uint32_t endoff = (uint32_t)(pos - bstart) & 0xffffu;
-    for (uint32_t c = (tail + kChainSyms - 1) / kChainSyms; c < (uint32_t)kChainsPerBlock; ++c) {
-        uint32_t& w = subs[(nb - 1) * kWave + c / 2];
-        if (c & 1) w = (w & 0xffffu) | (endoff << 16);
-        else w = endoff;
-    }
+    for (uint32_t c = (tail + kChainSyms - 1) / kChainSyms; c < (uint32_t)kChainsPerBlock; ++c)
+        subs[(nb - 1) * kChainsPerBlock + c] = (uint16_t)(pos - bstart);
     starts[nb] = pos;
     starts[nb + 1] = pos - bstart > maxb ? pos - bstart : maxb;
 }
@@ -1153,7 +1231,7 @@ hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = nullptr; a.subs = nullptr; a.out = nullptr; a.err = d_err;
-    uint32_t* subs = reinterpret_cast<uint32_t*>(d_index + index_sub_offset(a.nblocks));
+    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
     const int m = t.dec_mode;
     const void* fn = m == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE>
                    : m == DEC_FIXED16 ? (const void*)k_index_serial<DEC_FIXED16> : (const void*)k_index_serial<DEC_LUT>;

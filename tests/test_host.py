@@ -118,9 +118,9 @@ def test_header_parse_empty_conventions(built_lib):
 
 
 def test_index_geometry(built_lib):
-    """Block index: u64 start[nblocks + 1] + u64 max_bits + u32 sub[nblocks][64] (include/huffman_amd.h)."""
+    """Block index: u64 start[nblocks + 1] + u64 max_bits + u16 sub[nblocks][256] (include/huffman_amd.h)."""
     assert built_lib.hz_index_stride() == 2048
     assert built_lib.hz_index_bytes(0) == 0
-    assert built_lib.hz_index_bytes(1) == 8 * 3 + 256
-    assert built_lib.hz_index_bytes(2049) == 8 * 4 + 2 * 256
-    assert built_lib.hz_index_bytes(1 << 33) == 8 * ((1 << 22) + 2) + 256 * (1 << 22)
+    assert built_lib.hz_index_bytes(1) == 8 * 3 + 512
+    assert built_lib.hz_index_bytes(2049) == 8 * 4 + 2 * 512
+    assert built_lib.hz_index_bytes(1 << 33) == 8 * ((1 << 22) + 2) + 512 * (1 << 22)
