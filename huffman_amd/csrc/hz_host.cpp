@@ -361,9 +361,11 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     if (!d_payload || !d_index) return HZ_EINVAL;
     if (c->t.dec_mode < 0) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
+    int rc = ensure_scratch(c, index_scratch_words(payload_bytes, start_bit));
+    if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][0], c->stream));
-    HZ_TRY(launch_index_serial(c->t, d_payload, payload_bytes, start_bit, nsym,
-                               reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->stream));
+    HZ_TRY(launch_index_build(c->t, d_payload, payload_bytes, start_bit, nsym,
+                              reinterpret_cast<unsigned long long*>(d_index), c->d_desc, c->d_err, c->ncu, c->stream));
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][1], c->stream));
     c->ev_used[HZ_STAGE_INDEX] = true;
     return arm_err_check(c);

@@ -108,9 +108,10 @@ uint64_t pack_scratch_words(uint64_t nsym);  // u64 words of d_scratch hz_pack n
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                          uint64_t nsym, const unsigned long long* d_index, uint8_t* d_out,
                          uint32_t* d_err, int ncu, hipStream_t s);
-hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index,
-                               uint32_t* d_err, hipStream_t s);
+hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                              uint64_t start_bit, uint64_t nsym, unsigned long long* d_index,
+                              unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
+uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
 hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
                            const unsigned long long* d_thr, hipStream_t s);
 

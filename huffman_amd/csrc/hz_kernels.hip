@@ -3,7 +3,7 @@
 //   k_hist16   65 536-bin histogram of u16 symbols      <- Compressor.cu:38-48
 //   k_pack     codeword lookup + bit-length scan + pack  <- Compressor.cu:50-61,541-576,182-313
 //   k_decode   block-parallel table decode              <- Decompressor.cu:259-291
-//   k_index_serial  decode-unit index of an index-less stream (reference files)
+//   k_sync_*   block index of an index-less stream (reference files), parallel, self-synchronising
 //   k_generate synthetic Zipf / uniform byte streams (this build's generator)
 //
 // Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
@@ -1156,10 +1156,28 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     return wide ? run_decode<DEC_LUT, true>(a, pbits, ncu, s) : run_decode<DEC_LUT, false>(a, pbits, ncu, s);
 }
 
-// Serial index build for an index-less stream: one lane walks the stream and
-// records the start bit of every block and the offset of every 16-symbol
-// chain. Correct for any stream; used for reference-produced files (the
-// parallel self-synchronising builder is the next step).
+// ===========================================================================
+// Block index of an index-less stream (a .compressed file from the reference
+// encoder, Decompressor.cu:259-291 decodes it serially). Huffman codes
+// resynchronise: a decoder started at an arbitrary bit falls onto the true
+// codeword boundaries after a few codewords. The stream is cut into 4096-bit
+// segments, one lane each:
+//   k_sync_scan : decode segment k from its first bit to the first boundary
+//                 past its end -> exit[k], count[k], and a bitmap of the
+//                 boundaries in its first 256 bits
+//   k_sync_fix  : the true path enters segment k at exit[k-1]; if that bit is
+//                 a boundary of k's own path the two paths coincide from there
+//                 on, and count[k] drops the boundaries before it; otherwise
+//                 k is queued for the serial fixer (rare)
+//   k_sync_serial: redecodes queued segments from their true entry, in order
+//   k_scan_*    : exclusive scan of counts -> first symbol number per segment
+//   k_sync_emit : decode every segment again from its true entry and write
+//                 block starts and raw chain positions
+//   k_sync_subs : chain positions relative to their block, max block bits
+// ===========================================================================
+constexpr uint32_t kSegBits = 4096;
+constexpr uint32_t kSyncBits = 256;  // boundary bitmap per segment (8 words)
+
 struct BitReader {
     uint64_t buf;
     uint32_t nb;
@@ -1169,85 +1187,291 @@ struct BitReader {
 
 HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) { return w < a.nwords ? bswap32(a.words[w]) : 0u; }
 
+HZ_DEV void br_init(BitReader& r, const DecArgs& a, uint64_t p) {
+    const uint64_t w = p >> 5;
+    const uint32_t sh = (uint32_t)(p & 31);
+    r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
+    r.nb = 64 - sh;
+    r.nxt = ld_word(a, w + 2);
+    r.wpos = w + 3;
+}
+
+// Length (and symbol) of the codeword at the reader, then advance past it.
 template <int MODE>
-__global__ void k_index_serial(DecArgs a, uint64_t start_bit, unsigned long long* starts, uint16_t* subs) {
+HZ_DEV uint32_t br_next(BitReader& r, const DecArgs& a, const uint32_t* lds, uint32_t& sym) {
+    if (r.nb <= 32) {
+        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+        r.nb += 32;
+        r.nxt = ld_word(a, r.wpos++);
+    }
+    const uint64_t win = r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
+    uint32_t L;
+    dec_lookup<MODE>(a, lds, win, sym, L);
+    if (L < r.nb) {
+        r.buf <<= L;
+        r.nb -= L;
+    } else {
+        const uint32_t rr = L - r.nb;
+        r.buf = (uint64_t)r.nxt << (32 + rr);
+        r.nb = 32 - rr;
+        r.nxt = ld_word(a, r.wpos++);
+    }
+    return L;
+}
+
+struct SyncArgs {
+    uint64_t start;                 // stream bit of the first symbol (payload view: + bit_adj)
+    uint64_t nseg;
+    unsigned long long* exitp;      // first boundary >= segment end, on the path taken
+    unsigned long long* cnt;        // symbols on that path inside the segment
+    uint32_t* bmp;                  // boundaries in the segment's first 256 bits
+    uint32_t* queue;                // segments whose entry is not on their own path
+    uint32_t* nqueue;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sync_scan(DecArgs a, SyncArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
+        const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
+        BitReader r;
+        br_init(r, a, s0 + a.bit_adj);
+        uint64_t pos = s0, n = 0;
+        uint32_t bm[kSyncBits / 32];
+#pragma unroll
+        for (int i = 0; i < (int)(kSyncBits / 32); ++i) bm[i] = 0;
+        while (pos < s1) {
+            const uint64_t d = pos - s0;
+            if (d < kSyncBits) {
+#pragma unroll
+                for (int i = 0; i < (int)(kSyncBits / 32); ++i)
+                    if ((uint32_t)(d >> 5) == (uint32_t)i) bm[i] |= 1u << (d & 31);
+            }
+            uint32_t sym;
+            const uint32_t L = br_next<MODE>(r, a, lds, sym);
+            if (L == 0) { atomicOr(a.err, 2u); break; }
+            pos += L;
+            ++n;
+        }
+        y.exitp[k] = pos;
+        y.cnt[k] = n;
+#pragma unroll
+        for (int i = 0; i < (int)(kSyncBits / 32); ++i) y.bmp[k * (kSyncBits / 32) + i] = bm[i];
+    }
+}
+
+HZ_DEV uint32_t bits_below(const uint32_t* bm, uint32_t d) {  // boundaries before offset d (< 256)
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < (d >> 5); ++i) c += __popc(bm[i]);
+    if (d & 31) c += __popc(bm[d >> 5] & ((1u << (d & 31)) - 1u));
+    return c;
+}
+
+// The true path enters segment k at e = exit[k-1]. Follow it codeword by
+// codeword until it lands on a boundary of k's own path (in the bitmap); from
+// there the two coincide, so the true count is k's count minus its boundaries
+// before that point plus the true-path codewords walked. No landing within
+// the first 256 bits (rare): queue k for the serial fixer.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sync_fix(DecArgs a, SyncArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
+        const uint64_t s0 = y.start + k * kSegBits;
+        const uint32_t* bm = y.bmp + k * (kSyncBits / 32);
+        uint64_t p = y.exitp[k - 1];
+        uint64_t walked = 0;
+        bool synced = false;
+        BitReader r;
+        br_init(r, a, p + a.bit_adj);
+        while (p - s0 < kSyncBits) {
+            const uint64_t d = p - s0;
+            if ((bm[d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
+            uint32_t sym;
+            const uint32_t L = br_next<MODE>(r, a, lds, sym);
+            if (L == 0) break;
+            p += L;
+            ++walked;
+        }
+        if (synced) {
+            y.cnt[k] = y.cnt[k] - bits_below(bm, (uint32_t)(p - s0)) + walked;
+        } else {
+            const uint32_t q = atomicAdd(y.nqueue, 1u);
+            y.queue[q] = (uint32_t)k;
+        }
+    }
+}
+
+// One lane, queued segments in order: decode each from its true entry; when
+// its exit differs from the scanned one, the next segment's sync is checked
+// again against the new exit (and fixed the same way if needed).
+template <int MODE>
+__global__ void k_sync_serial(DecArgs a, SyncArgs y) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     if (threadIdx.x != 0) return;
-    uint64_t pos = start_bit;
-    const uint64_t p = pos + a.bit_adj;
-    BitReader r;
-    {
-        const uint64_t w = p >> 5;
-        const uint32_t sh = (uint32_t)(p & 31);
-        r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
-        r.nb = 64 - sh;
-        r.nxt = ld_word(a, w + 2);
-        r.wpos = w + 3;
+    const uint32_t nq = *y.nqueue;
+    for (uint32_t i = 1; i < nq; ++i) {  // insertion sort: the queue is short
+        const uint32_t v = y.queue[i];
+        uint32_t j = i;
+        while (j > 0 && y.queue[j - 1] > v) { y.queue[j] = y.queue[j - 1]; --j; }
+        y.queue[j] = v;
     }
-    uint64_t bstart = 0, maxb = 0;
-    for (uint64_t i = 0; i < a.nsym; ++i) {
-        const uint32_t in_blk = (uint32_t)(i % kBlockSyms);
-        if (in_blk == 0) {
-            if (i) maxb = pos - bstart > maxb ? pos - bstart : maxb;
-            starts[i / kBlockSyms] = pos;
-            bstart = pos;
-        }
-        if (in_blk % kChainSyms == 0)
-            subs[(i / kBlockSyms) * kChainsPerBlock + in_blk / kChainSyms] = (uint16_t)(pos - bstart);
-        if (r.nb <= 32) {
-            r.buf |= (uint64_t)r.nxt << (32 - r.nb);
-            r.nb += 32;
-            r.nxt = ld_word(a, r.wpos++);
-        }
-        const uint64_t win = r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
-        uint32_t sym, L;
-        dec_lookup<MODE>(a, lds, win, sym, L);
-        if (L == 0) { atomicOr(a.err, 2u); return; }
-        pos += L;
-        if (L < r.nb) {
-            r.buf <<= L;
-            r.nb -= L;
-        } else {
-            const uint32_t rr = L - r.nb;
-            r.buf = (uint64_t)r.nxt << (32 + rr);
-            r.nb = 32 - rr;
-            r.nxt = ld_word(a, r.wpos++);
+    uint64_t last = 0;  // last segment fixed (0: none; segment 0 never needs it)
+    for (uint32_t i = 0; i < nq; ++i) {
+        uint64_t k = y.queue[i];
+        if (k <= last) continue;
+        for (;;) {
+            const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
+            uint64_t pos = y.exitp[k - 1];
+            BitReader r;
+            br_init(r, a, pos + a.bit_adj);
+            uint64_t n = 0;
+            while (pos < s1) {
+                uint32_t sym;
+                const uint32_t L = br_next<MODE>(r, a, lds, sym);
+                if (L == 0) { atomicOr(a.err, 2u); return; }
+                pos += L;
+                ++n;
+            }
+            (void)s0;
+            const uint64_t old_exit = y.exitp[k];
+            y.exitp[k] = pos;
+            y.cnt[k] = n;
+            last = k;
+            if (pos == old_exit || k + 1 >= y.nseg) break;
+            // k_sync_fix walked segment k+1 from old_exit: fix k+1 from the new
+            // exit as well (its count is recomputed from scratch)
+            k = k + 1;
         }
     }
-    // chains past the end of a tail block start at the end
-    const uint64_t nb = a.nblocks;
-    const uint32_t tail = (uint32_t)(a.nsym - (nb - 1) * kBlockSyms);
-    for (uint32_t c = (tail + kChainSyms - 1) / kChainSyms; c < (uint32_t)kChainsPerBlock; ++c)
-        subs[(nb - 1) * kChainsPerBlock + c] = (uint16_t)(pos - bstart);
-    starts[nb] = pos;
-    starts[nb + 1] = pos - bstart > maxb ? pos - bstart : maxb;
 }
 
-hipError_t launch_index_serial(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index, uint32_t* d_err,
-                               hipStream_t s) {
+// Decode each segment from its true entry; symbol i (global) lands at pos.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* first,
+                                                  unsigned long long* starts, uint16_t* subs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
+        uint64_t i = first[k];
+        if (i >= a.nsym) continue;
+        const uint64_t s1 = y.start + (k + 1) * kSegBits;
+        uint64_t pos = k ? y.exitp[k - 1] : y.start;
+        BitReader r;
+        br_init(r, a, pos + a.bit_adj);
+        while (pos < s1 && i < a.nsym) {
+            if (i % kBlockSyms == 0) starts[i / kBlockSyms] = pos;
+            if (i % kChainSyms == 0) subs[i / kChainSyms] = (uint16_t)pos;
+            uint32_t sym;
+            const uint32_t L = br_next<MODE>(r, a, lds, sym);
+            if (L == 0) { atomicOr(a.err, 2u); break; }
+            pos += L;
+            ++i;
+        }
+        if (i == a.nsym) starts[a.nblocks] = pos;
+    }
+}
+
+// Chain positions relative to their block start (mod 2^16), chains past the
+// stream's end at the end, and the largest block.
+__global__ __launch_bounds__(256) void k_sync_subs(uint64_t nsym, uint64_t nblocks, unsigned long long* starts,
+                                                   uint16_t* subs) {
+    const uint64_t nch = nblocks * kChainsPerBlock;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long mx = 0;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += stride) {
+        const uint64_t b = c / kChainsPerBlock;
+        const uint64_t bs = starts[b];
+        const uint64_t raw = c * kChainSyms < nsym ? (uint64_t)subs[c] : starts[nblocks];
+        subs[c] = (uint16_t)((raw - bs) & 0xffffu);
+        if (c % kChainsPerBlock == 0) {
+            const unsigned long long bits = starts[b + 1] - bs;
+            mx = bits > mx ? bits : mx;
+        }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t lo = shfl_xor_u32((uint32_t)mx, m), hi = shfl_xor_u32((uint32_t)(mx >> 32), m);
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(starts + nblocks + 1, mx);
+}
+
+uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
+    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
+    const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
+    // exit, cnt, first (u64 each), bitmap (4 u64), queue (u32, as u64/2), counter, tiles
+    return nseg * (3 + kSyncBits / 64) + (nseg + 1) / 2 + 1 + ntiles + 8;
+}
+
+template <int MODE>
+static hipError_t run_index(const DecArgs& a, const SyncArgs& y, unsigned long long* first, unsigned long long* tiles,
+                            unsigned long long* d_index, uint32_t lds, int ncu, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        const void* fns[4] = {(const void*)k_sync_scan<MODE>, (const void*)k_sync_fix<MODE>,
+                              (const void*)k_sync_serial<MODE>, (const void*)k_sync_emit<MODE>};
+        for (const void* f : fns) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            if (e != hipSuccess) return e;
+        }
+        attr = true;
+    }
+    uint64_t wgs = (y.nseg + 255) / 256;
+    const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 4 ? kLdsBytes / lds : 4) : 4);
+    wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
+    hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(256), lds, s, a, y);
+    hipLaunchKernelGGL(k_sync_fix<MODE>, dim3(wgs), dim3(256), lds, s, a, y);
+    hipLaunchKernelGGL(k_sync_serial<MODE>, dim3(1), dim3(64), lds, s, a, y);
+    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
+    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       (const unsigned long long*)tiles, first);
+    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
+    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(256), lds, s, a, y, (const unsigned long long*)first, d_index,
+                       subs);
+    hipError_t e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
+    if (e != hipSuccess) return e;
+    uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
+    sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
+    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index, subs);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                              uint64_t nsym, unsigned long long* d_index, unsigned long long* d_scratch, uint32_t* d_err,
+                              int ncu, hipStream_t s) {
     if (nsym == 0) return hipSuccess;
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = nullptr; a.subs = nullptr; a.out = nullptr; a.err = d_err;
-    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
-    const int m = t.dec_mode;
-    const void* fn = m == DEC_DENSE ? (const void*)k_index_serial<DEC_DENSE>
-                   : m == DEC_FIXED16 ? (const void*)k_index_serial<DEC_FIXED16> : (const void*)k_index_serial<DEC_LUT>;
-    static bool attr[3] = {false, false, false};
-    if (!attr[m]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        if (e != hipSuccess) return e;
-        attr[m] = true;
-    }
-    if (m == DEC_DENSE)
-        hipLaunchKernelGGL(k_index_serial<DEC_DENSE>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
-    else if (m == DEC_FIXED16)
-        hipLaunchKernelGGL(k_index_serial<DEC_FIXED16>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
-    else
-        hipLaunchKernelGGL(k_index_serial<DEC_LUT>, dim3(1), dim3(256), t.dec_lds_bytes, s, a, start_bit, d_index, subs);
-    return hipGetLastError();
+    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    SyncArgs y;
+    y.start = start_bit;
+    y.nseg = (bits + kSegBits - 1) / kSegBits;
+    if (y.nseg == 0) return hipErrorInvalidValue;
+    unsigned long long* p = d_scratch;
+    y.exitp = p; p += y.nseg;
+    y.cnt = p; p += y.nseg;
+    unsigned long long* first = p; p += y.nseg;
+    y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kSyncBits / 64);
+    y.queue = reinterpret_cast<uint32_t*>(p); p += (y.nseg + 1) / 2;
+    y.nqueue = reinterpret_cast<uint32_t*>(p); p += 1;
+    unsigned long long* tiles = p;
+    hipError_t e = hipMemsetAsync(y.nqueue, 0, 8, s);
+    if (e != hipSuccess) return e;
+    const uint32_t lds = t.dec_lds_bytes;
+    if (t.dec_mode == DEC_DENSE) return run_index<DEC_DENSE>(a, y, first, tiles, d_index, lds, ncu, s);
+    if (t.dec_mode == DEC_FIXED16) return run_index<DEC_FIXED16>(a, y, first, tiles, d_index, lds, ncu, s);
+    return run_index<DEC_LUT>(a, y, first, tiles, d_index, lds, ncu, s);
 }
 
 }  // namespace hz

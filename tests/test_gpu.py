@@ -196,6 +196,24 @@ def test_pipeline_256mib_matches_oracle(codec, kind):
     assert torch.equal(out[:2 * nsym], x[:2 * nsym])
 
 
+@pytest.mark.parametrize("kind,n", [(1, (64 << 20) + 2), (0, (64 << 20) + 1), (1, 4097 * 2 + 1), (1, 3)])
+def test_index_build_equals_pack_index(codec, kind, n):
+    """The self-synchronising index builder (for index-less reference files)
+    reproduces, from the payload alone, exactly the block index hz_pack wrote."""
+    import torch
+    from huffman_amd import index_bytes
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=5)
+    plan, payload, index = codec.encode(x)
+    rebuilt = torch.full_like(index, -1)
+    codec.dev.index_build(payload.data_ptr(), payload.numel(), plan.start_bit, n // 2, rebuilt.data_ptr())
+    codec.sync()
+    nb = index_bytes(n // 2)
+    a = index.cpu().numpy().view(np.uint8)[:nb]
+    b = rebuilt.cpu().numpy().view(np.uint8)[:nb]
+    assert np.array_equal(a, b)
+
+
 def test_pipeline_4gib_roundtrip_properties(codec):
     """Above the reference's 4 GiB int-index limit: u64 counts, round trip,
     total bits == sum(hist * len), index monotone."""
