@@ -160,9 +160,21 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    codec.sync()  # surfaces device-side errors (look-back timeout, capacity)
+    codec.sync()  # surfaces device-side errors (capacity, format)
     ok = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
     plan = state["plan"]
+    # Index-less decode path (reference-produced files): rebuild the block index
+    # from the payload alone, outside the timed loop, and check it against pack's.
+    from huffman_amd import index_bytes
+    from huffman_amd._lib import STAGE_INDEX
+    nidx = (index_bytes(nsym) + 7) // 8
+    rebuilt = torch.empty_like(state["index"])
+    codec.dev.index_build(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit, nsym,
+                          rebuilt.data_ptr())
+    codec.sync()
+    index_build = {"ms": round(codec.dev.kernel_ms(STAGE_INDEX), 3),
+                   "matches_pack_index": bool(torch.equal(rebuilt[:nidx], state["index"][:nidx]))}
+    del rebuilt
     C = plan.payload_bits // 8
     if world > 1:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
@@ -216,6 +228,7 @@ def main():
                 "max_code_len": int(plan.cb.max_len),
             },
             "roundtrip_bit_exact": ok,
+            "index_build_from_payload": index_build,
             # algorithmic HBM bytes of one step per GPU: hist N + pack (N + C) + decode (C + N)
             "step_algorithmic_GBps": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9, 1),
             "step_hbm_frac": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),

@@ -301,7 +301,7 @@ std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m) {
         }
         if (best >= 0) {
             const uint32_t s = (uint32_t)best;
-            img[slot] = ((s >> 15) << 31) | ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
+            img[hot_word(slot)] = ((s >> 15) << 31) | ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
         }
     }
     return img;

@@ -365,7 +365,8 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][0], c->stream));
     HZ_TRY(launch_index_build(c->t, d_payload, payload_bytes, start_bit, nsym,
-                              reinterpret_cast<unsigned long long*>(d_index), c->d_desc, c->d_err, c->ncu, c->stream));
+                              reinterpret_cast<unsigned long long*>(d_index), c->d_desc, c->d_err, c->h_err + 2,
+                              c->ncu, c->stream));
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][1], c->stream));
     c->ev_used[HZ_STAGE_INDEX] = true;
     return arm_err_check(c);

@@ -97,6 +97,9 @@ __host__ __device__ inline uint32_t len8_index(uint32_t s) { return s ^ (((s >> 
 
 // HOT slot of symbol s under pairing mask m (bit 15 of m set).
 __host__ __device__ inline uint32_t hot_slot(uint32_t s, uint32_t m) { return (s & 0x8000u) ? (s ^ m) : s; }
+// LDS word of a HOT slot: the symbol's second byte is XORed into the bank bits
+// (the first byte alone would pick the bank; skewed data keeps it small).
+__host__ __device__ inline uint32_t hot_word(uint32_t slot) { return slot ^ ((slot >> 8) & 0x3fu); }
 
 // Launchers (hz_kernels.hip). All stream ordered; return hipError_t.
 hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu,
@@ -110,7 +113,8 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
                          uint32_t* d_err, int ncu, hipStream_t s);
 hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index,
-                              unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
+                              unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
+                              hipStream_t s);  // synchronises the stream (iterates to a fixed point)
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
 hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
                            const unsigned long long* d_thr, hipStream_t s);

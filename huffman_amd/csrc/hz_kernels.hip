@@ -86,13 +86,19 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 constexpr int kHistThreads = 1024;
 constexpr int kHistUnroll = 4;
 
-// Fix-up after `old = atomicAdd(&lds[s >> 1], inc)`; rare (once per 65 536 adds of a bin).
+// LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
+// their low bits (the first byte), which alone would pick the LDS bank: the
+// second byte's low bits are XORed into the bank bits (a bijection).
+HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ ((s >> 8) & 0x3fu); }
+HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ ((w >> 7) & 0x3fu); }
+
+// Fix-up after `old = atomicAdd(&lds[hist_word(s)], inc)`; rare (once per 65 536 adds of a bin).
 HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old) {
     const uint32_t inc = (s & 1) ? 0x10000u : 1u;
     if (old + inc < old) atomicAdd(&hist[s | 1], 65536ull);  // the dword (high half) wrapped
     if (!(s & 1) && (old & 0xffffu) == 0xffffu) {            // low half crossed 65 536: undo its carry
         atomicAdd(&hist[s], 65536ull);
-        uint32_t o2 = atomicSub(&lds[s >> 1], 0x10000u);
+        uint32_t o2 = atomicSub(&lds[hist_word(s)], 0x10000u);
         if (o2 < 0x10000u) atomicAdd(&hist[s | 1], (unsigned long long)(-65536ll));
     }
 }
@@ -103,7 +109,7 @@ HZ_DEV bool hist_needs_fix(uint32_t s, uint32_t old) {
 }
 
 HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s) {
-    uint32_t old = atomicAdd(&lds[s >> 1], (s & 1) ? 0x10000u : 1u);
+    uint32_t old = atomicAdd(&lds[hist_word(s)], (s & 1) ? 0x10000u : 1u);
     if (hist_needs_fix(s, old)) hist_fix(lds, hist, s, old);
 }
 
@@ -137,7 +143,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                    old[u * 8 + k] = atomicAdd(&lds[s >> 1], ok ? ((s & 1) ? 0x10000u : 1u) : 0u);
+                    old[u * 8 + k] = atomicAdd(&lds[hist_word(s)], ok ? ((s & 1) ? 0x10000u : 1u) : 0u);
                 }
             }
             bool any = false;
@@ -173,8 +179,9 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
     __syncthreads();
     for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
         const uint32_t v = lds[i];
-        if (v & 0xffffu) atomicAdd(&hist[2 * i], (unsigned long long)(v & 0xffffu));
-        if (v >> 16) atomicAdd(&hist[2 * i + 1], (unsigned long long)(v >> 16));
+        const uint32_t s2 = hist_word_inv((uint32_t)i) << 1;  // the symbol pair this word counts
+        if (v & 0xffffu) atomicAdd(&hist[s2], (unsigned long long)(v & 0xffffu));
+        if (v >> 16) atomicAdd(&hist[s2 + 1], (unsigned long long)(v >> 16));
     }
 }
 
@@ -311,13 +318,13 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
             const uint32_t slot = s ^ (m & (uint32_t)((int32_t)(s << 16) >> 31));
-            const uint32_t x = lds[slot] ^ ((s << 16) & 0x80000000u);
+            const uint32_t x = lds[hot_word(slot)] ^ ((s << 16) & 0x80000000u);
             const bool hit = x - 0x04000000u < 0x7c000000u;  // tag matches and len != 0
             e[k] = k < nvalid ? (T)x : (T)0;
             if (!hit && k < nvalid) miss |= 1u << k;
         }
         const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
-        const uint32_t xx = lds[xslot] ^ ((xs << 16) & 0x80000000u);
+        const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
         const bool xmiss = !(xx - 0x04000000u < 0x7c000000u);
         xe = (T)xx;
         if (miss | (uint32_t)xmiss) {
@@ -1158,25 +1165,27 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
 
 // ===========================================================================
 // Block index of an index-less stream (a .compressed file from the reference
-// encoder, Decompressor.cu:259-291 decodes it serially). Huffman codes
+// encoder; Decompressor.cu:259-291 decodes it serially). Huffman codes
 // resynchronise: a decoder started at an arbitrary bit falls onto the true
-// codeword boundaries after a few codewords. The stream is cut into 4096-bit
-// segments, one lane each:
+// codeword boundaries after some codewords (measured on Zipf(1.1): median 81
+// bits, p99 600). The stream is cut into 4096-bit segments, one lane each:
 //   k_sync_scan : decode segment k from its first bit to the first boundary
-//                 past its end -> exit[k], count[k], and a bitmap of the
-//                 boundaries in its first 256 bits
-//   k_sync_fix  : the true path enters segment k at exit[k-1]; if that bit is
-//                 a boundary of k's own path the two paths coincide from there
-//                 on, and count[k] drops the boundaries before it; otherwise
-//                 k is queued for the serial fixer (rare)
-//   k_sync_serial: redecodes queued segments from their true entry, in order
+//                 past its end -> exit0[k], cnt0[k] and a bitmap of every
+//                 boundary of that path in the segment
+//   k_sync_iter : the true path enters k at exit[k-1]; follow it until it
+//                 lands on a bitmap boundary (from there both paths agree:
+//                 count = cnt0 - boundaries before + codewords walked, exit =
+//                 exit0) or leaves the segment (count and exit from the walk).
+//                 Repeated (host loop) for segments whose entry changed,
+//                 until no exit changes: chains of unsynchronised segments
+//                 are rare and short.
 //   k_scan_*    : exclusive scan of counts -> first symbol number per segment
 //   k_sync_emit : decode every segment again from its true entry and write
 //                 block starts and raw chain positions
 //   k_sync_subs : chain positions relative to their block, max block bits
 // ===========================================================================
 constexpr uint32_t kSegBits = 4096;
-constexpr uint32_t kSyncBits = 256;  // boundary bitmap per segment (8 words)
+constexpr uint32_t kSegWords = kSegBits / 32;
 
 struct BitReader {
     uint64_t buf;
@@ -1222,11 +1231,13 @@ HZ_DEV uint32_t br_next(BitReader& r, const DecArgs& a, const uint32_t* lds, uin
 struct SyncArgs {
     uint64_t start;                 // stream bit of the first symbol (payload view: + bit_adj)
     uint64_t nseg;
-    unsigned long long* exitp;      // first boundary >= segment end, on the path taken
-    unsigned long long* cnt;        // symbols on that path inside the segment
-    uint32_t* bmp;                  // boundaries in the segment's first 256 bits
-    uint32_t* queue;                // segments whose entry is not on their own path
-    uint32_t* nqueue;
+    unsigned long long* exit0;      // scan path: first boundary >= segment end
+    unsigned long long* cnt0;       // scan path: codewords inside the segment
+    uint32_t* bmp;                  // scan path: boundaries, kSegWords per segment
+    unsigned long long* ex[2];      // true exits, ping-pong between iterations
+    unsigned long long* cnt;        // true counts
+    uint32_t* dirty[2];             // entry changed in the previous iteration
+    uint32_t* changed;              // exits changed in this iteration
 };
 
 template <int MODE>
@@ -1236,124 +1247,81 @@ __global__ __launch_bounds__(256) void k_sync_scan(DecArgs a, SyncArgs y) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
+        uint32_t* bm = y.bmp + k * kSegWords;
         BitReader r;
         br_init(r, a, s0 + a.bit_adj);
         uint64_t pos = s0, n = 0;
-        uint32_t bm[kSyncBits / 32];
-#pragma unroll
-        for (int i = 0; i < (int)(kSyncBits / 32); ++i) bm[i] = 0;
+        uint32_t cw = 0, cur = 0;  // bitmap word being filled
         while (pos < s1) {
-            const uint64_t d = pos - s0;
-            if (d < kSyncBits) {
-#pragma unroll
-                for (int i = 0; i < (int)(kSyncBits / 32); ++i)
-                    if ((uint32_t)(d >> 5) == (uint32_t)i) bm[i] |= 1u << (d & 31);
-            }
+            const uint32_t d = (uint32_t)(pos - s0);
+            while ((d >> 5) != cw) { bm[cw++] = cur; cur = 0; }
+            cur |= 1u << (d & 31);
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
             pos += L;
             ++n;
         }
-        y.exitp[k] = pos;
-        y.cnt[k] = n;
-#pragma unroll
-        for (int i = 0; i < (int)(kSyncBits / 32); ++i) y.bmp[k * (kSyncBits / 32) + i] = bm[i];
+        for (; cw < kSegWords; ++cw) { bm[cw] = cur; cur = 0; }
+        y.exit0[k] = pos;
+        y.cnt0[k] = n;
     }
 }
 
-HZ_DEV uint32_t bits_below(const uint32_t* bm, uint32_t d) {  // boundaries before offset d (< 256)
-    uint32_t c = 0;
-    for (uint32_t i = 0; i < (d >> 5); ++i) c += __popc(bm[i]);
-    if (d & 31) c += __popc(bm[d >> 5] & ((1u << (d & 31)) - 1u));
-    return c;
-}
-
-// The true path enters segment k at e = exit[k-1]. Follow it codeword by
-// codeword until it lands on a boundary of k's own path (in the bitmap); from
-// there the two coincide, so the true count is k's count minus its boundaries
-// before that point plus the true-path codewords walked. No landing within
-// the first 256 bits (rare): queue k for the serial fixer.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sync_fix(DecArgs a, SyncArgs y) {
+__global__ __launch_bounds__(256) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
+    const unsigned long long* exr = y.ex[it & 1];
+    unsigned long long* exw = y.ex[(it + 1) & 1];
+    const uint32_t* dr = y.dirty[it & 1];
+    uint32_t* dw = y.dirty[(it + 1) & 1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
-        const uint64_t s0 = y.start + k * kSegBits;
-        const uint32_t* bm = y.bmp + k * (kSyncBits / 32);
-        uint64_t p = y.exitp[k - 1];
-        uint64_t walked = 0;
-        bool synced = false;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
+        if (k == 0) { if (it == 0) { exw[0] = y.exit0[0]; y.cnt[0] = y.cnt0[0]; } else exw[0] = exr[0]; continue; }
+        if (it > 0 && !dr[k]) { exw[k] = exr[k]; continue; }
+        const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
+        const uint32_t* bm = y.bmp + k * kSegWords;
+        uint64_t p = it == 0 ? y.exit0[k - 1] : exr[k - 1];
+        uint64_t walked = 0, ex = 0, n = 0;
+        bool landed = false;
         BitReader r;
         br_init(r, a, p + a.bit_adj);
-        while (p - s0 < kSyncBits) {
-            const uint64_t d = p - s0;
-            if ((bm[d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
+        while (p < s1) {
+            const uint32_t d = (uint32_t)(p - s0);
+            if ((bm[d >> 5] >> (d & 31)) & 1u) { landed = true; break; }
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
-            if (L == 0) break;
+            if (L == 0) { atomicOr(a.err, 2u); break; }
             p += L;
             ++walked;
         }
-        if (synced) {
-            y.cnt[k] = y.cnt[k] - bits_below(bm, (uint32_t)(p - s0)) + walked;
+        if (landed) {
+            const uint32_t d = (uint32_t)(p - s0);
+            uint32_t below = 0;
+            for (uint32_t i = 0; i < (d >> 5); ++i) below += __popc(bm[i]);
+            if (d & 31) below += __popc(bm[d >> 5] & ((1u << (d & 31)) - 1u));
+            n = y.cnt0[k] - below + walked;
+            ex = y.exit0[k];
         } else {
-            const uint32_t q = atomicAdd(y.nqueue, 1u);
-            y.queue[q] = (uint32_t)k;
+            n = walked;
+            ex = p;
         }
-    }
-}
-
-// One lane, queued segments in order: decode each from its true entry; when
-// its exit differs from the scanned one, the next segment's sync is checked
-// again against the new exit (and fixed the same way if needed).
-template <int MODE>
-__global__ void k_sync_serial(DecArgs a, SyncArgs y) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, a.lds_img, a.lds_words);
-    if (threadIdx.x != 0) return;
-    const uint32_t nq = *y.nqueue;
-    for (uint32_t i = 1; i < nq; ++i) {  // insertion sort: the queue is short
-        const uint32_t v = y.queue[i];
-        uint32_t j = i;
-        while (j > 0 && y.queue[j - 1] > v) { y.queue[j] = y.queue[j - 1]; --j; }
-        y.queue[j] = v;
-    }
-    uint64_t last = 0;  // last segment fixed (0: none; segment 0 never needs it)
-    for (uint32_t i = 0; i < nq; ++i) {
-        uint64_t k = y.queue[i];
-        if (k <= last) continue;
-        for (;;) {
-            const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
-            uint64_t pos = y.exitp[k - 1];
-            BitReader r;
-            br_init(r, a, pos + a.bit_adj);
-            uint64_t n = 0;
-            while (pos < s1) {
-                uint32_t sym;
-                const uint32_t L = br_next<MODE>(r, a, lds, sym);
-                if (L == 0) { atomicOr(a.err, 2u); return; }
-                pos += L;
-                ++n;
-            }
-            (void)s0;
-            const uint64_t old_exit = y.exitp[k];
-            y.exitp[k] = pos;
-            y.cnt[k] = n;
-            last = k;
-            if (pos == old_exit || k + 1 >= y.nseg) break;
-            // k_sync_fix walked segment k+1 from old_exit: fix k+1 from the new
-            // exit as well (its count is recomputed from scratch)
-            k = k + 1;
+        y.cnt[k] = n;
+        const uint64_t prev = it == 0 ? y.exit0[k] : exr[k];
+        exw[k] = ex;
+        if (ex != prev) {
+            if (k + 1 < y.nseg) dw[k + 1] = 1;
+            atomicAdd(y.changed, 1u);
         }
     }
 }
 
 // Decode each segment from its true entry; symbol i (global) lands at pos.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* first,
-                                                  unsigned long long* starts, uint16_t* subs) {
+__global__ __launch_bounds__(256) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* exits,
+                                                  const unsigned long long* first, unsigned long long* starts,
+                                                  uint16_t* subs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1361,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_sync_emit(DecArgs a, SyncArgs y, const 
         uint64_t i = first[k];
         if (i >= a.nsym) continue;
         const uint64_t s1 = y.start + (k + 1) * kSegBits;
-        uint64_t pos = k ? y.exitp[k - 1] : y.start;
+        uint64_t pos = k ? exits[k - 1] : y.start;
         BitReader r;
         br_init(r, a, pos + a.bit_adj);
         while (pos < s1 && i < a.nsym) {
@@ -1406,17 +1374,17 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // exit, cnt, first (u64 each), bitmap (4 u64), queue (u32, as u64/2), counter, tiles
-    return nseg * (3 + kSyncBits / 64) + (nseg + 1) / 2 + 1 + ntiles + 8;
+    // exit0, cnt0, ex[2], cnt, first (u64), bitmap (kSegWords u32), dirty[2] (u32), counter, tiles
+    return nseg * (6 + kSegWords / 2 + 1) + 1 + ntiles + 8;
 }
 
 template <int MODE>
-static hipError_t run_index(const DecArgs& a, const SyncArgs& y, unsigned long long* first, unsigned long long* tiles,
-                            unsigned long long* d_index, uint32_t lds, int ncu, hipStream_t s) {
+static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* first, unsigned long long* tiles,
+                            unsigned long long* d_index, uint32_t* h_changed, uint32_t lds, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        const void* fns[4] = {(const void*)k_sync_scan<MODE>, (const void*)k_sync_fix<MODE>,
-                              (const void*)k_sync_serial<MODE>, (const void*)k_sync_emit<MODE>};
+        const void* fns[3] = {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>,
+                              (const void*)k_sync_emit<MODE>};
         for (const void* f : fns) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
             if (e != hipSuccess) return e;
@@ -1427,8 +1395,18 @@ static hipError_t run_index(const DecArgs& a, const SyncArgs& y, unsigned long l
     const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 4 ? kLdsBytes / lds : 4) : 4);
     wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
     hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(256), lds, s, a, y);
-    hipLaunchKernelGGL(k_sync_fix<MODE>, dim3(wgs), dim3(256), lds, s, a, y);
-    hipLaunchKernelGGL(k_sync_serial<MODE>, dim3(1), dim3(64), lds, s, a, y);
+    // resolve entries until no exit changes (host loop; typically 1-3 passes)
+    int it = 0;
+    for (;; ++it) {
+        hipError_t e = hipMemsetAsync(y.changed, 0, 4, s);
+        if (e != hipSuccess) return e;
+        if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nseg, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sync_iter<MODE>, dim3(wgs), dim3(256), lds, s, a, y, it);
+        if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (*h_changed == 0 || it > (int)y.nseg) break;
+    }
+    const unsigned long long* exits = y.ex[(it + 1) & 1];
     const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
                        tiles);
@@ -1436,8 +1414,8 @@ static hipError_t run_index(const DecArgs& a, const SyncArgs& y, unsigned long l
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
                        (const unsigned long long*)tiles, first);
     uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
-    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(256), lds, s, a, y, (const unsigned long long*)first, d_index,
-                       subs);
+    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(256), lds, s, a, y, exits, (const unsigned long long*)first,
+                       d_index, subs);
     hipError_t e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
     if (e != hipSuccess) return e;
     uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
@@ -1448,7 +1426,7 @@ static hipError_t run_index(const DecArgs& a, const SyncArgs& y, unsigned long l
 
 hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
                               uint64_t nsym, unsigned long long* d_index, unsigned long long* d_scratch, uint32_t* d_err,
-                              int ncu, hipStream_t s) {
+                              uint32_t* h_scratch, int ncu, hipStream_t s) {
     if (nsym == 0) return hipSuccess;
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
@@ -1459,19 +1437,22 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.nseg = (bits + kSegBits - 1) / kSegBits;
     if (y.nseg == 0) return hipErrorInvalidValue;
     unsigned long long* p = d_scratch;
-    y.exitp = p; p += y.nseg;
+    y.exit0 = p; p += y.nseg;
+    y.cnt0 = p; p += y.nseg;
+    y.ex[0] = p; p += y.nseg;
+    y.ex[1] = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     unsigned long long* first = p; p += y.nseg;
-    y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kSyncBits / 64);
-    y.queue = reinterpret_cast<uint32_t*>(p); p += (y.nseg + 1) / 2;
-    y.nqueue = reinterpret_cast<uint32_t*>(p); p += 1;
+    y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kSegWords / 2);
+    y.dirty[0] = reinterpret_cast<uint32_t*>(p);
+    y.dirty[1] = y.dirty[0] + y.nseg;
+    p += y.nseg;
+    y.changed = reinterpret_cast<uint32_t*>(p); p += 1;
     unsigned long long* tiles = p;
-    hipError_t e = hipMemsetAsync(y.nqueue, 0, 8, s);
-    if (e != hipSuccess) return e;
     const uint32_t lds = t.dec_lds_bytes;
-    if (t.dec_mode == DEC_DENSE) return run_index<DEC_DENSE>(a, y, first, tiles, d_index, lds, ncu, s);
-    if (t.dec_mode == DEC_FIXED16) return run_index<DEC_FIXED16>(a, y, first, tiles, d_index, lds, ncu, s);
-    return run_index<DEC_LUT>(a, y, first, tiles, d_index, lds, ncu, s);
+    if (t.dec_mode == DEC_DENSE) return run_index<DEC_DENSE>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
+    if (t.dec_mode == DEC_FIXED16) return run_index<DEC_FIXED16>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
+    return run_index<DEC_LUT>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
 }
 
 }  // namespace hz
