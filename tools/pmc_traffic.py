@@ -14,7 +14,8 @@ decode: 64-B chunk loads as dwordx4), so fetch bytes = 2 x FETCH_SIZE x 1024.
 WRITE_SIZE is exact for 16-B-per-lane streaming stores (decode output bursts,
 pack output words are 4-B stores and are reported as counted). The stage
 figures are summed over the kernels of a stage and divided by the number of
-launches of the stage's last kernel (k_hist16 / k_pack_write / k_decode), so they are per launch of the stage like bench.py's `achieved`.
+launches of the stage's marker kernel (k_hist16 / k_pack_write or k_pack_fixed16 / k_decode or
+k_decode_fixed16), so they are per launch of the stage like bench.py's `achieved`.
 """
 import argparse
 import csv
@@ -22,16 +23,22 @@ import json
 import os
 from collections import defaultdict
 
+# stage -> (kernels of the stage, kernels that mark one launch of the stage)
 STAGES = {
-    "hist": ("k_hist16",),
-    "pack": ("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write"),
-    "decode": ("k_decode",),
+    "hist": (("k_hist16",), ("k_hist16",)),
+    "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16"),
+             ("k_pack_write", "k_pack_fixed16")),
+    "decode": (("k_decode", "k_decode_fixed16"), ("k_decode", "k_decode_fixed16")),
 }
 
 
+def _is(name, k):
+    return k + "<" in name or k + "(" in name
+
+
 def stage_of(name):
-    for st, keys in STAGES.items():
-        if any(k + "<" in name or k + "(" in name for k in keys):
+    for st, (keys, _) in STAGES.items():
+        if any(_is(name, k) for k in keys):
             return st
     return None
 
@@ -48,7 +55,7 @@ def read_counter(d, counter):
             if st is None:
                 continue
             per[st] += float(row["Counter_Value"]) * 1024.0
-            if STAGES[st][-1] + "<" in row["Kernel_Name"] or STAGES[st][-1] + "(" in row["Kernel_Name"]:
+            if any(_is(row["Kernel_Name"], k) for k in STAGES[st][1]):
                 calls[st].add(row["Dispatch_Id"])
     return per, {k: len(v) for k, v in calls.items()}
 
