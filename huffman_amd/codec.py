@@ -59,6 +59,13 @@ def archive(path, verbose=True):
     return str(path) + ".compressed"
 
 
+def archive_stream(path, out_path, chunk_bytes=1 << 30, verbose=False):
+    """Streaming `archive` with bounded memory (chunks of chunk_bytes)."""
+    check(load().hz_archive_stream(str(path).encode(), str(out_path).encode(), chunk_bytes, int(verbose)),
+          "hz_archive_stream")
+    return str(out_path)
+
+
 def extract(path, verbose=True):
     """`extract <path>`: writes ./DECOMPRESSED_FILE (or (k)); returns its name."""
     name = ctypes.create_string_buffer(256)

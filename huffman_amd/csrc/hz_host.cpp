@@ -404,6 +404,8 @@ extern "C" int hz_generate(hz_ctx* c, uint8_t* d_out, uint64_t n, uint64_t offse
 // ---------------------------------------------------------------------------
 namespace {
 
+constexpr uint64_t kArchiveChunk = 1ull << 30;  // 1 GiB per streamed chunk
+
 std::mutex g_mu;
 hz_ctx* g_ctx = nullptr;
 
@@ -554,6 +556,147 @@ int write_file(const std::string& path, const uint8_t* p, uint64_t n) {
 
 }  // namespace
 
+// ---- streaming archive: bounded host and device memory ----
+// Pass 1 reads the file in chunks and accumulates the histogram on the device;
+// pass 2 packs chunk by chunk at the running bit offset. Each chunk's last,
+// partial word is carried into the next chunk as its `lead` bits, so the file
+// is byte-identical to the whole-buffer encoder's. Two pinned host buffers let
+// the next chunk's fread overlap the device work on the current one.
+namespace {
+
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    int alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault) == hipSuccess ? HZ_OK : HZ_ENOMEM; }
+};
+
+int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
+    return (n == 0 || fread(p, 1, n, fp) == n) ? HZ_OK : HZ_EIO;
+}
+
+}  // namespace
+
+extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+    if (!in_path || !out_path || chunk_bytes < 64) return HZ_EINVAL;
+    chunk_bytes &= ~(uint64_t)15;  // even (whole symbols) and 16-byte aligned device reads
+    struct stat st;
+    if (stat(in_path, &st) != 0) return HZ_EIO;
+    const uint64_t n = (uint64_t)st.st_size;
+    hz_ctx* c;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    HZ_TRY(hipSetDevice(c->device));
+    const uint64_t chunk = std::min<uint64_t>(chunk_bytes, std::max<uint64_t>(n, 16));
+    PinnedBuf hin[2];
+    DevBuf din[2], dhist;
+    for (int i = 0; i < 2; ++i) {
+        if ((rc = hin[i].alloc(chunk))) return rc;
+        if ((rc = din[i].alloc(chunk + 16))) return rc;
+    }
+    if ((rc = dhist.alloc(HZ_NSYM * 8))) return rc;
+    uint8_t last_byte = 0;
+    FILE* fp = fopen(in_path, "rb");
+    if (!fp) return HZ_EIO;
+    std::unique_ptr<FILE, int (*)(FILE*)> fin(fp, fclose);
+    // ---- pass 1: histogram
+    HZ_TRY(hipMemsetAsync(dhist.p, 0, HZ_NSYM * 8, c->stream));
+    hipEvent_t done[2];
+    HZ_TRY(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+    HZ_TRY(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+    std::unique_ptr<hipEvent_t, void (*)(hipEvent_t*)> ev_guard(done, [](hipEvent_t* e) {
+        (void)hipEventDestroy(e[0]);
+        (void)hipEventDestroy(e[1]);
+    });
+    for (uint64_t off = 0, k = 0; off < n; off += chunk, ++k) {
+        const uint64_t len = std::min(chunk, n - off);
+        const int b = (int)(k & 1);
+        if (k >= 2) HZ_TRY(hipEventSynchronize(done[b]));  // buffer b's previous chunk is consumed
+        if ((rc = read_exact(fp, hin[b].p, len))) return rc;
+        if (off + len == n && (n & 1)) last_byte = hin[b].p[len - 1];
+        HZ_TRY(hipMemcpyAsync(din[b].p, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
+        if ((rc = hz_hist16(c, (const uint8_t*)din[b].p, len, (uint64_t*)dhist.p, 1))) return rc;
+        HZ_TRY(hipEventRecord(done[b], c->stream));
+    }
+    std::vector<uint64_t> hist(HZ_NSYM);
+    HZ_TRY(hipMemcpyAsync(hist.data(), dhist.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = hz_ctx_sync(c))) return rc;
+    std::unique_ptr<hz_codebook> cb(new hz_codebook());
+    if ((rc = hz_codebook_build(hist.data(), cb.get()))) return rc;
+    uint64_t hbits = 0, pbits = 0;
+    hz_header_bits(cb.get(), n, &hbits);
+    hz_payload_bits(cb.get(), hist.data(), &pbits);
+    if (verbose) {
+        std::cout << "The size of the sum of ORIGINAL files is: " << n << " bytes" << std::endl;
+        std::cout << "Unique symbols count: " << cb->nsym << std::endl;
+    }
+    // ---- header
+    std::vector<uint8_t> head(hbits / 8 + 8);
+    uint64_t hb;
+    uint32_t pend_bits;
+    uint8_t pend;
+    if ((rc = hz_header_write(cb.get(), n, last_byte, head.data(), head.size(), &hb, &pend_bits, &pend))) return rc;
+    FILE* fo = fopen(out_path, "wb");
+    if (!fo) return HZ_EIO;
+    std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
+    if (hb && fwrite(head.data(), 1, hb, fo) != hb) return HZ_EIO;
+    uint64_t written = hb;
+    const uint64_t nsym_total = n / 2;
+    if (nsym_total == 0) {
+        if (pend_bits && fwrite(&pend, 1, 1, fo) != 1) return HZ_EIO;
+        written += pend_bits ? 1 : 0;
+    } else {
+        // ---- pass 2: pack chunk by chunk at the running bit offset
+        if ((rc = hz_codebook_upload_encode(c, cb.get()))) return rc;
+        const uint64_t csym = chunk / 2;
+        const uint64_t out_cap = ((32 + csym * (uint64_t)cb->max_len + 31) / 32 + 1) * 4;
+        DevBuf dout, didx;
+        PinnedBuf hout;
+        if ((rc = dout.alloc(out_cap))) return rc;
+        if ((rc = hout.alloc(out_cap))) return rc;
+        if ((rc = didx.alloc(hz_index_bytes(csym)))) return rc;
+        if (fseek(fp, 0, SEEK_SET) != 0) return HZ_EIO;
+        uint32_t sbit = pend_bits;                       // bit of the chunk's first code in its first word
+        uint32_t lead = pend_bits ? (uint32_t)(pend >> (8 - pend_bits)) : 0u;
+        const uint64_t body = 2 * nsym_total;             // the odd last byte travels in the header
+        if ((rc = read_exact(fp, hin[0].p, std::min(chunk, body)))) return rc;
+        for (uint64_t off = 0, k = 0; off < body; off += chunk, ++k) {
+            const int b = (int)(k & 1);
+            const uint64_t len = std::min(chunk, body - off);
+            HZ_TRY(hipMemcpyAsync(din[b].p, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
+            if ((rc = hz_pack(c, (const uint8_t*)din[b].p, len, sbit, lead, (uint8_t*)dout.p, out_cap, (uint64_t*)didx.p)))
+                return rc;
+            const uint64_t nb = (len / 2 + 2047) / 2048;
+            uint64_t end_bit = 0;
+            HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
+            // the next chunk's fread overlaps this chunk's upload and pack
+            const uint64_t next = off + len;
+            if (next < body && (rc = read_exact(fp, hin[1 - b].p, std::min(chunk, body - next)))) return rc;
+            if ((rc = hz_ctx_sync(c))) return rc;
+            const bool last = next >= body;
+            const uint64_t bytes = last ? (end_bit + 7) / 8 : end_bit / 32 * 4;  // complete words until the end
+            const uint64_t copy = last ? bytes : (end_bit + 31) / 32 * 4;        // plus the partial word to carry
+            HZ_TRY(hipMemcpyAsync(hout.p, dout.p, copy, hipMemcpyDeviceToHost, c->stream));
+            if ((rc = hz_ctx_sync(c))) return rc;
+            if (bytes && fwrite(hout.p, 1, bytes, fo) != bytes) return HZ_EIO;
+            written += bytes;
+            sbit = (uint32_t)(end_bit % 32);
+            uint32_t w = 0;
+            if (sbit && !last) memcpy(&w, hout.p + bytes, 4);
+            lead = sbit ? (__builtin_bswap32(w) >> (32 - sbit)) : 0u;
+        }
+    }
+    if (written != (hbits + pbits + 7) / 8) return HZ_EFORMAT;
+    if (verbose) {
+        std::cout << "The size of the COMPRESSED file is: " << written << " bytes" << std::endl;
+        const float ratio = 100.0f * (float)written / (float)(n ? n : 1);
+        std::cout << "Compressed file's size is [" << ratio << "%] of the original files." << std::endl;
+        if (written > n) std::cout << "\nWARNING: The compressed file's size is larger than the sum of the originals.\n\n";
+        std::cout << std::endl << "Created compressed file: " << out_path << std::endl;
+        std::cout << "Compression is complete" << std::endl;
+    }
+    return HZ_OK;
+}
+
 extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     if ((!in && n) || !out_len) return HZ_EINVAL;
     std::vector<uint8_t> img;
@@ -594,34 +737,15 @@ extern "C" int hz_decode_host(const uint8_t* file, uint64_t len, uint8_t* out, u
 // Compressor.cu:315-632, stdout lines kept (:335-336,385,612-631).
 extern "C" int hz_archive_file(const char* path, int verbose) {
     if (!path) return HZ_EINVAL;
-    std::vector<uint8_t> in;
-    if (read_file(path, in)) {
+    struct stat st;
+    if (stat(path, &st) != 0) {
         if (verbose) std::cout << path << " file does not exist" << std::endl << "Process has been terminated" << std::endl;
         return HZ_EIO;
     }
-    const uint64_t n = in.size();
-    if (verbose) std::cout << "The size of the sum of ORIGINAL files is: " << n << " bytes" << std::endl;
-    std::vector<uint8_t> img;
-    uint32_t U = 0;
-    int rc = encode_image(in.data(), n, img, &U);
-    if (rc) {
-        if (verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;
-        return rc;
-    }
-    if (verbose) std::cout << "Unique symbols count: " << U << std::endl;
-    std::string outname = std::string(path) + ".compressed";
-    if ((rc = write_file(outname, img.data(), img.size()))) return rc;
-    if (verbose) {
-        const long sz = (long)img.size();
-        std::cout << "The size of the COMPRESSED file is: " << sz << " bytes" << std::endl;
-        const float ratio = 100.0f * (float)sz / (float)n;
-        std::cout << "Compressed file's size is [" << ratio << "%] of the original files." << std::endl;
-        if ((uint64_t)sz > n)
-            std::cout << "\nWARNING: The compressed file's size is larger than the sum of the originals.\n\n";
-        std::cout << std::endl << "Created compressed file: " << outname << std::endl;
-        std::cout << "Compression is complete" << std::endl;
-    }
-    return HZ_OK;
+    const std::string outname = std::string(path) + ".compressed";
+    const int rc = hz_archive_stream(path, outname.c_str(), kArchiveChunk, verbose);
+    if (rc && verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;
+    return rc;
 }
 
 // Decompressor.cu:47-114.

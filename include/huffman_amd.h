@@ -164,6 +164,12 @@ int hz_generate(hz_ctx *ctx, uint8_t *d_out, uint64_t n, uint64_t offset, int ki
 
 /* `archive <path>`: writes <path>.compressed (Compressor.cu:315-632). */
 int hz_archive_file(const char *path, int verbose);
+/* Streaming archive of in_path into out_path with bounded memory: two passes
+ * over the file in chunk_bytes pieces (histogram, then pack at the running bit
+ * offset with the previous chunk's partial word carried as `lead`). Output is
+ * byte-identical to the whole-buffer encoder. hz_archive_file uses it with
+ * 1 GiB chunks. Replaces the whole-file buffers of Compressor.cu:343-367,585-601. */
+int hz_archive_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* `extract <path>`: writes ./DECOMPRESSED_FILE or DECOMPRESSED_FILE(k)
  * (Decompressor.cu:47-114,185-219). out_name may be NULL. */
 int hz_extract_file(const char *path, char *out_name, size_t out_name_cap, int verbose);

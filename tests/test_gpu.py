@@ -149,6 +149,31 @@ def test_cli_exit_codes(hz, tmp_path):
 
 
 # ---- device pipeline at scale --------------------------------------------------------
+# ---- streaming archive (bounded memory) ---------------------------
+@pytest.mark.parametrize("n,chunk", [((5 << 20) + 3, 1 << 20), (10001, 64), (4096 * 3, 4096), (4096 * 3 + 1, 4096),
+                                     (0, 4096), (1, 4096), (3, 64), (1 << 20, 1 << 20), ((1 << 20) + 2, 1 << 20)])
+def test_archive_stream_matches_whole_buffer(hz, tmp_path, n, chunk):
+    data = _zipf_bytes(n, n + 7)
+    src = tmp_path / "in.bin"
+    src.write_bytes(data)
+    out = hz.archive_stream(src, tmp_path / "in.bin.compressed", chunk_bytes=chunk)
+    blob = open(out, "rb").read()
+    assert blob == oracle_lib.encode(data)
+    assert hz.decode(blob) == data
+
+
+@pytest.mark.parametrize("kind", ["fib28", "uniform"])
+def test_archive_stream_table_modes(hz, tmp_path, kind):
+    if kind == "fib28":
+        data = _fib_input(28)                                  # WIDE tables, codes up to 28 bits
+    else:
+        data = np.random.default_rng(5).integers(0, 256, 1 << 21, dtype=np.uint8).tobytes()  # FIXED16
+    src = tmp_path / "in.bin"
+    src.write_bytes(data)
+    blob = open(hz.archive_stream(src, tmp_path / "o", chunk_bytes=4096 * 5 + 16), "rb").read()
+    assert blob == oracle_lib.encode(data)
+
+
 def test_generator_matches_oracle(codec):
     import torch
     n = 1 << 24
