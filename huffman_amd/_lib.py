@@ -82,6 +82,7 @@ PROTOTYPES = [
     ("hz_generate", _I, [_P, _P, _U64, _U64, _I, ctypes.c_double, _U64]),
     ("hz_archive_file", _I, [ctypes.c_char_p, _I]),
     ("hz_archive_stream", _I, [ctypes.c_char_p, ctypes.c_char_p, _U64, _I]),
+    ("hz_extract_stream", _I, [ctypes.c_char_p, ctypes.c_char_p, _U64, _I]),
     ("hz_extract_file", _I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, _I]),
     ("hz_encode_host", _I, [_P, _U64, _P, _U64, ctypes.POINTER(_U64)]),
     ("hz_encoded_size", _I, [_P, _U64, ctypes.POINTER(_U64)]),

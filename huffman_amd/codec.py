@@ -66,6 +66,13 @@ def archive_stream(path, out_path, chunk_bytes=1 << 30, verbose=False):
     return str(out_path)
 
 
+def extract_stream(path, out_path, chunk_bytes=1 << 30, verbose=False):
+    """Streaming `extract` with bounded memory (payload windows of chunk_bytes)."""
+    check(load().hz_extract_stream(str(path).encode(), str(out_path).encode(), chunk_bytes, int(verbose)),
+          "hz_extract_stream")
+    return str(out_path)
+
+
 def extract(path, verbose=True):
     """`extract <path>`: writes ./DECOMPRESSED_FILE (or (k)); returns its name."""
     name = ctypes.create_string_buffer(256)

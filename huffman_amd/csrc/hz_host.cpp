@@ -697,6 +697,118 @@ extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint
     return HZ_OK;
 }
 
+// Streaming extract: the payload passes through a device window of chunk_bytes.
+// Each round decodes as many symbols as the window surely holds (the file's
+// mean code length with a margin; a round whose codes overrun the window is
+// redone at the max_len bound), writes them out, and moves the unconsumed
+// tail of the window to the front of the other buffer before refilling it.
+extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+    if (!in_path || !out_path || chunk_bytes < 4096) return HZ_EINVAL;
+    chunk_bytes &= ~(uint64_t)15;
+    struct stat st;
+    if (stat(in_path, &st) != 0) return HZ_EIO;
+    const uint64_t fsize = (uint64_t)st.st_size;
+    FILE* fp = fopen(in_path, "rb");
+    if (!fp) return HZ_EIO;
+    std::unique_ptr<FILE, int (*)(FILE*)> fin(fp, fclose);
+    // the header is at most 12 + 65536 * (3 + 8) bytes
+    std::vector<uint8_t> head(std::min<uint64_t>(fsize, 1u << 20));
+    int rc = read_exact(fp, head.data(), head.size());
+    if (rc) return rc;
+    std::unique_ptr<hz_codebook> cb(new hz_codebook());
+    hz_header_info info;
+    if ((rc = hz_header_parse(head.data(), head.size(), cb.get(), &info))) return rc;
+    FILE* fo = fopen(out_path, "wb");
+    if (!fo) return HZ_EIO;
+    std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
+    const uint64_t nsym = info.n / 2;
+    if (nsym > 0) {
+        hz_ctx* c;
+        if ((rc = default_ctx(&c))) return rc;
+        HZ_TRY(hipSetDevice(c->device));
+        if ((rc = hz_codebook_upload_decode(c, cb.get()))) return rc;
+        const uint64_t W = chunk_bytes;               // window bytes
+        const uint64_t pay_total = fsize > info.payload_byte ? fsize - info.payload_byte : 0;
+        const uint64_t max_len = std::max<uint32_t>(cb->max_len, 1);
+        // mean bits per symbol of this file, 3% margin (a mispredicted round is redone exactly)
+        const double mean = pay_total ? ((double)pay_total * 8 - info.payload_bit) / (double)nsym : (double)max_len;
+        const uint64_t sym_cap = std::max<uint64_t>(W / 2, kBlockSyms);  // output per round <= W bytes
+        DevBuf dwin[2], didx, dout;
+        PinnedBuf hin, hout;
+        for (int i = 0; i < 2; ++i)
+            if ((rc = dwin[i].alloc(W + 16))) return rc;
+        if ((rc = didx.alloc(hz_index_bytes(sym_cap)))) return rc;
+        if ((rc = dout.alloc(2 * sym_cap + 16))) return rc;
+        if ((rc = hin.alloc(W))) return rc;
+        if ((rc = hout.alloc(2 * sym_cap))) return rc;
+        if (fseek(fp, (long)info.payload_byte, SEEK_SET) != 0) return HZ_EIO;
+        uint64_t file_left = pay_total, have = 0, done = 0;
+        uint64_t bit = info.payload_bit;
+        int cur = 0;
+        // first fill
+        uint64_t r = std::min(W, file_left);
+        if ((rc = read_exact(fp, hin.p, r))) return rc;
+        HZ_TRY(hipMemsetAsync(dwin[cur].p, 0, W + 16, c->stream));
+        HZ_TRY(hipMemcpyAsync(dwin[cur].p, hin.p, r, hipMemcpyHostToDevice, c->stream));
+        have = r;
+        file_left -= r;
+        while (done < nsym) {
+            const uint64_t left = nsym - done;
+            const uint64_t avail = have * 8 - bit;
+            uint64_t k;
+            if (file_left == 0) {
+                k = std::min(left, sym_cap);
+            } else {
+                k = (uint64_t)((double)avail / (mean * 1.03));
+                k = std::min(std::min(left, sym_cap), k);
+                if (k < left) k = std::max<uint64_t>(k / kBlockSyms * kBlockSyms, 1);
+            }
+            uint64_t end_bit = 0;
+            for (int attempt = 0;; ++attempt) {
+                if ((rc = hz_index_build(c, (const uint8_t*)dwin[cur].p, have, bit, k, (uint64_t*)didx.p))) return rc;
+                HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(k), 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+                if ((rc = hz_ctx_sync(c))) return rc;
+                if (end_bit <= have * 8 || file_left == 0) break;
+                if (attempt) return HZ_EFORMAT;
+                k = std::max<uint64_t>(avail / max_len, 1);  // codes surely inside the window
+            }
+            if (end_bit > have * 8) return HZ_EFORMAT;    // truncated file
+            if ((rc = hz_decode(c, (const uint8_t*)dwin[cur].p, have, k, (const uint64_t*)didx.p, (uint8_t*)dout.p)))
+                return rc;
+            HZ_TRY(hipMemcpyAsync(hout.p, dout.p, 2 * k, hipMemcpyDeviceToHost, c->stream));
+            // move the unconsumed tail to the other window and refill it behind
+            const uint64_t used = end_bit / 8, tail = have - used;
+            const int nxt = cur ^ 1;
+            if (done + k < nsym) {
+                if (tail) HZ_TRY(hipMemcpyAsync(dwin[nxt].p, (const uint8_t*)dwin[cur].p + used, tail,
+                                                hipMemcpyDeviceToDevice, c->stream));
+                r = std::min(W - tail, file_left);
+                if ((rc = read_exact(fp, hin.p, r))) return rc;  // overlaps the decode
+            } else {
+                r = 0;
+            }
+            if ((rc = hz_ctx_sync(c))) return rc;    // decode, output copy and tail move done
+            if (fwrite(hout.p, 1, 2 * k, fo) != 2 * k) return HZ_EIO;
+            done += k;
+            if (done < nsym) {
+                if (r < W - tail) HZ_TRY(hipMemsetAsync((uint8_t*)dwin[nxt].p + tail + r, 0, W + 16 - tail - r, c->stream));
+                if (r) HZ_TRY(hipMemcpyAsync((uint8_t*)dwin[nxt].p + tail, hin.p, r, hipMemcpyHostToDevice, c->stream));
+                have = tail + r;
+                file_left -= r;
+                bit = end_bit % 8;
+                cur = nxt;
+            }
+        }
+    }
+    if (info.is_odd) {
+        const uint8_t b = (uint8_t)info.last_byte;
+        if (fwrite(&b, 1, 1, fo) != 1) return HZ_EIO;
+    }
+    if (verbose) std::cout << "Decompression is complete" << std::endl;
+    return HZ_OK;
+}
+
 extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     if ((!in && n) || !out_len) return HZ_EINVAL;
     std::vector<uint8_t> img;
@@ -751,19 +863,18 @@ extern "C" int hz_archive_file(const char* path, int verbose) {
 // Decompressor.cu:47-114.
 extern "C" int hz_extract_file(const char* path, char* out_name, size_t out_name_cap, int verbose) {
     if (!path) return HZ_EINVAL;
-    std::vector<uint8_t> f;
-    if (read_file(path, f)) {
+    struct stat st;
+    if (stat(path, &st) != 0) {
         if (verbose) std::cout << path << " does not exist" << std::endl;
         return HZ_EIO;
     }
-    std::vector<uint8_t> dec;
-    int rc = decode_image(f.data(), f.size(), dec);
+    std::string name = output_name();
+    int rc = hz_extract_stream(path, name.c_str(), kArchiveChunk, 0);
     if (rc) {
+        remove(name.c_str());
         if (verbose) std::cerr << "extract: " << hz_strerror(rc) << std::endl;
         return rc;
     }
-    std::string name = output_name();
-    if ((rc = write_file(name, dec.data(), dec.size()))) return rc;
     if (out_name && out_name_cap) {
         strncpy(out_name, name.c_str(), out_name_cap - 1);
         out_name[out_name_cap - 1] = 0;

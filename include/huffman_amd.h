@@ -170,6 +170,11 @@ int hz_archive_file(const char *path, int verbose);
  * byte-identical to the whole-buffer encoder. hz_archive_file uses it with
  * 1 GiB chunks. Replaces the whole-file buffers of Compressor.cu:343-367,585-601. */
 int hz_archive_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
+/* Streaming extract of in_path into out_path through a device window of
+ * chunk_bytes of payload (index-less: hz_index_build per window), bounded
+ * host and device memory. hz_extract_file uses it with 1 GiB windows.
+ * Replaces the whole-file buffers of Decompressor.cu:65-114,259-291. */
+int hz_extract_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* `extract <path>`: writes ./DECOMPRESSED_FILE or DECOMPRESSED_FILE(k)
  * (Decompressor.cu:47-114,185-219). out_name may be NULL. */
 int hz_extract_file(const char *path, char *out_name, size_t out_name_cap, int verbose);

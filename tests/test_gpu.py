@@ -174,6 +174,40 @@ def test_archive_stream_table_modes(hz, tmp_path, kind):
     assert blob == oracle_lib.encode(data)
 
 
+def _hetero_bytes(n, seed=3):
+    """Incompressible first half, one repeated symbol after: the file's mean
+    code length underestimates the first half (the window retry path)."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, n // 2, dtype=np.uint8)
+    return (a.tobytes() + b"\x07\x01" * ((n - n // 2) // 2) + b"\x05" * (n % 2))
+
+
+@pytest.mark.parametrize("kind,n,window", [("zipf", (5 << 20) + 3, 4096), ("zipf", (5 << 20) + 3, 1 << 16),
+                                           ("zipf", 10001, 4096), ("zipf", 0, 4096), ("zipf", 1, 4096),
+                                           ("zipf", 3, 4096), ("hetero", 3 << 20, 1 << 16),
+                                           ("hetero", (1 << 20) + 1, 5000), ("fib28", 0, 4096),
+                                           ("uniform", 1 << 21, 1 << 15)])
+def test_extract_stream_roundtrip(hz, tmp_path, kind, n, window):
+    if kind == "zipf":
+        data = _zipf_bytes(n, n + 11)
+    elif kind == "hetero":
+        data = _hetero_bytes(n)
+    elif kind == "fib28":
+        data = _fib_input(28)
+    else:
+        data = np.random.default_rng(9).integers(0, 256, n, dtype=np.uint8).tobytes()
+    blob = oracle_lib.encode(data)
+    (tmp_path / "in.compressed").write_bytes(blob)
+    out = hz.extract_stream(tmp_path / "in.compressed", tmp_path / "out", chunk_bytes=window)
+    assert open(out, "rb").read() == data
+
+
+@pytest.mark.parametrize("name", INPUTS)
+def test_extract_stream_baseline_files(hz, tmp_path, name):
+    out = hz.extract_stream(os.path.join(GOLD, name + ".baseline.compressed"), tmp_path / "out", chunk_bytes=4096)
+    assert open(out, "rb").read() == read(name)
+
+
 def test_generator_matches_oracle(codec):
     import torch
     n = 1 << 24
