@@ -1414,9 +1414,12 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
                        (const unsigned long long*)tiles, first);
     uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
+    // end bit = all ones unless the payload holds nsym codewords (k_sync_emit writes it then)
+    hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(256), lds, s, a, y, exits, (const unsigned long long*)first,
                        d_index, subs);
-    hipError_t e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
+    e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
     if (e != hipSuccess) return e;
     uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
     sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;

@@ -146,7 +146,8 @@ int hz_decode(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uin
               const uint64_t *d_index, uint8_t *d_out);
 
 /* Build the block index of an index-less stream (a .compressed file from
- * the reference encoder) on the device. */
+ * the reference encoder) on the device. If the payload holds fewer than nsym
+ * codewords, start[nblocks] (the end bit) is left at UINT64_MAX. */
 int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                    uint64_t nsym, uint64_t *d_index);
 
