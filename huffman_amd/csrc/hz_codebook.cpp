@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <queue>
 #include <vector>
 
 #include "huffman_amd.h"
@@ -429,11 +430,86 @@ static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t 
         const size_t off = l2.size();
         if (off + (1ull << nb2) >= (1ull << 26)) return HZ_ENOMEM;
         l2.resize(off + (1ull << nb2), 0u);
-        tab[base + q] = (nb2 << 26) | (uint32_t)off;  // (tab may alias l2: index, not pointer)
+        tab[base + q] = (nb2 << 26) | (uint32_t)off;  // nb2 <= 8 (4 bits); bit 30 = LDS link  // (tab may alias l2: index, not pointer)
         const int rc = fill_level(cb, l2, off, nb2, D + nb, order.data() + cnt[q], cnt[q + 1] - cnt[q], l2);
         if (rc) return rc;
     }
     return HZ_OK;
+}
+
+// Hot second level in the LDS image. The LDS left after level 1 and the
+// decoder's staging slots (16 waves, slots sized from the Kraft-weighted mean
+// code length) holds c-bit heads of the most used global subtables: entry j
+// of a head is the leaf its range resolves to, or a link to the rest of the
+// global subtable. Choice: greedy by decoded-mass per LDS word; the Kraft
+// weight 2^-L of a code stands in for its frequency, so each global entry of
+// an nb-bit subtable under level 1 carries mass 2^-(K1+nb).
+static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, const std::vector<uint32_t>& l2, int K1) {
+    static const long env = getenv("HZ_DEC_L2LDS") ? atol(getenv("HZ_DEC_L2LDS")) : -1;  // tuning: words
+    double kbits = 0.0;
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) kbits += ldexp((double)cb->len[s], -(int)cb->len[s]);
+    const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
+    const long room = (long)(kLdsBytes / 4) - (long)img.size() -
+                      (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64;
+    long budget = env >= 0 ? env : room;
+    if (budget < 64) return;
+    struct Head { uint32_t q, nb, off, c; };
+    std::vector<Head> heads;
+    std::vector<std::vector<uint32_t>> resolved;  // per head: entries resolved within c bits, c = 1..nb
+    for (uint32_t q = 0; q < img.size(); ++q) {
+        const uint32_t e = img[q];
+        if (e & kLeafBit) continue;
+        const uint32_t nb = (e >> 26) & 15u, off = e & 0x3ffffffu;
+        std::vector<uint32_t> r(nb + 1, 0u);
+        for (uint32_t t = 0; t < (1u << nb); ++t) {
+            const uint32_t x = l2[off + t];
+            if (!(x & kLeafBit)) continue;
+            const uint32_t rem = ((x >> 16) & 63u) - (uint32_t)K1;
+            for (uint32_t c = rem; c <= nb; ++c) r[c]++;
+        }
+        heads.push_back({q, nb, off, 0});
+        resolved.push_back(std::move(r));
+    }
+    // marginal greedy: mass gain (in units of 2^-(K1+nb) per entry) per added LDS word
+    struct Cand { double rate; uint32_t h, c; bool operator<(const Cand& o) const { return rate < o.rate; } };
+    std::priority_queue<Cand> pq;
+    auto push = [&](uint32_t h) {
+        const Head& hd = heads[h];
+        const double unit = ldexp(1.0, -(K1 + (int)hd.nb));
+        const uint32_t cs = hd.c ? (1u << hd.c) : 0u, cr = hd.c ? resolved[h][hd.c] : 0u;
+        Cand best{0.0, h, 0};
+        for (uint32_t c = hd.c + 1; c <= hd.nb; ++c) {
+            const double rate = unit * (double)(resolved[h][c] - cr) / (double)((1u << c) - cs);
+            if (rate > best.rate) best = {rate, h, c};
+        }
+        if (best.c) pq.push(best);
+    };
+    for (uint32_t h = 0; h < heads.size(); ++h) push(h);
+    long used = 0;
+    while (!pq.empty()) {
+        const Cand cd = pq.top();
+        pq.pop();
+        Head& hd = heads[cd.h];
+        if (cd.c <= hd.c) continue;
+        const long add = (long)(1u << cd.c) - (hd.c ? (long)(1u << hd.c) : 0);
+        if (used + add > budget) continue;
+        used += add;
+        hd.c = cd.c;
+        push(cd.h);
+    }
+    for (const Head& hd : heads) {
+        if (!hd.c) continue;
+        const uint32_t o = (uint32_t)img.size(), rest = hd.nb - hd.c;
+        for (uint32_t j = 0; j < (1u << hd.c); ++j) {
+            const uint32_t t0 = hd.off + (j << rest);
+            const uint32_t x = l2[t0];
+            const bool done = (x & kLeafBit) && ((x >> 16) & 63u) - (uint32_t)K1 <= hd.c;
+            img.push_back(done ? x : (rest ? ((rest << 26) | t0) : x));
+        }
+        img[hd.q] = kDecLdsLink | (hd.c << 26) | o;
+    }
+    while (img.size() & 3) img.push_back(leaf(1, 0));
 }
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
@@ -455,6 +531,7 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     for (auto& e : img) if (!e) e = leaf(1, 0);
     for (auto& e : l2) if (!e) e = leaf(1, 0);
     if (l2.empty()) l2.push_back(leaf(1, 0));
+    add_lds_level(cb, img, l2, K1);
     return HZ_OK;
 }
 

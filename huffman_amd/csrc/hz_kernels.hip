@@ -859,6 +859,7 @@ struct DecArgs {
     const uint32_t* l2;
     uint8_t* out;
     uint32_t* err;
+    int group2;              // k_decode: allow two blocks per wave
 };
 
 template <int MODE>
@@ -874,9 +875,10 @@ HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint
     } else {
         uint32_t e = lds[(uint32_t)(win >> (64 - a.k))];
         uint32_t D = (uint32_t)a.k;
-        while (!(e >> 31)) {
-            const uint32_t nb = (e >> 26) & 31u;
-            e = a.l2[(e & 0x3ffffffu) + (uint32_t)((win << D) >> (64 - nb))];
+        while (!(e >> 31)) {  // link: bit 30 = subtable in the LDS image, else in l2
+            const uint32_t nb = (e >> 26) & 15u;
+            const uint32_t i = (e & 0x3ffffffu) + (uint32_t)((win << D) >> (64 - nb));
+            e = (e & kDecLdsLink) ? lds[i] : a.l2[i];
             D += nb;
         }
         L = (e >> 16) & 63u;
@@ -901,6 +903,153 @@ HZ_DEV uint64_t stage_window(const uint32_t* stg, uint32_t pos) {
     return (two << sh) | ((((uint64_t)stg[wi + 2]) << sh) >> 32);
 }
 
+// Stage payload words [w0, w0 + 4 npc) of block b into `stg`, byte-swapped.
+template <bool WIDE>
+HZ_DEV void dec_stage(const DecArgs& a, uint64_t b0, uint64_t b1, uint32_t npc_max, uint32_t* stg, int lane,
+                      uint64_t& w0) {
+    w0 = (b0 >> 5) & ~3ull;
+    const uint64_t wend = (b1 >> 5) + (WIDE ? 3 : 2);
+    uint32_t npc = (uint32_t)((wend - w0 + 3) >> 2);
+    npc = npc < npc_max ? npc : npc_max;
+    for (uint32_t p = lane; p < npc; p += kWave) {
+        const uint64_t w = w0 + 4ull * p;
+        uint4 v;
+        if (w + 4 <= a.nwords) {
+            v = *reinterpret_cast<const uint4*>(a.words + w);
+        } else {
+            v.x = w < a.nwords ? a.words[w] : 0u;
+            v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
+            v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
+            v.w = 0u;
+        }
+        reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+    }
+}
+
+// Chain start bits of the lane relative to the block start (index sub[]);
+// offsets are mod 2^16, rebuilt from deltas when the block is that long.
+HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bits, int lane, uint32_t (&off)[kChainsPerLane]) {
+    constexpr int C = kChainsPerLane;
+#pragma unroll
+    for (int c = 0; c < C; ++c) off[c] = (uint32_t)(sub >> (16 * c)) & 0xffffu;
+    if (bits >= 65536) {
+        uint32_t pv = shfl_up_u32(off[C - 1], 1);
+        if (lane == 0) pv = 0;
+        uint32_t d[C], sc = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) { d[c] = (off[c] - pv) & 0xffffu; pv = off[c]; sc += d[c]; }
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t o = shfl_up_u32(sc, dd);
+            if (lane >= dd) sc += o;
+        }
+#pragma unroll
+        for (int c = C - 1; c >= 0; --c) { off[c] = sc; sc -= d[c]; }
+    }
+}
+
+// 32 symbols = 64 contiguous output bytes of the lane in block b.
+HZ_DEV void dec_store(const DecArgs& a, uint64_t b, int lane, const uint32_t* pk) {
+    const uint64_t sym0 = b * kBlockSyms + (uint64_t)lane * kSPT;
+    if (sym0 + kSPT <= a.nsym) {
+        uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+    } else if (sym0 < a.nsym) {
+        uint8_t* ob = a.out + 2 * sym0;
+        const uint32_t cnt = (uint32_t)(a.nsym - sym0);
+        for (uint32_t q = 0; q < cnt; ++q) {
+            const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+            ob[2 * q] = (uint8_t)v;
+            ob[2 * q + 1] = (uint8_t)(v >> 8);
+        }
+    }
+}
+
+// One wave decodes NB blocks at once (NB * kChainsPerLane independent chains
+// per lane: every table wait covers more symbols). Block g of the group uses
+// staging slot g. Blocks past the stream's end decode nothing.
+template <int MODE, bool WIDE, int NB>
+HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uint32_t slot, uint64_t bfirst,
+                      int lane) {
+    constexpr int C1 = kChainsPerLane;
+    constexpr int C = NB * C1;
+    const uint32_t npc_max = slot >> 2;
+    uint32_t pos[C];
+#pragma unroll
+    for (int g = 0; g < NB; ++g) {
+        const uint64_t b = bfirst + g < a.nblocks ? bfirst + g : a.nblocks - 1;  // duplicates decode, never store
+        const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
+        const uint64_t sub = a.subs[b * kWave + lane];
+        uint64_t w0;
+        dec_stage<WIDE>(a, b0, b1, npc_max, stg0 + g * slot, lane, w0);
+        uint32_t off[C1];
+        dec_chain_offsets(sub, b1 - b0, lane, off);
+        const uint32_t base = (uint32_t)(b0 - (w0 << 5)) + (uint32_t)g * slot * 32u;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) pos[g * C1 + c] = base + off[c];
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+    uint32_t pk[NB][kSPT / 2];
+#pragma unroll
+    for (int q = 0; q < kChainSyms; ++q) {
+        uint64_t win[C];
+        uint32_t sym[C], L[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) win[c] = stage_window<WIDE>(stg0, pos[c]);
+        if (MODE == DEC_DENSE) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
+        } else {
+            uint32_t e[C], e2[C], D[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) { e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))]; D[c] = (uint32_t)a.k; }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {  // LDS-resident second level (hot subtables)
+                if ((e[c] >> 30) == 1u) {
+                    const uint32_t nb = (e[c] >> 26) & 15u;
+                    e[c] = lds[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << D[c]) >> (64 - nb))];
+                    D[c] += nb;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {  // first global level of every chain before one wait
+                e2[c] = e[c];
+                if (!(e[c] >> 31)) {
+                    const uint32_t nb = (e[c] >> 26) & 15u;
+                    e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << D[c]) >> (64 - nb))];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                uint32_t ee = e2[c];
+                if (!(e[c] >> 31)) {
+                    uint32_t Dd = D[c] + ((e[c] >> 26) & 15u);
+                    while (!(ee >> 31)) {  // deeper global levels: rare
+                        const uint32_t nb = (ee >> 26) & 15u;
+                        ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[c] << Dd) >> (64 - nb))];
+                        Dd += nb;
+                    }
+                }
+                L[c] = (ee >> 16) & 63u;
+                sym[c] = ee & 0xffffu;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            pos[c] += L[c];
+            const int g = c / C1;
+            const int i = ((c % C1) * kChainSyms + q) >> 1;  // symbol (c%C1)*8+q of the lane in block g
+            if (q & 1) pk[g][i] |= sym[c] << 16;
+            else pk[g][i] = sym[c];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < NB; ++g)
+        if (bfirst + g < a.nblocks) dec_store(a, bfirst + g, lane, pk[g]);
+}
+
 template <int MODE, bool WIDE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -909,117 +1058,20 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     const uint32_t wid = threadIdx.x >> 6;
     // slots fit the stream's largest block; waves without a slot have nothing to do
     const uint32_t slot = dec_slot_words(a.starts[a.nblocks + 1], a.max_len);
-    uint32_t nw = a.region_words / slot;
-    nw = nw < (blockDim.x >> 6) ? nw : (blockDim.x >> 6);
+    const uint32_t nwave = blockDim.x >> 6;
+    // two blocks per wave when that keeps at least kDecMinWaves2 waves busy
+    const bool two = a.group2 && a.region_words / (2 * slot) >= (uint32_t)kDecMinWaves2;
+    const uint32_t per = two ? 2 * slot : slot;
+    uint32_t nw = a.region_words / per;
+    nw = nw < nwave ? nw : nwave;
     if (wid >= nw) return;
-    uint32_t* stg = lds + a.lds_words + wid * slot;
-    const uint32_t npc_max = slot >> 2;
-    for (uint64_t b = (uint64_t)blockIdx.x * nw + wid; b < a.nblocks; b += (uint64_t)gridDim.x * nw) {
-        const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
-        const uint64_t sub = a.subs[b * kWave + lane];
-        // ---- stage words [w0, w0 + 4 npc) of the payload, byte-swapped
-        const uint64_t w0 = (b0 >> 5) & ~3ull;
-        const uint64_t wend = (b1 >> 5) + (WIDE ? 3 : 2);
-        uint32_t npc = (uint32_t)((wend - w0 + 3) >> 2);
-        npc = npc < npc_max ? npc : npc_max;
-        for (uint32_t p = lane; p < npc; p += kWave) {
-            const uint64_t w = w0 + 4ull * p;
-            uint4 v;
-            if (w + 4 <= a.nwords) {
-                v = *reinterpret_cast<const uint4*>(a.words + w);
-            } else {
-                v.x = w < a.nwords ? a.words[w] : 0u;
-                v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
-                v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
-                v.w = 0u;
-            }
-            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
-        }
-        __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
-        // ---- chain start bits, relative to the slot
-        constexpr int C = kChainsPerLane;
-        uint32_t off[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) off[c] = (uint32_t)(sub >> (16 * c)) & 0xffffu;
-        if (b1 - b0 >= 65536) {  // offsets are mod 2^16: rebuild them from deltas
-            uint32_t pv = shfl_up_u32(off[C - 1], 1);
-            if (lane == 0) pv = 0;
-            uint32_t d[C], sc = 0;
-#pragma unroll
-            for (int c = 0; c < C; ++c) { d[c] = (off[c] - pv) & 0xffffu; pv = off[c]; sc += d[c]; }
-#pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1) {
-                const uint32_t o = shfl_up_u32(sc, dd);
-                if (lane >= dd) sc += o;
-            }
-#pragma unroll
-            for (int c = C - 1; c >= 0; --c) { off[c] = sc; sc -= d[c]; }
-        }
-        const uint32_t base = (uint32_t)(b0 - (w0 << 5));
-        uint32_t pos[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) pos[c] = base + off[c];
-        uint32_t pk[kSPT / 2];
-#pragma unroll
-        for (int q = 0; q < kChainSyms; ++q) {
-            uint64_t win[C];
-            uint32_t sym[C], L[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) win[c] = stage_window<WIDE>(stg, pos[c]);
-            if (MODE == DEC_DENSE) {
-#pragma unroll
-                for (int c = 0; c < C; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
-            } else {
-                uint32_t e[C], e2[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))];
-#pragma unroll
-                for (int c = 0; c < C; ++c) {  // first deeper level of every chain before one wait
-                    e2[c] = e[c];
-                    if (!(e[c] >> 31)) {
-                        const uint32_t nb = (e[c] >> 26) & 31u;
-                        e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << a.k) >> (64 - nb))];
-                    }
-                }
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    uint32_t ee = e2[c];
-                    if (!(e[c] >> 31)) {
-                        uint32_t D = (uint32_t)a.k + ((e[c] >> 26) & 31u);
-                        while (!(ee >> 31)) {  // deeper than k1 + 8 bits: rare
-                            const uint32_t nb = (ee >> 26) & 31u;
-                            ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[c] << D) >> (64 - nb))];
-                            D += nb;
-                        }
-                    }
-                    L[c] = (ee >> 16) & 63u;
-                    sym[c] = ee & 0xffffu;
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                pos[c] += L[c];
-                const int i = (c * kChainSyms + q) >> 1;  // symbol c*8+q of the lane
-                if (q & 1) pk[i] |= sym[c] << 16;
-                else pk[i] = sym[c];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // ---- 32 symbols = 64 contiguous output bytes per lane
-        const uint64_t sym0 = b * kBlockSyms + (uint64_t)lane * kSPT;
-        if (sym0 + kSPT <= a.nsym) {
-            uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
-        } else if (sym0 < a.nsym) {
-            uint8_t* ob = a.out + 2 * sym0;
-            const uint32_t cnt = (uint32_t)(a.nsym - sym0);
-            for (uint32_t q = 0; q < cnt; ++q) {
-                const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-                ob[2 * q] = (uint8_t)v;
-                ob[2 * q + 1] = (uint8_t)(v >> 8);
-            }
-        }
+    uint32_t* stg = lds + a.lds_words + wid * per;
+    if (two) {
+        for (uint64_t g = (uint64_t)blockIdx.x * nw + wid; 2 * g < a.nblocks; g += (uint64_t)gridDim.x * nw)
+            dec_group<MODE, WIDE, 2>(a, lds, stg, slot, 2 * g, lane);
+    } else {
+        for (uint64_t b = (uint64_t)blockIdx.x * nw + wid; b < a.nblocks; b += (uint64_t)gridDim.x * nw)
+            dec_group<MODE, WIDE, 1>(a, lds, stg, slot, b, lane);
     }
 }
 
@@ -1092,6 +1144,7 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
     a.min_len = t.dec_min_len;
     a.max_len = t.dec_max_len;
     a.l2 = t.d_dec_l2;
+    a.group2 = 0;
 }
 
 // Launch shape: slots are sized for the average block (estimated from the
@@ -1108,26 +1161,37 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
         if (e != hipSuccess) return e;
         attr = true;
     }
+    static const int group_env = [] { const char* v = getenv("HZ_DEC_GROUP"); return v ? atoi(v) : 1; }();
     const uint64_t avg = (payload_bits + a.nblocks - 1) / a.nblocks;
     const uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
     const uint32_t worst = dec_slot_words_max(a.max_len);
     const uint32_t table = a.lds_words;
+    DecArgs b = a;
+    b.group2 = 0;
     int best_w = 0, best_g = 1;
-    for (int g = 1; g <= 2; ++g) {
-        const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
-        if (room <= table + est) continue;
-        int w = (int)((room - table) / est);
+    // two blocks per wave, one workgroup per CU, when enough waves get slots
+    if (group_env == 2 && kLdsBytes / 4 > table + 2 * est) {
+        int w = (int)((kLdsBytes / 4 - table) / (2 * est));
         w = w > kDecMaxWaves ? kDecMaxWaves : w;
-        if (g * w > best_g * best_w) { best_w = w; best_g = g; }
+        if (w >= kDecMinWaves2) { best_w = w; b.group2 = 1; }
+    }
+    if (!b.group2) {
+        for (int g = 1; g <= 2; ++g) {
+            const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
+            if (room <= table + est) continue;
+            int w = (int)((room - table) / est);
+            w = w > kDecMaxWaves ? kDecMaxWaves : w;
+            if (g * w > best_g * best_w) { best_w = w; best_g = g; }
+        }
     }
     if (best_w == 0) return hipErrorInvalidValue;
-    DecArgs b = a;
-    b.region_words = (uint32_t)best_w * est;
+    b.region_words = (uint32_t)best_w * est * (b.group2 ? 2 : 1);
     if (b.region_words < worst && table + worst <= kLdsBytes / 4) b.region_words = worst;  // any stream decodes
     if (table + b.region_words > kLdsBytes / 4 / (uint32_t)best_g) best_g = 1;
     if (table + b.region_words > kLdsBytes / 4) return hipErrorInvalidValue;
     const uint32_t lds = 4 * (table + b.region_words);
-    uint64_t wgs = (a.nblocks + best_w - 1) / best_w;
+    const uint64_t units = b.group2 ? (a.nblocks + 1) / 2 : a.nblocks;
+    uint64_t wgs = (units + best_w - 1) / best_w;
     const uint64_t cap = (uint64_t)ncu * best_g;
     if (wgs > cap) wgs = cap;
     hipLaunchKernelGGL((k_decode<MODE, WIDE>), dim3(wgs), dim3(64 * best_w), lds, s, b);

@@ -1,0 +1,26 @@
+"""Profiling harness: encode one synthetic stream on the device, then run
+pack and decode R more times (rocprofv3 --pmc passes attribute counters per kernel).
+usage: python tools/debug/stage_loop.py [bytes] [reps] [zipf|uniform] [stages]"""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch
+from huffman_amd.pipeline import StreamCodec
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4 << 30
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+kind = 0 if (len(sys.argv) > 3 and sys.argv[3] == "uniform") else 1
+stages = sys.argv[4] if len(sys.argv) > 4 else "hpd"
+c = StreamCodec(0)
+x = torch.empty(n, dtype=torch.uint8, device='cuda')
+c.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=42)
+plan, pay, idx = c.encode(x)
+out = torch.empty(n + 16, dtype=torch.uint8, device='cuda')
+for r in range(reps):
+    if "h" in stages:
+        c.histogram(x)
+    if "p" in stages:
+        c.pack(x, plan, pay, idx)
+    if "d" in stages:
+        c.decode(pay, n // 2, idx, out)
+    c.sync()
+    print("rep", r, c.kernel_ms(), flush=True)
+print('ok', torch.equal(out[:n - (n & 1)], x[:n - (n & 1)]))
