@@ -446,6 +446,30 @@ HZ_DEV void pack_emit(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& acc,
     }
 }
 
+// Branch-free emit into the wave's LDS slot. t = bit position in the slot;
+// after each code the last completed word, (t >> 5) - 1, is (re)written, so
+// no per-code branch: a word is rewritten with the same bits until the next
+// one completes. Before the lane completes its first word the write goes to
+// that first word (clamp; overwritten once it completes -- every lane of a
+// slot-path block holds >= 32 bits, so it does). On return the low t % 32
+// bits of acc are the lane's trailing partial word.
+template <int MODE>
+HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& acc, uint32_t t, uint32_t* slot) {
+    constexpr int SH = PackEnt<MODE>::kShift;
+    const uint32_t lo = (t >> 5) + 1;
+    uint32_t* base = slot - 1;
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        const uint32_t L = (uint32_t)(e[k] >> SH);
+        const uint32_t c = (uint32_t)e[k] & ((1u << SH) - 1u);
+        acc = (acc << L) | c;
+        t += L;
+        const uint32_t w = __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, t);
+        const uint32_t idx = (t >> 5) > lo ? (t >> 5) : lo;
+        base[idx] = w;
+    }
+}
+
 constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
 
 template <int MODE>
@@ -517,9 +541,13 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
             // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
             // own: emit with the leading bits zero, then OR in the previous
             // lane's tail once all lanes are done.
-            uint32_t na = (uint32_t)(o & 31);
             uint64_t acc = 0;
-            pack_emit<MODE, true>(e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
+            if (MODE == ENC_WIDE) {  // codes may exceed 32 bits
+                uint32_t na = (uint32_t)(o & 31);
+                pack_emit<MODE, true>(e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
+            } else {
+                pack_emit_lds<MODE>(e, acc, (uint32_t)(o - (wfirst << 5)), slot);
+            }
             uint32_t prev = shfl_up_u32((uint32_t)acc, 1);
             if (lane == 0) prev = ptail;
             const uint32_t h = (uint32_t)(o & 31);
