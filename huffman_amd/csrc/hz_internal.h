@@ -64,7 +64,7 @@ constexpr int kDecMinWaves2 = 8; // k_decode: two blocks per wave only with this
 // past the last bit.
 __host__ __device__ inline uint32_t dec_slot_words(uint64_t max_bits, int max_len) {
     const uint64_t bits = max_bits + (uint64_t)kChainSyms * (uint32_t)max_len;
-    const uint64_t w = (bits + 31) / 32 + 4 + 3;
+    const uint64_t w = (bits + 31) / 32 + 4 + 3 + 4;  // + 16-byte pad before the block
     return (uint32_t)((w + 3) & ~3ull);
 }
 // Worst case: every symbol of a block at max_len bits.

@@ -9,6 +9,8 @@
 // Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "hz_internal.h"
 
 namespace hz {
@@ -931,26 +933,46 @@ HZ_DEV uint64_t stage_window(const uint32_t* stg, uint32_t pos) {
     return (two << sh) | ((((uint64_t)stg[wi + 2]) << sh) >> 32);
 }
 
+// 16 staged payload bytes at word w (zeros past the payload; w may have wrapped below 0).
+HZ_DEV uint4 dec_stage_load(const DecArgs& a, uint64_t w) {
+    uint4 v;
+    if (w < a.nwords && w + 4 <= a.nwords) {
+        v = *reinterpret_cast<const uint4*>(a.words + w);
+    } else {
+        v.x = w < a.nwords ? a.words[w] : 0u;
+        v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
+        v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
+        v.w = 0u;
+    }
+    return v;
+}
+
 // Stage payload words [w0, w0 + 4 npc) of block b into `stg`, byte-swapped.
+// The first kStageUnroll 16-byte loads of every lane are issued before any
+// is used (one memory round trip for blocks up to 4 KiB of payload).
+constexpr int kStageUnroll = 4;
 template <bool WIDE>
 HZ_DEV void dec_stage(const DecArgs& a, uint64_t b0, uint64_t b1, uint32_t npc_max, uint32_t* stg, int lane,
                       uint64_t& w0) {
-    w0 = (b0 >> 5) & ~3ull;
+    w0 = ((b0 >> 5) & ~3ull) - 4;  // one 16-byte pad before the block: every position is >= 128 (may wrap: zeros)
     const uint64_t wend = (b1 >> 5) + (WIDE ? 3 : 2);
     uint32_t npc = (uint32_t)((wend - w0 + 3) >> 2);
     npc = npc < npc_max ? npc : npc_max;
-    for (uint32_t p = lane; p < npc; p += kWave) {
-        const uint64_t w = w0 + 4ull * p;
-        uint4 v;
-        if (w + 4 <= a.nwords) {
-            v = *reinterpret_cast<const uint4*>(a.words + w);
-        } else {
-            v.x = w < a.nwords ? a.words[w] : 0u;
-            v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
-            v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
-            v.w = 0u;
-        }
-        reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+    uint4 v[kStageUnroll];
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; ++u) {
+        const uint32_t p = (uint32_t)lane + (uint32_t)u * kWave;
+        if (p < npc) v[u] = dec_stage_load(a, w0 + 4ull * p);
+    }
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; ++u) {
+        const uint32_t p = (uint32_t)lane + (uint32_t)u * kWave;
+        if (p < npc)
+            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(v[u].x), bswap32(v[u].y), bswap32(v[u].z), bswap32(v[u].w));
+    }
+    for (uint32_t p = (uint32_t)lane + kStageUnroll * kWave; p < npc; p += kWave) {
+        const uint4 x = dec_stage_load(a, w0 + 4ull * p);
+        reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
     }
 }
 
@@ -1019,24 +1041,41 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
     }
     __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
     uint32_t pk[NB][kSPT / 2];
+    // Windows: 32 bits (bit 31 = the chain's next bit) for codes <= 32 bits,
+    // one funnel shift of two staged words; 64 bits for WIDE.
+    using Win = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+    constexpr uint32_t WB = WIDE ? 64 : 32;
 #pragma unroll
     for (int q = 0; q < kChainSyms; ++q) {
-        uint64_t win[C];
+        Win win[C];
         uint32_t sym[C], L[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) win[c] = stage_window<WIDE>(stg0, pos[c]);
+        for (int c = 0; c < C; ++c) {
+            if constexpr (WIDE) {
+                win[c] = stage_window<true>(stg0, pos[c]);
+            } else {
+                const uint32_t p1 = pos[c] - 1u;  // >= 127 (staging pad)
+                const uint32_t* w = stg0 + (p1 >> 5);
+                win[c] = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
+            }
+        }
         if (MODE == DEC_DENSE) {
 #pragma unroll
-            for (int c = 0; c < C; ++c) dec_lookup<DEC_DENSE>(a, lds, win[c], sym[c], L[c]);
+            for (int c = 0; c < C; ++c) {
+                const uint32_t idx = (uint32_t)(win[c] >> (WB - (uint32_t)a.k));
+                sym[c] = reinterpret_cast<const uint16_t*>(lds)[idx];
+                const uint32_t lw = lds[(1u << a.k) / 2 + (idx >> 4)];
+                L[c] = (uint32_t)a.min_len + ((lw >> ((idx & 15) * 2)) & 3u);
+            }
         } else {
             uint32_t e[C], e2[C], D[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) { e[c] = lds[(uint32_t)(win[c] >> (64 - a.k))]; D[c] = (uint32_t)a.k; }
+            for (int c = 0; c < C; ++c) { e[c] = lds[(uint32_t)(win[c] >> (WB - (uint32_t)a.k))]; D[c] = (uint32_t)a.k; }
 #pragma unroll
             for (int c = 0; c < C; ++c) {  // LDS-resident second level (hot subtables)
                 if ((e[c] >> 30) == 1u) {
                     const uint32_t nb = (e[c] >> 26) & 15u;
-                    e[c] = lds[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << D[c]) >> (64 - nb))];
+                    e[c] = lds[(e[c] & 0x3ffffffu) + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
                     D[c] += nb;
                 }
             }
@@ -1045,7 +1084,7 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
                 e2[c] = e[c];
                 if (!(e[c] >> 31)) {
                     const uint32_t nb = (e[c] >> 26) & 15u;
-                    e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((win[c] << D[c]) >> (64 - nb))];
+                    e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
                 }
             }
 #pragma unroll
@@ -1055,7 +1094,7 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
                     uint32_t Dd = D[c] + ((e[c] >> 26) & 15u);
                     while (!(ee >> 31)) {  // deeper global levels: rare
                         const uint32_t nb = (ee >> 26) & 15u;
-                        ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((win[c] << Dd) >> (64 - nb))];
+                        ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((Win)(win[c] << Dd) >> (WB - nb))];
                         Dd += nb;
                     }
                 }
