@@ -235,7 +235,7 @@ namespace hz {
 int select_enc_mode(const hz_codebook* cb) {
     if (cb->min_len == 16 && cb->max_len == 16) return ENC_FIXED16;  // U = 65 536, a complete 16-bit code
     if (cb->max_len <= 16) return ENC_DENSE;
-    if (cb->max_len <= kNarrowMaxLen) return ENC_HOT;
+    if (cb->max_len <= kHotMaxLen) return ENC_HOT;  // every code fits a slot: a miss is a taken slot
     return ENC_WIDE;
 }
 

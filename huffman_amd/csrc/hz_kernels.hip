@@ -282,16 +282,17 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
 // plus the entry of one more symbol `xs` (the previous block's tail). HOT
-// slots hold tag << 31 | len << 26 | code: the entry is a hit when the tag
-// matches bit 15 of the symbol and len != 0; misses (slot taken by the
-// partner symbol, or codes > 25 bits) come from the escape table, all issued
-// before one wait.
-template <int MODE>
+// slots hold tag << 31 | len << 26 | code, and every occurring symbol's code
+// fits a slot (HOT mode needs max_len <= 25): an entry is a hit when its tag
+// (bit 31) equals bit 15 of the symbol, i.e. when bit 31 of entry ^ tag is 0.
+// Misses (the slot holds the partner symbol) come from the escape table, all
+// issued before one wait. FULL: all 32 symbols valid (no per-symbol masking).
+template <int MODE, bool FULL>
 HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid, uint32_t (&raw)[kSPT / 2],
                         typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
-    if (nvalid < kSPT) {
+    if (!FULL) {
 #pragma unroll
         for (int k = 0; k < kSPT / 2; ++k) {
             uint32_t w = 0;
@@ -310,39 +311,38 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             const uint64_t two = ((uint64_t)lds[w + 1] << 32) | lds[w];
             const uint32_t f = (uint32_t)(two >> (bit & 31)) & 0x1ffffu;
             const uint32_t L = f ? 16u - (uint32_t)__builtin_ctz(f) : 0u;
-            e[k] = (k < nvalid && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
+            e[k] = ((FULL || k < nvalid) && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
         }
         xe = pack_dense_one<T, SH>(lds, xs);
     } else if (MODE == ENC_HOT) {
         const uint32_t m = a.hot_mask;
-        uint32_t miss = 0;
+        uint32_t any = 0;
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
             const uint32_t slot = s ^ (m & (uint32_t)((int32_t)(s << 16) >> 31));
-            const uint32_t x = lds[hot_word(slot)] ^ ((s << 16) & 0x80000000u);
-            const bool hit = x - 0x04000000u < 0x7c000000u;  // tag matches and len != 0
-            e[k] = k < nvalid ? (T)x : (T)0;
-            if (!hit && k < nvalid) miss |= 1u << k;
+            uint32_t x = lds[hot_word(slot)] ^ ((s << 16) & 0x80000000u);
+            if (!FULL) x = k < nvalid ? x : 0u;
+            e[k] = (T)x;
+            any |= x;
         }
         const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
         const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
-        const bool xmiss = !(xx - 0x04000000u < 0x7c000000u);
         xe = (T)xx;
-        if (miss | (uint32_t)xmiss) {
+        if ((any | xx) >> 31) {
             // The escape table holds entries in the register format, so each
             // load lands in its e[k] directly and the single wait falls at the
             // first use.
 #pragma unroll
             for (int k = 0; k < kSPT; ++k)
-                if ((miss >> k) & 1u) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
-            if (xmiss) xe = (T)a.esc[xs];
+                if ((uint32_t)e[k] >> 31) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
+            if (xx >> 31) xe = (T)a.esc[xs];
         }
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            e[k] = k < nvalid ? (T)a.wide[s] : (T)0;
+            e[k] = (FULL || k < nvalid) ? (T)a.wide[s] : (T)0;
         }
         xe = (T)a.wide[xs];
     }
@@ -498,7 +498,8 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
         const uint64_t bstart = cur.bstart;
         T e[kSPT];
         T pe;
-        pack_lookup<MODE>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
+        if (nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
+        else pack_lookup<MODE, false>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
         // next block's loads: after this block's escapes, so no wait covers them early
         pack_prefetch(a, blk + W < a.nblocks ? blk + W : blk, lane, nx);
         // lane bits, decode-chain offsets, wave scan of the bit counts
