@@ -86,7 +86,7 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 // exactly through the value the LDS atomic returns (DESIGN.md "Histogram").
 // ===========================================================================
 constexpr int kHistThreads = 1024;
-constexpr int kHistUnroll = 4;
+constexpr int kHistUnroll = 1;
 
 // LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
 // their low bits (the first byte), which alone would pick the LDS bank: the
@@ -130,13 +130,23 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
         per = (per + step - 1) / step * step;
         const uint64_t beg = blockIdx.x * per;
         const uint64_t end = beg + per < nvec ? beg + per : nvec;
-        for (uint64_t i = beg + threadIdx.x; i < end; i += step) {
-            uint4 v[kHistUnroll];
+        // software pipelined: the next iteration's loads are in flight while
+        // this one's LDS atomics run (loads and LDS ops use separate counters)
+        uint4 nx[kHistUnroll];
+        auto load = [&](uint64_t i0, uint4 (&v)[kHistUnroll]) {
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u) {
-                const uint64_t j = i + (uint64_t)u * blockDim.x;
+                const uint64_t j = i0 + (uint64_t)u * blockDim.x;
                 v[u] = j < end ? in4[j] : make_uint4(0, 0, 0, 0);
             }
+        };
+        uint64_t i = beg + threadIdx.x;
+        if (i < end) load(i, nx);
+        for (; i < end; i += step) {
+            uint4 v[kHistUnroll];
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u) v[u] = nx[u];
+            if (i + step < end) load(i + step, nx);
             uint32_t old[kHistUnroll * 8];
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u) {
