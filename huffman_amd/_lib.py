@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libhuffman_amd.so")
+# HZ_LIB_VARIANT=<dir> loads <pkg>/<dir>/libhuffman_amd.so (kernel A/B builds, tools/); never a fallback
+LIB_PATH = os.path.join(_PKG, os.environ.get("HZ_LIB_VARIANT", "lib"), "libhuffman_amd.so")
 BIN_DIR = os.path.join(_PKG, "bin")
 
 HZ_NSYM = 65536

@@ -56,7 +56,6 @@ constexpr int kDecLevelBits = 8;
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
-constexpr int kDecMinWaves2 = 8; // k_decode: two blocks per wave only with this many waves
 
 // Per-wave LDS slot for one block's payload (u32 words), from the largest
 // block of the stream: its bits, chains past the end of a tail block (16 codes

@@ -900,7 +900,6 @@ struct DecArgs {
     const uint32_t* l2;
     uint8_t* out;
     uint32_t* err;
-    int group2;              // k_decode: allow two blocks per wave
 };
 
 template <int MODE>
@@ -1128,7 +1127,164 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
         if (bfirst + g < a.nblocks) dec_store(a, bfirst + g, lane, pk[g]);
 }
 
-template <int MODE, bool WIDE>
+// Two-level LUT decode of one block with the global lookups software
+// pipelined. Needs max_len <= k + kDecLevelBits (every global lookup ends in
+// a leaf) and max_len <= 32. The lane's chains are two halves, {0,1} and
+// {2,3}; a half's LDS step (window, level 1, LDS second level) issues its
+// global lookups unconditionally (lanes that do not need one read l2[0]:
+// same-address lanes coalesce), and those are consumed only after the other
+// half's LDS step has issued its own, so every wait is vmcnt(2) in
+// straight-line code and one half's table walk hides the other's gather.
+struct PipeLane {
+    uint32_t e, gi;
+};
+
+HZ_DEV PipeLane dec_pipe_lds(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, uint32_t pos) {
+    const uint32_t p1 = pos - 1u;  // >= 127 (staging pad)
+    const uint32_t* w = stg + (p1 >> 5);
+    const uint32_t W = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
+    uint32_t e = lds[W >> (32 - a.k)];
+    uint32_t D = (uint32_t)a.k;
+    if ((e >> 30) == 1u) {  // LDS second level
+        const uint32_t nb = (e >> 26) & 15u;
+        e = lds[(e & 0x3ffffffu) + ((W << D) >> (32 - nb))];
+        D += nb;
+    }
+    const bool lk = !(e >> 31);
+    const uint32_t nb = (e >> 26) & 15u;
+    PipeLane r;
+    r.e = e;
+    r.gi = lk ? (e & 0x3ffffffu) + ((W << D) >> (32 - nb)) : 0u;
+    return r;
+}
+
+// Block metadata of the pipelined decoder: start and end bit, the lane's chain offsets.
+struct PipeMeta {
+    uint64_t b0, b1, sub;
+};
+
+HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
+    const uint64_t bb = b < a.nblocks ? b : a.nblocks - 1;  // past the end: any block, never used
+    m.b0 = a.starts[bb];
+    m.b1 = a.starts[bb + 1];
+    m.sub = a.subs[bb * kWave + lane];
+}
+
+// The first kStageUnroll 16-byte chunks of a block's staging window, always
+// exactly kStageUnroll loads per lane (static vmcnt for the pipelined waits):
+// chunks past the window or the payload read a clamped address and are fixed
+// up in registers. Requires nwords >= 4 (host check).
+HZ_DEV void dec_stage_prefetch(const DecArgs& a, const PipeMeta& m, int lane, uint4 (&v)[kStageUnroll]) {
+    const uint64_t w0 = (((m.b0 + a.bit_adj) >> 5) & ~3ull) - 4;
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; ++u) {
+        const uint64_t w = w0 + 4ull * ((uint32_t)lane + (uint32_t)u * kWave);
+        const bool in = w < a.nwords;  // also false for a window that wrapped below word 0
+        const uint64_t wl = !in ? 0 : (w + 4 <= a.nwords ? w : a.nwords - 4);
+        v[u] = *reinterpret_cast<const uint4*>(a.words + wl);
+    }
+}
+
+HZ_DEV uint32_t pick4(const uint4& v, uint32_t i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// Writes the prefetched chunks (fixed up for the payload's end) and any
+// further chunks of an oversized window into the slot.
+HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_max, uint32_t* stg, int lane,
+                             const uint4 (&v)[kStageUnroll], uint64_t& w0) {
+    const uint64_t b0 = m.b0 + a.bit_adj, b1 = m.b1 + a.bit_adj;
+    w0 = ((b0 >> 5) & ~3ull) - 4;
+    const uint64_t wend = (b1 >> 5) + 2;
+    uint32_t npc = (uint32_t)((wend - w0 + 3) >> 2);
+    npc = npc < npc_max ? npc : npc_max;
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; ++u) {
+        const uint32_t p = (uint32_t)lane + (uint32_t)u * kWave;
+        if (p < npc) {
+            const uint64_t w = w0 + 4ull * p;
+            uint4 x = v[u];
+            if (!(w < a.nwords && w + 4 <= a.nwords)) {  // tail of the payload (or wrapped): shift, zero-fill
+                const uint64_t base = a.nwords - 4;
+                uint32_t q[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint64_t wt = w + t;
+                    q[t] = wt < a.nwords && w < a.nwords ? pick4(x, (uint32_t)(wt - base)) : 0u;
+                }
+                x = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+        }
+    }
+    for (uint32_t p = (uint32_t)lane + kStageUnroll * kWave; p < npc; p += kWave) {  // oversized block: rare
+        const uint4 x = dec_stage_load(a, w0 + 4ull * p);
+        reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+    }
+}
+
+// Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
+// staging chunks of the next block and the metadata of the one after are
+// loaded halfway through this block's steps, so no block waits on HBM.
+HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, uint32_t slot, uint64_t b,
+                          uint64_t stride, int lane) {
+    constexpr int C = kChainsPerLane;
+    static_assert(C == 4, "two halves of two chains");
+    PipeMeta mc, mn, mn2;
+    uint4 sc[kStageUnroll], sn[kStageUnroll];
+    dec_meta_load(a, b, lane, mc);
+    dec_meta_load(a, b + stride, lane, mn);
+    dec_stage_prefetch(a, mc, lane, sc);
+    for (; b < a.nblocks; b += stride) {
+        uint64_t w0;
+        dec_stage_commit(a, mc, slot >> 2, stg, lane, sc, w0);
+        uint32_t off[C];
+        dec_chain_offsets(mc.sub, mc.b1 - mc.b0, lane, off);
+        const uint32_t base = (uint32_t)(mc.b0 + a.bit_adj - (w0 << 5));
+        uint32_t pos[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) pos[c] = base + off[c];
+        __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+        uint32_t pk[kSPT / 2];
+        PipeLane st[C];
+        uint32_t g[C];
+        auto finish = [&](int c, int q) {
+            const uint32_t ee = (st[c].e >> 31) ? st[c].e : g[c];
+            pos[c] += (ee >> 16) & 63u;
+            const uint32_t sym = ee & 0xffffu;
+            const int i = (c * kChainSyms + q) >> 1;
+            if (q & 1) pk[i] |= sym << 16;
+            else pk[i] = sym;
+        };
+#pragma unroll
+        for (int c = 0; c < 2; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+#pragma unroll
+            for (int c = 2; c < 4; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
+            if (q == kChainSyms / 2) {  // next block's staging chunks, the metadata after it
+                dec_stage_prefetch(a, mn, lane, sn);
+                dec_meta_load(a, b + 2 * stride, lane, mn2);
+            }
+            finish(0, q);
+            finish(1, q);
+            if (q + 1 < kChainSyms) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
+            }
+            finish(2, q);
+            finish(3, q);
+        }
+        __builtin_amdgcn_wave_barrier();
+        dec_store(a, b, lane, pk);
+        mc = mn;
+        mn = mn2;
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) sc[u] = sn[u];
+    }
+}
+
+template <int MODE, bool WIDE, bool PIPE>
 __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
@@ -1137,19 +1293,15 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     // slots fit the stream's largest block; waves without a slot have nothing to do
     const uint32_t slot = dec_slot_words(a.starts[a.nblocks + 1], a.max_len);
     const uint32_t nwave = blockDim.x >> 6;
-    // two blocks per wave when that keeps at least kDecMinWaves2 waves busy
-    const bool two = a.group2 && a.region_words / (2 * slot) >= (uint32_t)kDecMinWaves2;
-    const uint32_t per = two ? 2 * slot : slot;
-    uint32_t nw = a.region_words / per;
+    uint32_t nw = a.region_words / slot;
     nw = nw < nwave ? nw : nwave;
     if (wid >= nw) return;
-    uint32_t* stg = lds + a.lds_words + wid * per;
-    if (two) {
-        for (uint64_t g = (uint64_t)blockIdx.x * nw + wid; 2 * g < a.nblocks; g += (uint64_t)gridDim.x * nw)
-            dec_group<MODE, WIDE, 2>(a, lds, stg, slot, 2 * g, lane);
+    uint32_t* stg = lds + a.lds_words + wid * slot;
+    const uint64_t b = (uint64_t)blockIdx.x * nw + wid, stride = (uint64_t)gridDim.x * nw;
+    if constexpr (PIPE) {
+        dec_wave_pipe(a, lds, stg, slot, b, stride, lane);
     } else {
-        for (uint64_t b = (uint64_t)blockIdx.x * nw + wid; b < a.nblocks; b += (uint64_t)gridDim.x * nw)
-            dec_group<MODE, WIDE, 1>(a, lds, stg, slot, b, lane);
+        for (uint64_t bb = b; bb < a.nblocks; bb += stride) dec_group<MODE, WIDE, 1>(a, lds, stg, slot, bb, lane);
     }
 }
 
@@ -1222,7 +1374,6 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
     a.min_len = t.dec_min_len;
     a.max_len = t.dec_max_len;
     a.l2 = t.d_dec_l2;
-    a.group2 = 0;
 }
 
 // Launch shape: slots are sized for the average block (estimated from the
@@ -1230,49 +1381,38 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
 // index's max_bits and idles the waves that do not get one. Up to two
 // workgroups per CU (each holds its own table copy): whichever shape runs
 // more waves.
-template <int MODE, bool WIDE>
+template <int MODE, bool WIDE, bool PIPE>
 static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, PIPE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    static const int group_env = [] { const char* v = getenv("HZ_DEC_GROUP"); return v ? atoi(v) : 1; }();
     const uint64_t avg = (payload_bits + a.nblocks - 1) / a.nblocks;
     const uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
     const uint32_t worst = dec_slot_words_max(a.max_len);
     const uint32_t table = a.lds_words;
-    DecArgs b = a;
-    b.group2 = 0;
     int best_w = 0, best_g = 1;
-    // two blocks per wave, one workgroup per CU, when enough waves get slots
-    if (group_env == 2 && kLdsBytes / 4 > table + 2 * est) {
-        int w = (int)((kLdsBytes / 4 - table) / (2 * est));
+    for (int g = 1; g <= 2; ++g) {
+        const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
+        if (room <= table + est) continue;
+        int w = (int)((room - table) / est);
         w = w > kDecMaxWaves ? kDecMaxWaves : w;
-        if (w >= kDecMinWaves2) { best_w = w; b.group2 = 1; }
-    }
-    if (!b.group2) {
-        for (int g = 1; g <= 2; ++g) {
-            const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
-            if (room <= table + est) continue;
-            int w = (int)((room - table) / est);
-            w = w > kDecMaxWaves ? kDecMaxWaves : w;
-            if (g * w > best_g * best_w) { best_w = w; best_g = g; }
-        }
+        if (g * w > best_g * best_w) { best_w = w; best_g = g; }
     }
     if (best_w == 0) return hipErrorInvalidValue;
-    b.region_words = (uint32_t)best_w * est * (b.group2 ? 2 : 1);
+    DecArgs b = a;
+    b.region_words = (uint32_t)best_w * est;
     if (b.region_words < worst && table + worst <= kLdsBytes / 4) b.region_words = worst;  // any stream decodes
     if (table + b.region_words > kLdsBytes / 4 / (uint32_t)best_g) best_g = 1;
     if (table + b.region_words > kLdsBytes / 4) return hipErrorInvalidValue;
     const uint32_t lds = 4 * (table + b.region_words);
-    const uint64_t units = b.group2 ? (a.nblocks + 1) / 2 : a.nblocks;
-    uint64_t wgs = (units + best_w - 1) / best_w;
+    uint64_t wgs = (a.nblocks + best_w - 1) / best_w;
     const uint64_t cap = (uint64_t)ncu * best_g;
     if (wgs > cap) wgs = cap;
-    hipLaunchKernelGGL((k_decode<MODE, WIDE>), dim3(wgs), dim3(64 * best_w), lds, s, b);
+    hipLaunchKernelGGL((k_decode<MODE, WIDE, PIPE>), dim3(wgs), dim3(64 * best_w), lds, s, b);
     return hipGetLastError();
 }
 
@@ -1301,8 +1441,13 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     }
     const uint64_t pbits = payload_bytes * 8;
     const bool wide = t.dec_max_len > 32;
-    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false>(a, pbits, ncu, s);
-    return wide ? run_decode<DEC_LUT, true>(a, pbits, ncu, s) : run_decode<DEC_LUT, false>(a, pbits, ncu, s);
+    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false, false>(a, pbits, ncu, s);
+    if (wide) return run_decode<DEC_LUT, true, false>(a, pbits, ncu, s);
+    // two levels suffice (no lookup chain past a global subtable): pipelined gathers
+    static const int pipe_env = [] { const char* v = getenv("HZ_DEC_PIPE"); return v ? atoi(v) : 1; }();
+    if (pipe_env && t.dec_max_len <= t.dec_k + kDecLevelBits && a.nwords >= 4)
+        return run_decode<DEC_LUT, false, true>(a, pbits, ncu, s);
+    return run_decode<DEC_LUT, false, false>(a, pbits, ncu, s);
 }
 
 // ===========================================================================
