@@ -1223,6 +1223,9 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
     }
 }
 
+#ifndef HZ_PF_STEP
+#define HZ_PF_STEP 4
+#endif
 // Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
 // staging chunks of the next block and the metadata of the one after are
 // loaded halfway through this block's steps, so no block waits on HBM.
@@ -1262,7 +1265,7 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
         for (int q = 0; q < kChainSyms; ++q) {
 #pragma unroll
             for (int c = 2; c < 4; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
-            if (q == kChainSyms / 2) {  // next block's staging chunks, the metadata after it
+            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
                 dec_stage_prefetch(a, mn, lane, sn);
                 dec_meta_load(a, b + 2 * stride, lane, mn2);
             }
