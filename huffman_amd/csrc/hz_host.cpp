@@ -533,27 +533,6 @@ std::string output_name() {
     return name;
 }
 
-int read_file(const char* path, std::vector<uint8_t>& buf) {
-    FILE* fp = fopen(path, "rb");
-    if (!fp) return HZ_EIO;
-    fseek(fp, 0, SEEK_END);
-    long sz = ftell(fp);
-    fseek(fp, 0, SEEK_SET);
-    if (sz < 0) { fclose(fp); return HZ_EIO; }
-    buf.resize((size_t)sz);
-    size_t got = sz ? fread(buf.data(), 1, (size_t)sz, fp) : 0;
-    fclose(fp);
-    return got == (size_t)sz ? HZ_OK : HZ_EIO;
-}
-
-int write_file(const std::string& path, const uint8_t* p, uint64_t n) {
-    FILE* fp = fopen(path.c_str(), "wb");
-    if (!fp) return HZ_EIO;
-    size_t put = n ? fwrite(p, 1, n, fp) : 0;
-    fclose(fp);
-    return put == n ? HZ_OK : HZ_EIO;
-}
-
 }  // namespace
 
 // ---- streaming archive: bounded host and device memory ----

@@ -312,7 +312,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             raw[k] = w;
         }
     }
-    if (MODE == ENC_DENSE) {
+    if constexpr (MODE == ENC_DENSE) {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
@@ -324,7 +324,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             e[k] = ((FULL || k < nvalid) && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
         }
         xe = pack_dense_one<T, SH>(lds, xs);
-    } else if (MODE == ENC_HOT) {
+    } else if constexpr (MODE == ENC_HOT) {
         const uint32_t m = a.hot_mask;
         uint32_t any = 0;
 #pragma unroll
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
             // own: emit with the leading bits zero, then OR in the previous
             // lane's tail once all lanes are done.
             uint64_t acc = 0;
-            if (MODE == ENC_WIDE) {  // codes may exceed 32 bits
+            if constexpr (MODE == ENC_WIDE) {  // codes may exceed 32 bits
                 uint32_t na = (uint32_t)(o & 31);
                 pack_emit<MODE, true>(e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
             } else {
@@ -1475,6 +1475,7 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
 //   k_sync_subs : chain positions relative to their block, max block bits
 // ===========================================================================
 constexpr uint32_t kSegBits = 4096;
+constexpr int kSyncThreads = 1024;
 constexpr uint32_t kSegWords = kSegBits / 32;
 
 struct BitReader {
@@ -1531,7 +1532,7 @@ struct SyncArgs {
 };
 
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sync_scan(DecArgs a, SyncArgs y) {
+__global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs y) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1559,7 +1560,7 @@ __global__ __launch_bounds__(256) void k_sync_scan(DecArgs a, SyncArgs y) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
+__global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const unsigned long long* exr = y.ex[it & 1];
@@ -1609,7 +1610,7 @@ __global__ __launch_bounds__(256) void k_sync_iter(DecArgs a, SyncArgs y, int it
 
 // Decode each segment from its true entry; symbol i (global) lands at pos.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* exits,
+__global__ __launch_bounds__(kSyncThreads) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* exits,
                                                   const unsigned long long* first, unsigned long long* starts,
                                                   uint16_t* subs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1681,17 +1682,18 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
         }
         attr = true;
     }
-    uint64_t wgs = (y.nseg + 255) / 256;
-    const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 4 ? kLdsBytes / lds : 4) : 4);
+    // 16-wave workgroups: one table copy per workgroup, as many waves as a CU holds
+    uint64_t wgs = (y.nseg + kSyncThreads - 1) / kSyncThreads;
+    const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 2 ? 1 : 2) : 2);
     wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
-    hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(256), lds, s, a, y);
+    hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
     // resolve entries until no exit changes (host loop; typically 1-3 passes)
     int it = 0;
     for (;; ++it) {
         hipError_t e = hipMemsetAsync(y.changed, 0, 4, s);
         if (e != hipSuccess) return e;
         if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nseg, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sync_iter<MODE>, dim3(wgs), dim3(256), lds, s, a, y, it);
+        hipLaunchKernelGGL(k_sync_iter<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, it);
         if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         if (*h_changed == 0 || it > (int)y.nseg) break;
@@ -1707,7 +1709,7 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     // end bit = all ones unless the payload holds nsym codewords (k_sync_emit writes it then)
     hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(256), lds, s, a, y, exits, (const unsigned long long*)first,
+    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits, (const unsigned long long*)first,
                        d_index, subs);
     e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
     if (e != hipSuccess) return e;
