@@ -1226,6 +1226,9 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
 #ifndef HZ_PF_STEP
 #define HZ_PF_STEP 4
 #endif
+#ifndef HZ_PIPE_QUARTER
+#define HZ_PIPE_QUARTER 0
+#endif
 // Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
 // staging chunks of the next block and the metadata of the one after are
 // loaded halfway through this block's steps, so no block waits on HBM.
@@ -1259,6 +1262,28 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
             if (q & 1) pk[i] |= sym << 16;
             else pk[i] = sym;
         };
+#if HZ_PIPE_QUARTER
+        // each chain's gathers are consumed after the other three chains' LDS steps
+        auto issue = [&](int c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; };
+        issue(0);
+        issue(1);
+        issue(2);
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+            issue(3);
+            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
+                dec_stage_prefetch(a, mn, lane, sn);
+                dec_meta_load(a, b + 2 * stride, lane, mn2);
+            }
+            finish(0, q);
+            if (q + 1 < kChainSyms) issue(0);
+            finish(1, q);
+            if (q + 1 < kChainSyms) issue(1);
+            finish(2, q);
+            if (q + 1 < kChainSyms) issue(2);
+            finish(3, q);
+        }
+#else
 #pragma unroll
         for (int c = 0; c < 2; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
 #pragma unroll
@@ -1278,6 +1303,7 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
             finish(2, q);
             finish(3, q);
         }
+#endif
         __builtin_amdgcn_wave_barrier();
         dec_store(a, b, lane, pk);
         mc = mn;
