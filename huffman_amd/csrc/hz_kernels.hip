@@ -389,9 +389,10 @@ __global__ __launch_bounds__(kCountThreads) void k_pack_count(PackArgs a) {
         uint4 v[kCountUnroll][kSPT / 8];
 #pragma unroll
         for (int u = 0; u < kCountUnroll; ++u) {
-            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ((blk + u * W) * kBlockSyms + (uint64_t)lane * kSPT));
+            // the sum is order-free: instruction q reads bytes [1024 q + 16 lane, +16) (fully coalesced)
+            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * (blk + u * W) * kBlockSyms) + lane;
 #pragma unroll
-            for (int q = 0; q < kSPT / 8; ++q) v[u][q] = p[q];
+            for (int q = 0; q < kSPT / 8; ++q) v[u][q] = p[q * kWave];
         }
 #pragma unroll
         for (int u = 0; u < kCountUnroll; ++u) {
