@@ -137,6 +137,7 @@ def main():
         codec.pack(x, plan, state["payload"], state["index"])
         codec.upload_decode(plan)  # host builds the decode tables while pack runs
         codec.decode(state["payload"], nsym, state["index"], out)
+        state["header"] = plan.header  # the .compressed header, written on the host while the GPU runs
         state["plan"] = plan
 
     for _ in range(args.warmup):

@@ -23,14 +23,15 @@
 namespace {
 
 // LSD radix sort of u64 keys with 16-bit digits over the bits in use.
-void radix_sort_u64(std::vector<uint64_t>& k) {
+// LSD radix sort, 16-bit digits from bit `lo` (digits below lo are already in order).
+void radix_sort_u64(std::vector<uint64_t>& k, int lo = 0) {
     if (k.size() < 2) return;
     uint64_t mx = 0;
     for (uint64_t v : k) mx |= v;
     int bits = 64 - __builtin_clzll(mx | 1);
     std::vector<uint64_t> tmp(k.size());
     std::vector<uint32_t> cnt(65536);
-    for (int sh = 0; sh < bits; sh += 16) {
+    for (int sh = lo; sh < bits; sh += 16) {
         std::fill(cnt.begin(), cnt.end(), 0u);
         for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
         uint32_t sum = 0;
@@ -96,7 +97,7 @@ extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
     const uint32_t U = (uint32_t)keys.size();
     cb->nsym = U;
     if (U == 0) return HZ_OK;
-    radix_sort_u64(keys);  // (count, symbol) ascending == thrust stable order
+    radix_sort_u64(keys, 16);  // keys were built in symbol order: a stable sort by count == (count, symbol) order (thrust's)
     for (uint32_t i = 0; i < U; ++i) cb->order[i] = (uint16_t)(keys[i] & 0xffff);
     if (U == 1) {  // reference defect B4: its code would be empty; use "0"
         cb->len[cb->order[0]] = 1;

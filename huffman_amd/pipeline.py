@@ -31,12 +31,26 @@ class Plan:
         # absolute payload bit where this shard starts (header pending bits first)
         self.stream_bit = self.header_bits % 8 + shard_bit_offset
         self.start_bit = self.stream_bit % 32 if not first_shard else self.stream_bit
-        self.lead = 0
-        self.header = b""
-        if first_shard:
-            self.header, pbits, pend = write_header(cb, n_total, last_byte)
-            self.lead = (pend >> (8 - pbits)) if pbits else 0
+        self.first_shard = first_shard
+        self.last_byte = last_byte
+        self._header = None
+        # The header's last header_bits % 8 bits open the payload's first byte.
+        # They are the low bits of N's top byte, the last of the 8 N bytes the
+        # header ends with (Compressor.cu:487,661-669), so pack needs no header.
+        pbits = self.header_bits % 8
+        self.lead = ((n_total >> 56) & ((1 << pbits) - 1)) if first_shard else 0
         self.words = (self.start_bit + self.payload_bits + 31) // 32
+
+    @property
+    def header(self):
+        """Complete header bytes (first shard only); written on first use, so a
+        caller can launch pack/decode before paying for it on the host."""
+        if self._header is None:
+            self._header = b""
+            if self.first_shard:
+                self._header, pbits, pend = write_header(self.cb, self.n_total, self.last_byte)
+                assert ((pend >> (8 - pbits)) if pbits else 0) == self.lead
+        return self._header
 
 
 class StreamCodec:
