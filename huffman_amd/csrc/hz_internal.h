@@ -34,7 +34,7 @@ __host__ __device__ inline uint64_t index_sub_offset(uint64_t nblocks) { return 
 // Encode table modes (selected on the host per codebook, DESIGN.md "Pack").
 enum EncMode : int {
     ENC_DENSE = 0,  // max_len <= 16: 65536 x 17-bit sentinel entries, 139 264 B LDS
-    ENC_HOT = 1,    // max_len <= 26: 32768 u32 slots (tag,len,code) + u64 escapes
+    ENC_HOT = 1,    // max_len <= 25: 32768 u32 slots (tag,len,code) + u32 escapes
     ENC_WIDE = 2,   // anything up to 56 bits: u64 table in global memory
     ENC_FIXED16 = 3 // every code 16 bits (U = 65536, min_len = max_len): u16 codes in LDS, no scan
 };

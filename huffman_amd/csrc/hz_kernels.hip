@@ -483,7 +483,10 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
     }
 }
 
-constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
+#ifndef HZ_PACK_THREADS
+#define HZ_PACK_THREADS 512
+#endif
+constexpr int kPackWriteThreads = HZ_PACK_THREADS;  // <= 8 waves: room for a block of registers in flight per lane
 
 template <int MODE>
 __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
