@@ -156,7 +156,7 @@ extern "C" int hz_ctx_sync(hz_ctx* c) {
         const uint32_t e = *c->h_err;
         *c->h_err = 0;
         HZ_TRY(hipMemset(c->d_err, 0, 16));
-        return (e & 4u) ? HZ_ECAP : HZ_EFORMAT;
+        return (e & 4u) ? HZ_ECAP : (e & 8u) ? HZ_ETIMEOUT : HZ_EFORMAT;
     }
     return HZ_OK;
 }

@@ -251,6 +251,8 @@ struct PackArgs {
     unsigned long long* index_sub;  // block index sub[] (four u16 chain offsets per lane)
     uint32_t* err;
     uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
+    uint64_t start_bit;          // k_pack_onepass: the stream's first bit (the end of chunk -1)
+    unsigned long long* ticket;  // k_pack_onepass: chunk ticket counter (zeroed per launch)
 };
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
@@ -276,6 +278,7 @@ struct PackIn {
     uint64_t bstart;
 };
 
+template <bool WITH_START = true>
 HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     const uint64_t ls = sym0 + kSPT <= a.nsym ? sym0 : 0;
@@ -287,7 +290,7 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
     x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
-    x.bstart = a.blk_start[blk];
+    x.bstart = WITH_START ? a.blk_start[blk] : 0ull;
 }
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
@@ -488,11 +491,146 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
 #endif
 constexpr int kPackWriteThreads = HZ_PACK_THREADS;  // <= 8 waves: room for a block of registers in flight per lane
 
+// One block of a wave between its lookup and its emit: the lane's 32 entries,
+// the entry of one of the previous block's last 32 symbols, the lane's bits,
+// its offset in the block, its decode-chain offsets, and the block's bits
+// (wave uniform).
 template <int MODE>
-__global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
+struct PackBlk {
+    typename PackEnt<MODE>::T e[kSPT];
+    typename PackEnt<MODE>::T pe;
+    uint32_t n, ex_n, bits;
+    uint32_t nc[kChainsPerLane];
+    int nvalid;
+};
+
+template <int MODE>
+HZ_DEV void pack_block_lookup(const PackArgs& a, const uint32_t* lds, uint64_t blk, int lane, PackIn& in,
+                              PackBlk<MODE>& b) {
+    const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+    b.nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
+    if (b.nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe);
+    else pack_lookup<MODE, false>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe);
+}
+
+// Lane bits, decode-chain offsets, wave scan of the bit counts.
+template <int MODE>
+HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
+    constexpr int SH = PackEnt<MODE>::kShift;
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        if (k % kChainSyms == 0) b.nc[k / kChainSyms] = n;
+        n += (uint32_t)(b.e[k] >> SH);
+    }
+    uint32_t sn = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = shfl_up_u32(sn, d);
+        if (lane >= d) sn += o;
+    }
+    b.n = n;
+    b.ex_n = sn - n;
+    b.bits = shfl_u32(sn, 63);
+}
+
+// Writes block `blk` starting at absolute bit `bstart`, plus its index entries.
+template <int MODE>
+HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int lane, const PackBlk<MODE>& b,
+                            uint64_t bstart, uint64_t& max_bits) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
+    const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+    const uint32_t n = b.n, ex_n = b.ex_n;
+    const uint64_t bend = bstart + b.bits;
+    // The 32 bits before the block: codes of the previous block's last 32
+    // symbols (each code >= 1 bit), combined across lanes 0..31.
+    uint32_t ptail = a.lead;
+    if (blk > 0) {
+        uint32_t pn = (uint32_t)(b.pe >> SH);
+        uint32_t pt = (uint32_t)(b.pe & CMASK);  // low 32 bits of the code
+#pragma unroll
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t on = shfl_up_u32(pn, d), ot = shfl_up_u32(pt, d);
+            if ((lane & 31) >= d) {
+                pt = pn >= 32 ? pt : ((ot << pn) | pt);
+                pn += on;
+            }
+        }
+        ptail = shfl_u32(pt, 31);
+    }
+    const uint64_t o = bstart + ex_n;
+    // every word this block writes lies below ceil(bend / 32)
+    const bool fits = ((bend + 31) >> 5) <= a.out_words;
+    if (!fits && lane == 0) atomicOr(a.err, 4u);
+    const bool last = blk + 1 == a.nblocks;
+    const uint64_t wfirst = bstart >> 5;
+    const uint32_t nwords = (uint32_t)((bend >> 5) - wfirst);  // words completed inside the block
+    if (slot && !last && nwords <= a.slot_words) {
+        // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
+        // own: emit with the leading bits zero, then OR in the previous
+        // lane's tail once all lanes are done.
+        uint64_t acc = 0;
+        if constexpr (MODE == ENC_WIDE) {  // codes may exceed 32 bits
+            uint32_t na = (uint32_t)(o & 31);
+            pack_emit<MODE, true>(b.e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
+        } else {
+            pack_emit_lds<MODE>(b.e, acc, (uint32_t)(o - (wfirst << 5)), slot);
+        }
+        uint32_t prev = shfl_up_u32((uint32_t)acc, 1);
+        if (lane == 0) prev = ptail;
+        const uint32_t h = (uint32_t)(o & 31);
+        if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
+        __builtin_amdgcn_wave_barrier();
+        if (fits)
+            for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        // direct path: each lane needs the 32 bits before its run from the
+        // (bits, tail) scan, since a lane of the last block may hold < 32 bits
+        uint64_t t64 = 0;
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const uint32_t L = (uint32_t)(b.e[k] >> SH);
+            t64 = L ? ((t64 << L) | (uint64_t)(b.e[k] & CMASK)) : t64;
+        }
+        uint32_t tn = n, st = (uint32_t)t64;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t on = shfl_up_u32(tn, d), ot = shfl_up_u32(st, d);
+            if (lane >= d) {
+                st = tn >= 32 ? st : (tn == 0 ? ot : ((ot << tn) | st));
+                tn += on;
+            }
+        }
+        uint32_t ex_t = shfl_up_u32(st, 1);
+        if (lane == 0) ex_t = 0;
+        const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
+        uint32_t na = (uint32_t)(o & 31);
+        uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
+        uint32_t* dst = a.out + (o >> 5);
+        pack_emit<MODE, false>(b.e, acc, na, dst, fits);
+        dst += (uint32_t)(((o & 31) + n) >> 5);
+        if (fits && b.nvalid > 0 && sym0 + (uint64_t)b.nvalid == a.nsym && na > 0)
+            *dst = bswap32((uint32_t)(acc << (32 - na)));
+    }
+    if (a.index) {  // block index (hz_internal.h): start bits + the lane's chain offsets
+        uint64_t sub = 0;
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) sub |= (uint64_t)((ex_n + b.nc[c]) & 0xffffu) << (16 * c);
+        a.index_sub[blk * kWave + lane] = sub;
+        if (lane == 0) {
+            a.index[blk] = bstart;
+            if (last) a.index[a.nblocks] = bend;
+        }
+        max_bits = bend - bstart > max_bits ? bend - bstart : max_bits;
+    }
+}
+
+// Three-pass pack (after k_pack_count + k_scan_*): block starts are known.
+template <int MODE>
+__global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
@@ -506,112 +644,180 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     PackIn nx;  // the next block's inputs, in flight while this block is packed
     if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
     for (; blk < a.nblocks; blk += W) {
-        const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
-        const int nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
         PackIn cur = nx;
-        const uint64_t bstart = cur.bstart;
-        T e[kSPT];
-        T pe;
-        if (nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
-        else pack_lookup<MODE, false>(a, lds, sym0, nvalid, cur.raw, e, cur.psym, pe);
+        PackBlk<MODE> b;
+        pack_block_lookup<MODE>(a, lds, blk, lane, cur, b);
         // next block's loads: after this block's escapes, so no wait covers them early
         pack_prefetch(a, blk + W < a.nblocks ? blk + W : blk, lane, nx);
-        // lane bits, decode-chain offsets, wave scan of the bit counts
-        uint32_t n = 0, nc[kChainsPerLane];
+        pack_block_count<MODE>(lane, b);
+        pack_block_emit<MODE>(a, slot, blk, lane, b, cur.bstart, max_bits);
+    }
+    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
+}
+
+// ---- one pass: decoupled look-back replaces k_pack_count + k_scan_* ---------
+// A workgroup of nw waves packs chunks of nw consecutive blocks (one per
+// wave) and takes chunks in ticket order, so every chunk's predecessors belong
+// to running workgroups (hard part (e)). Chunk c publishes one
+// status word {flag:2 | bits:62}: AGG (its own bits) once its blocks are
+// looked up, PRE (its end bit) once its start is known. Its start comes from
+// the status words of the 256 chunks before it, read by one wave in one
+// round trip (4 per lane) and summed back to the nearest PRE; chunk -1 is PRE
+// at the stream's start bit. Status words are written and read only with
+// agent-scope atomics, the value being its own flag (cdna_hip_programming.md
+// Guideline 16, R2), and are zeroed before every launch.
+// Schedule per step: the look-back loads of chunk c are issued, chunk c + 1 is
+// looked up (its AGG published), then chunk c's look-back is resolved -- the
+// chunks before it published AGG a step earlier and those a round earlier
+// (one chunk per workgroup) PRE -- and chunk c is written. Tickets run two
+// chunks ahead so chunk c + 2's input is in flight meanwhile.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr unsigned long long kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
+constexpr int kLookbackPerLane = 4;
+constexpr uint32_t kLookbackSpins = 1u << 22;  // bounded: a wave that gives up flags HZ_ETIMEOUT (err bit 8)
+constexpr uint32_t kOnepassCtlWords = 48;      // LDS: tickets, block bits [2][8], block starts u64[8]
+
+HZ_DEV unsigned long long st_load(const unsigned long long* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+HZ_DEV void st_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+HZ_DEV uint32_t chunk_ticket(unsigned long long* ctr) {
+    return (uint32_t)__hip_atomic_fetch_add((gu64*)ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Status of chunks top - 1 - (4 lane + j).
+HZ_DEV void lookback_load(const PackArgs& a, int64_t top, int lane, unsigned long long (&v)[kLookbackPerLane]) {
 #pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            if (k % kChainSyms == 0) nc[k / kChainSyms] = n;
-            n += (uint32_t)(e[k] >> SH);
-        }
-        uint32_t sn = n;
+    for (int j = 0; j < kLookbackPerLane; ++j) {
+        const int64_t idx = top - 1 - (int64_t)(kLookbackPerLane * lane + j);
+        v[j] = idx >= 0 ? st_load(a.blk + idx) : (idx == -1 ? (kStPre | a.start_bit) : kStPre);
+    }
+}
+
+// Start bit of chunk c (wave uniform) from the window v = lookback_load(c).
+HZ_DEV uint64_t lookback_resolve(const PackArgs& a, uint64_t c, int lane, unsigned long long (&v)[kLookbackPerLane]) {
+    uint64_t acc = 0;
+    int64_t top = (int64_t)c;
+    uint32_t spins = 0;
+    for (;;) {
+        int jp = kLookbackPerLane;  // the lane's first PRE
+        bool z = false;             // a status not yet written before it
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = shfl_up_u32(sn, d);
-            if (lane >= d) sn += o;
-        }
-        const uint32_t ex_n = sn - n;
-        const uint64_t bend = bstart + shfl_u32(sn, 63);
-        // The 32 bits before the block: codes of the previous block's last 32
-        // symbols (each code >= 1 bit), combined across lanes 0..31.
-        uint32_t ptail = a.lead;
-        if (blk > 0) {
-            uint32_t pn = (uint32_t)(pe >> SH);
-            uint32_t pt = (uint32_t)(pe & CMASK);  // low 32 bits of the code
-#pragma unroll
-            for (int d = 1; d < 32; d <<= 1) {
-                const uint32_t on = shfl_up_u32(pn, d), ot = shfl_up_u32(pt, d);
-                if ((lane & 31) >= d) {
-                    pt = pn >= 32 ? pt : ((ot << pn) | pt);
-                    pn += on;
-                }
+        for (int j = 0; j < kLookbackPerLane; ++j) {
+            const uint32_t f = (uint32_t)(v[j] >> 62);
+            if (jp == kLookbackPerLane) {
+                if (f == 2u) jp = j;
+                else if (f == 0u) z = true;
             }
-            ptail = shfl_u32(pt, 31);
         }
-        const uint64_t o = bstart + ex_n;
-        // every word this block writes lies below ceil(bend / 32)
-        const bool fits = ((bend + 31) >> 5) <= a.out_words;
-        if (!fits && lane == 0) atomicOr(a.err, 4u);
-        const bool last = blk + 1 == a.nblocks;
-        const uint64_t wfirst = bstart >> 5;
-        const uint32_t nwords = (uint32_t)((bend >> 5) - wfirst);  // words completed inside the block
-        if (slot && !last && nwords <= a.slot_words) {
-            // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
-            // own: emit with the leading bits zero, then OR in the previous
-            // lane's tail once all lanes are done.
-            uint64_t acc = 0;
-            if constexpr (MODE == ENC_WIDE) {  // codes may exceed 32 bits
-                uint32_t na = (uint32_t)(o & 31);
-                pack_emit<MODE, true>(e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
-            } else {
-                pack_emit_lds<MODE>(e, acc, (uint32_t)(o - (wfirst << 5)), slot);
+        const uint64_t P = __ballot(jp < kLookbackPerLane);
+        const uint64_t upto = P ? ((P & (~P + 1)) << 1) - 1 : ~0ull;  // lanes up to the nearest PRE
+        if (!(__ballot(z) & upto)) {
+            uint64_t s = 0;
+            if ((upto >> lane) & 1) {
+#pragma unroll
+                for (int j = 0; j < kLookbackPerLane; ++j) s += j <= jp ? (v[j] & kStVal) : 0ull;
             }
-            uint32_t prev = shfl_up_u32((uint32_t)acc, 1);
-            if (lane == 0) prev = ptail;
-            const uint32_t h = (uint32_t)(o & 31);
-            if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
-            __builtin_amdgcn_wave_barrier();
-            if (fits)
-                for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
-            __builtin_amdgcn_wave_barrier();
+            acc += wave_sum_u64(s);
+            if (P) return acc;
+            top -= kWave * kLookbackPerLane;
+        } else if (++spins > kLookbackSpins) {
+            if (lane == 0) atomicOr(a.err, 8u);
+            return acc;
         } else {
-            // direct path: each lane needs the 32 bits before its run from the
-            // (bits, tail) scan, since a lane of the last block may hold < 32 bits
-            uint64_t t64 = 0;
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k) {
-                const uint32_t L = (uint32_t)(e[k] >> SH);
-                t64 = L ? ((t64 << L) | (uint64_t)(e[k] & CMASK)) : t64;
-            }
-            uint32_t tn = n, st = (uint32_t)t64;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t on = shfl_up_u32(tn, d), ot = shfl_up_u32(st, d);
-                if (lane >= d) {
-                    st = tn >= 32 ? st : (tn == 0 ? ot : ((ot << tn) | st));
-                    tn += on;
-                }
-            }
-            uint32_t ex_t = shfl_up_u32(st, 1);
-            if (lane == 0) ex_t = 0;
-            const uint32_t pre = ex_n >= 32 ? ex_t : (ex_n == 0 ? ptail : ((ptail << ex_n) | ex_t));
-            uint32_t na = (uint32_t)(o & 31);
-            uint64_t acc = na ? (uint64_t)(pre & ((1u << na) - 1u)) : 0ull;
-            uint32_t* dst = a.out + (o >> 5);
-            pack_emit<MODE, false>(e, acc, na, dst, fits);
-            dst += (uint32_t)(((o & 31) + n) >> 5);
-            if (fits && nvalid > 0 && sym0 + (uint64_t)nvalid == a.nsym && na > 0)
-                *dst = bswap32((uint32_t)(acc << (32 - na)));
+            __builtin_amdgcn_s_sleep(1);
         }
-        if (a.index) {  // block index (hz_internal.h): start bits + the lane's chain offsets
-            uint64_t sub = 0;
-#pragma unroll
-            for (int c = 0; c < kChainsPerLane; ++c) sub |= (uint64_t)((ex_n + nc[c]) & 0xffffu) << (16 * c);
-            a.index_sub[blk * kWave + lane] = sub;
-            if (lane == 0) {
-                a.index[blk] = bstart;
-                if (last) a.index[a.nblocks] = bend;
+        lookback_load(a, top, lane, v);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kPackWriteThreads) void k_pack_onepass(PackArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t* slot = a.slot_words ? lds + a.lds_words + wid * a.slot_words : nullptr;
+    uint32_t* ctl = lds + a.lds_words + nw * a.slot_words;  // 16-byte aligned (launcher)
+    uint32_t* wb = ctl + 8;                                 // block bits: [chunk parity][wave]
+    unsigned long long* ws = reinterpret_cast<unsigned long long*>(ctl + 24);  // block starts of the chunk
+    // Wave 0 is the control wave: tickets, status words and the look-back.
+    // It issues no other memory operation, so its look-back loads are never
+    // waited on behind the packing waves' table escapes (vmcnt is in order).
+    // Waves 1 .. nw-1 pack one block each of a chunk of np = nw - 1 blocks.
+    const uint32_t np = nw - 1;
+    const uint64_t nchunks = (a.nblocks + np - 1) / np;
+    if (threadIdx.x == 0) {
+        ctl[0] = chunk_ticket(a.ticket);
+        ctl[1] = chunk_ticket(a.ticket);
+        ctl[2] = chunk_ticket(a.ticket);
+    }
+    __syncthreads();
+    uint64_t c0 = ctl[0], c1 = ctl[1], c2 = ctl[2];
+    uint64_t max_bits = 0;
+    if (c0 < nchunks) {
+        const uint32_t pw = wid ? wid - 1 : 0;  // packing wave index
+        auto blk_of = [&](uint64_t c) { return c * np + pw; };
+        auto clampb = [&](uint64_t b) { return b < a.nblocks ? b : a.nblocks - 1; };
+        PackIn nx;
+        PackBlk<MODE> bA, bB;
+        if (wid) {
+            pack_prefetch<false>(a, clampb(blk_of(c0)), lane, nx);
+            pack_block_lookup<MODE>(a, lds, blk_of(c0), lane, nx, bA);
+            pack_prefetch<false>(a, clampb(blk_of(c1)), lane, nx);
+            pack_block_count<MODE>(lane, bA);
+            if (lane == 0) wb[pw] = blk_of(c0) < a.nblocks ? bA.bits : 0u;
+        }
+        __syncthreads();
+        uint32_t q = 0;
+        uint64_t cbits0 = 0;  // chunk c0's bits (wave 0)
+        if (wid == 0) {
+            for (uint32_t w = 0; w < np; ++w) cbits0 += wb[w];
+            if (lane == 0) st_store(a.blk + c0, kStAgg | cbits0);
+        }
+        // cur: chunk c0 (looked up, AGG published); nx: chunk c1's input in flight
+        auto step = [&](PackBlk<MODE>& cur, PackBlk<MODE>& nxt) -> bool {
+            uint64_t cbits1 = 0;
+            if (wid == 0) {
+                // while the packing waves look up chunk c1: resolve chunk c0's
+                // start (its predecessors published AGG a step ago) and publish PRE
+                uint32_t t3 = 0xffffffffu;  // one ticket per workgroup: lane 0 only
+                if (lane == 0 && c2 < nchunks) t3 = chunk_ticket(a.ticket);
+                unsigned long long v[kLookbackPerLane];
+                lookback_load(a, (int64_t)c0, lane, v);
+                const uint64_t s0 = lookback_resolve(a, c0, lane, v);
+                if (lane == 0) {
+                    st_store(a.blk + c0, kStPre | ((s0 + cbits0) & kStVal));
+                    uint64_t s = s0;
+                    for (uint32_t w = 0; w < np; ++w) { ws[w] = s; s += wb[q * 8 + w]; }
+                    ctl[3] = t3;
+                }
+            } else if (c1 < nchunks) {
+                pack_block_lookup<MODE>(a, lds, blk_of(c1), lane, nx, nxt);
+                pack_prefetch<false>(a, clampb(blk_of(c2)), lane, nx);
+                pack_block_count<MODE>(lane, nxt);
+                if (lane == 0) wb[(q ^ 1) * 8 + pw] = blk_of(c1) < a.nblocks ? nxt.bits : 0u;
             }
-            max_bits = bend - bstart > max_bits ? bend - bstart : max_bits;
+            __syncthreads();
+            const uint64_t c3 = ctl[3];
+            if (wid == 0) {
+                if (c1 < nchunks) {
+                    for (uint32_t w = 0; w < np; ++w) cbits1 += wb[(q ^ 1) * 8 + w];
+                    if (lane == 0) st_store(a.blk + c1, kStAgg | cbits1);
+                }
+            } else {
+                const uint64_t b0 = blk_of(c0);
+                if (b0 < a.nblocks) pack_block_emit<MODE>(a, slot, b0, lane, cur, ws[pw], max_bits);
+            }
+            __syncthreads();
+            c0 = c1; c1 = c2; c2 = c3; cbits0 = cbits1; q ^= 1;
+            return c0 < nchunks;
+        };
+        for (;;) {
+            if (!step(bA, bB)) break;
+            if (!step(bB, bA)) break;
         }
     }
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
@@ -782,7 +988,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
-    return 2 * nblocks + ntiles;
+    const uint64_t three_pass = 2 * nblocks + ntiles;
+    const uint64_t one_pass = nblocks + 4;  // ticket, pad, one status word per chunk (16-byte multiple)
+    return three_pass > one_pass ? three_pass : one_pass;
+}
+
+// HZ_PACK_ONEPASS=0 selects the three-pass pack (count + scan + write) for A/B runs.
+static bool pack_onepass_enabled() {
+    static const int v = [] { const char* e = getenv("HZ_PACK_ONEPASS"); return e ? atoi(e) : 0; }();
+    return v != 0;
 }
 
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
@@ -822,21 +1036,44 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     }
     // Waves per workgroup: as many output slots of the expected block size
     // (Kraft estimate from the code lengths, +12 %) as fit beside the table.
+    const bool onepass = (t.enc_mode == ENC_HOT || t.enc_mode == ENC_DENSE) && pack_onepass_enabled();
+    const uint32_t ctl_words = onepass ? kOnepassCtlWords : 0;
     const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
     a.lds_words = table_words;
-    const uint32_t free_words = kLdsBytes / 4 - table_words;
+    const uint32_t free_words = kLdsBytes / 4 - table_words - ctl_words;
     const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * 1.12 / 32.0) + 4;
     constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
     uint32_t waves = free_words / est_words;
     waves = waves > kMaxWaves ? kMaxWaves : waves;
     a.slot_words = 0;
-    if (waves >= 6) a.slot_words = free_words / waves;
+    if (waves >= 6) a.slot_words = (free_words / waves) & ~3u;  // keeps the one-pass control block 16-B aligned
     else waves = kMaxWaves;  // no room for slots: lanes store directly
     const int threads = (int)waves * 64;
     uint64_t wgs = (nblocks + waves - 1) / waves;
-    const uint32_t lds = 4 * (table_words + waves * a.slot_words);
+    const uint32_t lds = 4 * (table_words + waves * a.slot_words + ctl_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
+    if (onepass) {
+        static bool attr1[2] = {false, false};
+        const void* f1 = t.enc_mode == ENC_HOT ? (const void*)k_pack_onepass<ENC_HOT> : (const void*)k_pack_onepass<ENC_DENSE>;
+        if (!attr1[t.enc_mode == ENC_HOT]) {
+            hipError_t e = hipFuncSetAttribute(f1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            attr1[t.enc_mode == ENC_HOT] = true;
+        }
+        // scratch: [0] ticket, [1] pad, [2 ..] one status word per chunk; zeroed together
+        const uint64_t nchunks = (nblocks + waves - 2) / (waves - 1);  // wave 0 of a workgroup packs nothing
+        a.ticket = d_scratch;
+        a.blk = d_scratch + 2;
+        a.start_bit = start_bit;
+        hipError_t e = hipMemsetAsync(d_scratch, 0, ((nchunks + 3) & ~1ull) * 8, s);
+        if (e != hipSuccess) return e;
+        if (t.enc_mode == ENC_HOT)
+            hipLaunchKernelGGL(k_pack_onepass<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a);
+        else
+            hipLaunchKernelGGL(k_pack_onepass<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a);
+        return hipGetLastError();
+    }
     static bool attr[3] = {false, false, false};
     static bool attr_count = false;
     if (!attr_count) {
