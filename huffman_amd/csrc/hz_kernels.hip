@@ -251,8 +251,6 @@ struct PackArgs {
     unsigned long long* index_sub;  // block index sub[] (four u16 chain offsets per lane)
     uint32_t* err;
     uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
-    uint64_t start_bit;          // k_pack_onepass: the stream's first bit (the end of chunk -1)
-    unsigned long long* ticket;  // k_pack_onepass: chunk ticket counter (zeroed per launch)
 };
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
@@ -278,7 +276,6 @@ struct PackIn {
     uint64_t bstart;
 };
 
-template <bool WITH_START = true>
 HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     const uint64_t ls = sym0 + kSPT <= a.nsym ? sym0 : 0;
@@ -290,7 +287,7 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
     x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
-    x.bstart = WITH_START ? a.blk_start[blk] : 0ull;
+    x.bstart = a.blk_start[blk];
 }
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
@@ -655,174 +652,6 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
-// ---- one pass: decoupled look-back replaces k_pack_count + k_scan_* ---------
-// A workgroup of nw waves packs chunks of nw consecutive blocks (one per
-// wave) and takes chunks in ticket order, so every chunk's predecessors belong
-// to running workgroups (hard part (e)). Chunk c publishes one
-// status word {flag:2 | bits:62}: AGG (its own bits) once its blocks are
-// looked up, PRE (its end bit) once its start is known. Its start comes from
-// the status words of the 256 chunks before it, read by one wave in one
-// round trip (4 per lane) and summed back to the nearest PRE; chunk -1 is PRE
-// at the stream's start bit. Status words are written and read only with
-// agent-scope atomics, the value being its own flag (cdna_hip_programming.md
-// Guideline 16, R2), and are zeroed before every launch.
-// Schedule per step: the look-back loads of chunk c are issued, chunk c + 1 is
-// looked up (its AGG published), then chunk c's look-back is resolved -- the
-// chunks before it published AGG a step earlier and those a round earlier
-// (one chunk per workgroup) PRE -- and chunk c is written. Tickets run two
-// chunks ahead so chunk c + 2's input is in flight meanwhile.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-constexpr unsigned long long kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
-constexpr int kLookbackPerLane = 4;
-constexpr uint32_t kLookbackSpins = 1u << 22;  // bounded: a wave that gives up flags HZ_ETIMEOUT (err bit 8)
-constexpr uint32_t kOnepassCtlWords = 48;      // LDS: tickets, block bits [2][8], block starts u64[8]
-
-HZ_DEV unsigned long long st_load(const unsigned long long* p) {
-    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-HZ_DEV void st_store(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-HZ_DEV uint32_t chunk_ticket(unsigned long long* ctr) {
-    return (uint32_t)__hip_atomic_fetch_add((gu64*)ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Status of chunks top - 1 - (4 lane + j).
-HZ_DEV void lookback_load(const PackArgs& a, int64_t top, int lane, unsigned long long (&v)[kLookbackPerLane]) {
-#pragma unroll
-    for (int j = 0; j < kLookbackPerLane; ++j) {
-        const int64_t idx = top - 1 - (int64_t)(kLookbackPerLane * lane + j);
-        v[j] = idx >= 0 ? st_load(a.blk + idx) : (idx == -1 ? (kStPre | a.start_bit) : kStPre);
-    }
-}
-
-// Start bit of chunk c (wave uniform) from the window v = lookback_load(c).
-HZ_DEV uint64_t lookback_resolve(const PackArgs& a, uint64_t c, int lane, unsigned long long (&v)[kLookbackPerLane]) {
-    uint64_t acc = 0;
-    int64_t top = (int64_t)c;
-    uint32_t spins = 0;
-    for (;;) {
-        int jp = kLookbackPerLane;  // the lane's first PRE
-        bool z = false;             // a status not yet written before it
-#pragma unroll
-        for (int j = 0; j < kLookbackPerLane; ++j) {
-            const uint32_t f = (uint32_t)(v[j] >> 62);
-            if (jp == kLookbackPerLane) {
-                if (f == 2u) jp = j;
-                else if (f == 0u) z = true;
-            }
-        }
-        const uint64_t P = __ballot(jp < kLookbackPerLane);
-        const uint64_t upto = P ? ((P & (~P + 1)) << 1) - 1 : ~0ull;  // lanes up to the nearest PRE
-        if (!(__ballot(z) & upto)) {
-            uint64_t s = 0;
-            if ((upto >> lane) & 1) {
-#pragma unroll
-                for (int j = 0; j < kLookbackPerLane; ++j) s += j <= jp ? (v[j] & kStVal) : 0ull;
-            }
-            acc += wave_sum_u64(s);
-            if (P) return acc;
-            top -= kWave * kLookbackPerLane;
-        } else if (++spins > kLookbackSpins) {
-            if (lane == 0) atomicOr(a.err, 8u);
-            return acc;
-        } else {
-            __builtin_amdgcn_s_sleep(1);
-        }
-        lookback_load(a, top, lane, v);
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kPackWriteThreads) void k_pack_onepass(PackArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
-    const int lane = threadIdx.x & 63;
-    const uint32_t wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t* slot = a.slot_words ? lds + a.lds_words + wid * a.slot_words : nullptr;
-    uint32_t* ctl = lds + a.lds_words + nw * a.slot_words;  // 16-byte aligned (launcher)
-    uint32_t* wb = ctl + 8;                                 // block bits: [chunk parity][wave]
-    unsigned long long* ws = reinterpret_cast<unsigned long long*>(ctl + 24);  // block starts of the chunk
-    // Wave 0 is the control wave: tickets, status words and the look-back.
-    // It issues no other memory operation, so its look-back loads are never
-    // waited on behind the packing waves' table escapes (vmcnt is in order).
-    // Waves 1 .. nw-1 pack one block each of a chunk of np = nw - 1 blocks.
-    const uint32_t np = nw - 1;
-    const uint64_t nchunks = (a.nblocks + np - 1) / np;
-    if (threadIdx.x == 0) {
-        ctl[0] = chunk_ticket(a.ticket);
-        ctl[1] = chunk_ticket(a.ticket);
-        ctl[2] = chunk_ticket(a.ticket);
-    }
-    __syncthreads();
-    uint64_t c0 = ctl[0], c1 = ctl[1], c2 = ctl[2];
-    uint64_t max_bits = 0;
-    if (c0 < nchunks) {
-        const uint32_t pw = wid ? wid - 1 : 0;  // packing wave index
-        auto blk_of = [&](uint64_t c) { return c * np + pw; };
-        auto clampb = [&](uint64_t b) { return b < a.nblocks ? b : a.nblocks - 1; };
-        PackIn nx;
-        PackBlk<MODE> bA, bB;
-        if (wid) {
-            pack_prefetch<false>(a, clampb(blk_of(c0)), lane, nx);
-            pack_block_lookup<MODE>(a, lds, blk_of(c0), lane, nx, bA);
-            pack_prefetch<false>(a, clampb(blk_of(c1)), lane, nx);
-            pack_block_count<MODE>(lane, bA);
-            if (lane == 0) wb[pw] = blk_of(c0) < a.nblocks ? bA.bits : 0u;
-        }
-        __syncthreads();
-        uint32_t q = 0;
-        uint64_t cbits0 = 0;  // chunk c0's bits (wave 0)
-        if (wid == 0) {
-            for (uint32_t w = 0; w < np; ++w) cbits0 += wb[w];
-            if (lane == 0) st_store(a.blk + c0, kStAgg | cbits0);
-        }
-        // cur: chunk c0 (looked up, AGG published); nx: chunk c1's input in flight
-        auto step = [&](PackBlk<MODE>& cur, PackBlk<MODE>& nxt) -> bool {
-            uint64_t cbits1 = 0;
-            if (wid == 0) {
-                // while the packing waves look up chunk c1: resolve chunk c0's
-                // start (its predecessors published AGG a step ago) and publish PRE
-                uint32_t t3 = 0xffffffffu;  // one ticket per workgroup: lane 0 only
-                if (lane == 0 && c2 < nchunks) t3 = chunk_ticket(a.ticket);
-                unsigned long long v[kLookbackPerLane];
-                lookback_load(a, (int64_t)c0, lane, v);
-                const uint64_t s0 = lookback_resolve(a, c0, lane, v);
-                if (lane == 0) {
-                    st_store(a.blk + c0, kStPre | ((s0 + cbits0) & kStVal));
-                    uint64_t s = s0;
-                    for (uint32_t w = 0; w < np; ++w) { ws[w] = s; s += wb[q * 8 + w]; }
-                    ctl[3] = t3;
-                }
-            } else if (c1 < nchunks) {
-                pack_block_lookup<MODE>(a, lds, blk_of(c1), lane, nx, nxt);
-                pack_prefetch<false>(a, clampb(blk_of(c2)), lane, nx);
-                pack_block_count<MODE>(lane, nxt);
-                if (lane == 0) wb[(q ^ 1) * 8 + pw] = blk_of(c1) < a.nblocks ? nxt.bits : 0u;
-            }
-            __syncthreads();
-            const uint64_t c3 = ctl[3];
-            if (wid == 0) {
-                if (c1 < nchunks) {
-                    for (uint32_t w = 0; w < np; ++w) cbits1 += wb[(q ^ 1) * 8 + w];
-                    if (lane == 0) st_store(a.blk + c1, kStAgg | cbits1);
-                }
-            } else {
-                const uint64_t b0 = blk_of(c0);
-                if (b0 < a.nblocks) pack_block_emit<MODE>(a, slot, b0, lane, cur, ws[pw], max_bits);
-            }
-            __syncthreads();
-            c0 = c1; c1 = c2; c2 = c3; cbits0 = cbits1; q ^= 1;
-            return c0 < nchunks;
-        };
-        for (;;) {
-            if (!step(bA, bB)) break;
-            if (!step(bB, bA)) break;
-        }
-    }
-    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
-}
-
 // ---- every code 16 bits (U = 65 536, min_len = max_len = 16) ---------------
 // Symbol i starts at bit start_bit + 16 i: no count pass and no scan. Lane j
 // packs symbols [32 j, 32 j + 32) into the 16 words whose last bit lies in its
@@ -988,15 +817,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
-    const uint64_t three_pass = 2 * nblocks + ntiles;
-    const uint64_t one_pass = nblocks + 4;  // ticket, pad, one status word per chunk (16-byte multiple)
-    return three_pass > one_pass ? three_pass : one_pass;
-}
-
-// HZ_PACK_ONEPASS=0 selects the three-pass pack (count + scan + write) for A/B runs.
-static bool pack_onepass_enabled() {
-    static const int v = [] { const char* e = getenv("HZ_PACK_ONEPASS"); return e ? atoi(e) : 0; }();
-    return v != 0;
+    return 2 * nblocks + ntiles;
 }
 
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
@@ -1036,44 +857,21 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     }
     // Waves per workgroup: as many output slots of the expected block size
     // (Kraft estimate from the code lengths, +12 %) as fit beside the table.
-    const bool onepass = (t.enc_mode == ENC_HOT || t.enc_mode == ENC_DENSE) && pack_onepass_enabled();
-    const uint32_t ctl_words = onepass ? kOnepassCtlWords : 0;
     const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
     a.lds_words = table_words;
-    const uint32_t free_words = kLdsBytes / 4 - table_words - ctl_words;
+    const uint32_t free_words = kLdsBytes / 4 - table_words;
     const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * 1.12 / 32.0) + 4;
     constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
     uint32_t waves = free_words / est_words;
     waves = waves > kMaxWaves ? kMaxWaves : waves;
     a.slot_words = 0;
-    if (waves >= 6) a.slot_words = (free_words / waves) & ~3u;  // keeps the one-pass control block 16-B aligned
+    if (waves >= 6) a.slot_words = free_words / waves;
     else waves = kMaxWaves;  // no room for slots: lanes store directly
     const int threads = (int)waves * 64;
     uint64_t wgs = (nblocks + waves - 1) / waves;
-    const uint32_t lds = 4 * (table_words + waves * a.slot_words + ctl_words);
+    const uint32_t lds = 4 * (table_words + waves * a.slot_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
-    if (onepass) {
-        static bool attr1[2] = {false, false};
-        const void* f1 = t.enc_mode == ENC_HOT ? (const void*)k_pack_onepass<ENC_HOT> : (const void*)k_pack_onepass<ENC_DENSE>;
-        if (!attr1[t.enc_mode == ENC_HOT]) {
-            hipError_t e = hipFuncSetAttribute(f1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-            attr1[t.enc_mode == ENC_HOT] = true;
-        }
-        // scratch: [0] ticket, [1] pad, [2 ..] one status word per chunk; zeroed together
-        const uint64_t nchunks = (nblocks + waves - 2) / (waves - 1);  // wave 0 of a workgroup packs nothing
-        a.ticket = d_scratch;
-        a.blk = d_scratch + 2;
-        a.start_bit = start_bit;
-        hipError_t e = hipMemsetAsync(d_scratch, 0, ((nchunks + 3) & ~1ull) * 8, s);
-        if (e != hipSuccess) return e;
-        if (t.enc_mode == ENC_HOT)
-            hipLaunchKernelGGL(k_pack_onepass<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a);
-        else
-            hipLaunchKernelGGL(k_pack_onepass<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a);
-        return hipGetLastError();
-    }
     static bool attr[3] = {false, false, false};
     static bool attr_count = false;
     if (!attr_count) {
