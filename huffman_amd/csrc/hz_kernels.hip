@@ -29,6 +29,28 @@ HZ_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 HZ_DEV uint32_t shfl_up_u32(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
 HZ_DEV uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
 HZ_DEV uint32_t shfl_xor_u32(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
+// DPP lane moves (VALU, no LDS round trip). Lanes whose source lies outside
+// the row (row_shr) or outside row_mask read 0.
+template <int CTRL, int ROWS = 0xf>
+HZ_DEV uint32_t dpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138;
+
+// Inclusive prefix sum over the 64 lanes.
+HZ_DEV uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp0<kDppRowShr1>(v);
+    v += dpp0<kDppRowShr2>(v);
+    v += dpp0<kDppRowShr4>(v);
+    v += dpp0<kDppRowShr8>(v);
+    v += dpp0<kDppRowBcast15, 0xa>(v);
+    v += dpp0<kDppRowBcast31, 0xc>(v);
+    return v;
+}
+
+HZ_DEV uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
 HZ_DEV uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
@@ -520,15 +542,10 @@ HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
         if (k % kChainSyms == 0) b.nc[k / kChainSyms] = n;
         n += (uint32_t)(b.e[k] >> SH);
     }
-    uint32_t sn = n;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = shfl_up_u32(sn, d);
-        if (lane >= d) sn += o;
-    }
+    const uint32_t sn = wave_incl_sum(n);
     b.n = n;
     b.ex_n = sn - n;
-    b.bits = shfl_u32(sn, 63);
+    b.bits = readlane(sn, 63);
 }
 
 // Writes block `blk` starting at absolute bit `bstart`, plus its index entries.
@@ -545,17 +562,20 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     // symbols (each code >= 1 bit), combined across lanes 0..31.
     uint32_t ptail = a.lead;
     if (blk > 0) {
+        // Concatenation scan (associative; (0, 0) is its identity, which is what
+        // DPP lanes without a source read) over lanes 0..31: rows, then row 0 into row 1.
         uint32_t pn = (uint32_t)(b.pe >> SH);
         uint32_t pt = (uint32_t)(b.pe & CMASK);  // low 32 bits of the code
-#pragma unroll
-        for (int d = 1; d < 32; d <<= 1) {
-            const uint32_t on = shfl_up_u32(pn, d), ot = shfl_up_u32(pt, d);
-            if ((lane & 31) >= d) {
-                pt = pn >= 32 ? pt : ((ot << pn) | pt);
-                pn += on;
-            }
-        }
-        ptail = shfl_u32(pt, 31);
+        auto step = [&](uint32_t on, uint32_t ot) {
+            pt = pn >= 32 ? pt : ((ot << pn) | pt);
+            pn += on;
+        };
+        step(dpp0<kDppRowShr1>(pn), dpp0<kDppRowShr1>(pt));
+        step(dpp0<kDppRowShr2>(pn), dpp0<kDppRowShr2>(pt));
+        step(dpp0<kDppRowShr4>(pn), dpp0<kDppRowShr4>(pt));
+        step(dpp0<kDppRowShr8>(pn), dpp0<kDppRowShr8>(pt));
+        step(dpp0<kDppRowBcast15, 0xa>(pn), dpp0<kDppRowBcast15, 0xa>(pt));
+        ptail = readlane(pt, 31);
     }
     const uint64_t o = bstart + ex_n;
     // every word this block writes lies below ceil(bend / 32)
@@ -575,8 +595,8 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
         } else {
             pack_emit_lds<MODE>(b.e, acc, (uint32_t)(o - (wfirst << 5)), slot);
         }
-        uint32_t prev = shfl_up_u32((uint32_t)acc, 1);
-        if (lane == 0) prev = ptail;
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)ptail, (int)(uint32_t)acc, kDppWaveShr1,
+                                                                    0xf, 0xf, false);  // lane 0: ptail
         const uint32_t h = (uint32_t)(o & 31);
         if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
         __builtin_amdgcn_wave_barrier();
@@ -1197,6 +1217,37 @@ HZ_DEV PipeLane dec_pipe_lds(const DecArgs& a, const uint32_t* lds, const uint32
     return r;
 }
 
+// The LDS steps of two chains at once, branch-free so the compiler keeps one
+// basic block: both window reads, then both level-1 reads, then both
+// LDS-second-level reads are in flight together (three LDS round trips for the
+// pair instead of three per chain). Lanes without an LDS second level read
+// word 0 (a broadcast, no bank conflict) and keep their level-1 entry.
+HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, uint32_t pos0, uint32_t pos1,
+                          PipeLane& r0, PipeLane& r1) {
+    const uint32_t k = (uint32_t)a.k;
+    const uint32_t pa = pos0 - 1u, pb = pos1 - 1u;  // >= 127 (staging pad)
+    const uint32_t* wa = stg + (pa >> 5);
+    const uint32_t* wb = stg + (pb >> 5);
+    const uint32_t a0 = wa[0], a1 = wa[1], b0 = wb[0], b1 = wb[1];
+    const uint32_t Wa = __builtin_amdgcn_alignbit(a0, a1, 31u - pa);
+    const uint32_t Wb = __builtin_amdgcn_alignbit(b0, b1, 31u - pb);
+    uint32_t ea = lds[Wa >> (32 - k)];
+    uint32_t eb = lds[Wb >> (32 - k)];
+    const bool ha = (ea >> 30) == 1u, hb = (eb >> 30) == 1u;
+    const uint32_t na = (ea >> 26) & 15u, nb = (eb >> 26) & 15u;
+    const uint32_t ia = ha ? (ea & 0x3ffffffu) + ((Wa << k) >> (32 - na)) : 0u;
+    const uint32_t ib = hb ? (eb & 0x3ffffffu) + ((Wb << k) >> (32 - nb)) : 0u;
+    const uint32_t xa = lds[ia], xb = lds[ib];
+    const uint32_t Da = ha ? k + na : k, Db = hb ? k + nb : k;
+    ea = ha ? xa : ea;
+    eb = hb ? xb : eb;
+    const uint32_t ga = (ea >> 26) & 15u, gb = (eb >> 26) & 15u;
+    r0.e = ea;
+    r1.e = eb;
+    r0.gi = (ea >> 31) ? 0u : (ea & 0x3ffffffu) + ((Wa << Da) >> (32 - ga));
+    r1.gi = (eb >> 31) ? 0u : (eb & 0x3ffffffu) + ((Wb << Db) >> (32 - gb));
+}
+
 // Block metadata of the pipelined decoder: start and end bit, the lane's chain offsets.
 struct PipeMeta {
     uint64_t b0, b1, sub;
@@ -1268,6 +1319,9 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
 #ifndef HZ_PIPE_QUARTER
 #define HZ_PIPE_QUARTER 0
 #endif
+#ifndef HZ_PIPE_PAIR
+#define HZ_PIPE_PAIR 1
+#endif
 // Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
 // staging chunks of the next block and the metadata of the one after are
 // loaded halfway through this block's steps, so no block waits on HBM.
@@ -1320,6 +1374,26 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
             if (q + 1 < kChainSyms) issue(1);
             finish(2, q);
             if (q + 1 < kChainSyms) issue(2);
+            finish(3, q);
+        }
+#elif HZ_PIPE_PAIR
+        auto issue2 = [&](int c) {
+            dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
+            g[c] = a.l2[st[c].gi];
+            g[c + 1] = a.l2[st[c + 1].gi];
+        };
+        issue2(0);
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+            issue2(2);
+            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
+                dec_stage_prefetch(a, mn, lane, sn);
+                dec_meta_load(a, b + 2 * stride, lane, mn2);
+            }
+            finish(0, q);
+            finish(1, q);
+            if (q + 1 < kChainSyms) issue2(0);
+            finish(2, q);
             finish(3, q);
         }
 #else
