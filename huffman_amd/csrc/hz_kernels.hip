@@ -1426,8 +1426,90 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
     }
 }
 
-template <int MODE, bool WIDE, bool PIPE>
-__global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
+// Two blocks per wave (8 chains per lane in 4 pairs): each pair's global
+// lookups are consumed after the other three pairs' LDS walks, so a gather
+// has three walks to land in instead of one. Half as many waves (two staging
+// slots each) hold the same LDS; blocks b, b + 1, then b + stride, ...
+HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg, uint32_t slot, uint64_t b,
+                           uint64_t stride, int lane) {
+    constexpr int C = 2 * kChainsPerLane;
+    static_assert(kChainsPerLane == 4, "four pairs of chains over two blocks");
+    PipeMeta mc[2], mn[2], mn2[2];
+    uint4 sc[2][kStageUnroll], sn[2][kStageUnroll];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        dec_meta_load(a, b + j, lane, mc[j]);
+        dec_meta_load(a, b + stride + j, lane, mn[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mc[j], lane, sc[j]);
+    for (; b < a.nblocks; b += stride) {
+        uint32_t pos[C];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            uint64_t w0;
+            dec_stage_commit(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
+            uint32_t off[kChainsPerLane];
+            dec_chain_offsets(mc[j].sub, mc[j].b1 - mc[j].b0, lane, off);
+            const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u;
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c) pos[j * kChainsPerLane + c] = base + off[c];
+        }
+        __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+        uint32_t pk[2][kSPT / 2];
+        PipeLane st[C];
+        uint32_t g[C];
+        auto finish = [&](int c, int q) {
+            const uint32_t ee = (st[c].e >> 31) ? st[c].e : g[c];
+            pos[c] += (ee >> 16) & 63u;
+            const uint32_t sym = ee & 0xffffu;
+            const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
+            if (q & 1) pk[c / kChainsPerLane][i] |= sym << 16;
+            else pk[c / kChainsPerLane][i] = sym;
+        };
+        auto issue2 = [&](int c) {
+            dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
+            g[c] = a.l2[st[c].gi];
+            g[c + 1] = a.l2[st[c + 1].gi];
+        };
+        issue2(0);
+        issue2(2);
+        issue2(4);
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+            issue2(6);
+            if (q == HZ_PF_STEP) {  // the next two blocks' staging chunks, the metadata after them
+#pragma unroll
+                for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) dec_meta_load(a, b + 2 * stride + j, lane, mn2[j]);
+            }
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) {
+                finish(c, q);
+                finish(c + 1, q);
+                if (q + 1 < kChainSyms) issue2(c);
+            }
+            finish(6, q);
+            finish(7, q);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (b + j < a.nblocks) dec_store(a, b + j, lane, pk[j]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            mc[j] = mn[j];
+            mn[j] = mn2[j];
+#pragma unroll
+            for (int u = 0; u < kStageUnroll; ++u) sc[j][u] = sn[j][u];
+        }
+    }
+}
+
+// PIPE: 0 plain block loop, 1 pipelined (one block per wave), 2 pipelined, two blocks per wave
+template <int MODE, bool WIDE, int PIPE>
+__global__ __launch_bounds__(PIPE == 2 ? 512 : 1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
@@ -1435,12 +1517,22 @@ __global__ __launch_bounds__(1024) void k_decode(DecArgs a) {
     // slots fit the stream's largest block; waves without a slot have nothing to do
     const uint32_t slot = dec_slot_words(a.starts[a.nblocks + 1], a.max_len);
     const uint32_t nwave = blockDim.x >> 6;
+    if constexpr (PIPE == 2) {
+        uint32_t nw2 = a.region_words / (2 * slot);
+        nw2 = nw2 < nwave ? nw2 : nwave;
+        if (nw2 > 0) {  // else one block per wave below (a stream whose largest block needs more)
+            if (wid >= nw2) return;
+            const uint64_t b = 2 * ((uint64_t)blockIdx.x * nw2 + wid), stride = 2 * (uint64_t)gridDim.x * nw2;
+            dec_wave_pipe2(a, lds, lds + a.lds_words + wid * 2 * slot, slot, b, stride, lane);
+            return;
+        }
+    }
     uint32_t nw = a.region_words / slot;
     nw = nw < nwave ? nw : nwave;
     if (wid >= nw) return;
     uint32_t* stg = lds + a.lds_words + wid * slot;
     const uint64_t b = (uint64_t)blockIdx.x * nw + wid, stride = (uint64_t)gridDim.x * nw;
-    if constexpr (PIPE) {
+    if constexpr (PIPE != 0) {
         dec_wave_pipe(a, lds, stg, slot, b, stride, lane);
     } else {
         for (uint64_t bb = b; bb < a.nblocks; bb += stride) dec_group<MODE, WIDE, 1>(a, lds, stg, slot, bb, lane);
@@ -1523,7 +1615,7 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
 // index's max_bits and idles the waves that do not get one. Up to two
 // workgroups per CU (each holds its own table copy): whichever shape runs
 // more waves.
-template <int MODE, bool WIDE, bool PIPE>
+template <int MODE, bool WIDE, int PIPE>
 static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
@@ -1554,7 +1646,9 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
     uint64_t wgs = (a.nblocks + best_w - 1) / best_w;
     const uint64_t cap = (uint64_t)ncu * best_g;
     if (wgs > cap) wgs = cap;
-    hipLaunchKernelGGL((k_decode<MODE, WIDE, PIPE>), dim3(wgs), dim3(64 * best_w), lds, s, b);
+    // PIPE 2: a wave takes two slots (at most 8 waves, up to 256 VGPRs each)
+    const int threads = PIPE == 2 ? (64 * best_w < 512 ? 64 * best_w : 512) : 64 * best_w;
+    hipLaunchKernelGGL((k_decode<MODE, WIDE, PIPE>), dim3(wgs), dim3(threads), lds, s, b);
     return hipGetLastError();
 }
 
@@ -1583,13 +1677,14 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     }
     const uint64_t pbits = payload_bytes * 8;
     const bool wide = t.dec_max_len > 32;
-    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false, false>(a, pbits, ncu, s);
-    if (wide) return run_decode<DEC_LUT, true, false>(a, pbits, ncu, s);
+    if (t.dec_mode == DEC_DENSE) return run_decode<DEC_DENSE, false, 0>(a, pbits, ncu, s);
+    if (wide) return run_decode<DEC_LUT, true, 0>(a, pbits, ncu, s);
     // two levels suffice (no lookup chain past a global subtable): pipelined gathers
-    static const int pipe_env = [] { const char* v = getenv("HZ_DEC_PIPE"); return v ? atoi(v) : 1; }();
+    static const int pipe_env = [] { const char* v = getenv("HZ_DEC_PIPE"); return v ? atoi(v) : 2; }();
     if (pipe_env && t.dec_max_len <= t.dec_k + kDecLevelBits && a.nwords >= 4)
-        return run_decode<DEC_LUT, false, true>(a, pbits, ncu, s);
-    return run_decode<DEC_LUT, false, false>(a, pbits, ncu, s);
+        return pipe_env == 1 ? run_decode<DEC_LUT, false, 1>(a, pbits, ncu, s)
+                             : run_decode<DEC_LUT, false, 2>(a, pbits, ncu, s);
+    return run_decode<DEC_LUT, false, 0>(a, pbits, ncu, s);
 }
 
 // ===========================================================================

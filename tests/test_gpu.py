@@ -139,6 +139,32 @@ def test_cli_archive_extract(hz, tmp_path):
         assert (d / "DECOMPRESSED_FILE").read_bytes() == read("romeo.txt")
 
 
+def _skewed_bytes(n, seed):
+    """One frequent symbol everywhere except a run of rare symbols (long codes):
+    the stream's largest block is far above the average block (decode slots
+    sized from max_bits, the two-block decoder's one-block fallback)."""
+    rng = np.random.default_rng(seed)
+    sym = np.zeros(n // 2, dtype=np.uint16)
+    sym[4096:8192] = rng.integers(1, 65536, 4096)
+    sym[8192:] = np.where(rng.random(n // 2 - 8192) < 0.02, rng.integers(1, 200, n // 2 - 8192), 0)
+    return sym.astype("<u2").tobytes()
+
+
+@pytest.mark.parametrize("pipe", ["0", "1", "2"])
+@pytest.mark.parametrize("kind", ["zipf", "skewed"])
+def test_decode_variants_cli(hz, tmp_path, pipe, kind):
+    """Every LUT decoder (HZ_DEC_PIPE: 0 plain, 1 pipelined, 2 two blocks per wave) through `extract`."""
+    data = _zipf_bytes((6 << 20) + 1, 11) if kind == "zipf" else _skewed_bytes(6 << 20, 5)
+    blob = hz.encode(data)
+    assert blob == oracle_lib.encode(data)
+    (tmp_path / "x.compressed").write_bytes(blob)
+    env = dict(os.environ, HZ_DEC_PIPE=pipe)
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "x.compressed"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
+
+
 def test_cli_exit_codes(hz, tmp_path):
     a = os.path.join(hz.BIN_DIR, "archive")
     e = os.path.join(hz.BIN_DIR, "extract")
