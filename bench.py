@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 rehearsal on one GPU: every rank on cuda:0, gloo collectives through host copies")
     return ap.parse_args()
 
 
@@ -92,9 +94,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def all_reduce(t, op=None):
+        op = dist.ReduceOp.SUM if op is None else op
+        if not args.rehearse:
+            dist.all_reduce(t, op=op)
+            return
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+
+    def all_gather(out, inp):
+        if not args.rehearse:
+            dist.all_gather_into_tensor(out, inp)
+            return
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, inp.cpu())
+        out.copy_(torch.cat(parts))
 
     from huffman_amd.codec import build_codebook, payload_bits
     from huffman_amd.pipeline import StreamCodec
@@ -120,14 +144,14 @@ def main():
         codec.histogram(x)
         if world > 1:
             hist_local.copy_(codec.hist)
-            dist.all_reduce(codec.hist)
+            all_reduce(codec.hist)
         h = codec.hist.cpu().numpy().view(np.uint64)
         hl = hist_local.cpu().numpy().view(np.uint64) if world > 1 else h
         cb = build_codebook(h)
         offset = 0
         if world > 1:
             mine = torch.tensor([payload_bits(cb, hl)], dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(tbits, mine)
+            all_gather(tbits, mine)
             offset = int(tbits[:rank].sum().item())
         last = 0  # N is even for every shard here
         plan = codec.make_plan(h, n_total, hist_local=hl, first_shard=(rank == 0), shard_bit_offset=offset,
@@ -179,7 +203,7 @@ def main():
     C = plan.payload_bits // 8
     if world > 1:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
         ok = bad == 0.0
     ms_step = elapsed / args.steps * 1e3
