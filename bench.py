@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-reassemble", action="store_true", help="N>1: skip the (untimed-in-step) stream reassembly")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on one GPU: every rank on cuda:0, gloo collectives through host copies")
     return ap.parse_args()
@@ -83,6 +84,45 @@ def cpu_baseline(sample_bytes, kind):
         "encode_GBps": round(sample_bytes / enc_s / 1e9, 5),
         "decode_GBps": round(sample_bytes / dec_s / 1e9, 5),
     }
+
+
+def reassemble(codec, plan, payload, rank, world, n_total, kind, args, dev):
+    """SURVEY.md 8(e) step 7, outside the timed step: every rank's shard of the
+    payload lands in ONE stream on rank 0 (RCCL point-to-point over xGMI).
+    Timed on its own; when the stream is small enough, rank 0 decodes it whole
+    (index rebuilt from the stream alone) and checks it against the input."""
+    import torch
+    import torch.distributed as dist
+    from huffman_amd import dist as hd
+    from huffman_amd import index_bytes
+    offset = plan.stream_bit - plan.header_bits % 8
+    word0, _, _ = hd.local_geometry(plan.header_bits, offset, plan.payload_bits, rank == 0)
+    nbytes = (plan.start_bit + plan.payload_bits + 7) // 8
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stream, total = hd.reassemble_on_device(payload, nbytes, word0, dst=0, via_host=args.rehearse)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    dist.barrier()
+    res = None
+    if rank == 0:
+        res = {"ms": round(ms, 3), "stream_bytes": int(total), "GBps_into_rank0": round(total / ms / 1e6, 1),
+               "transport": "gloo via host (rehearsal)" if args.rehearse else "RCCL isend/irecv"}
+        if n_total <= (8 << 30):
+            nsym = n_total // 2
+            idx = torch.empty((index_bytes(nsym) + 7) // 8 + 1, dtype=torch.int64, device=dev)
+            codec.dev.index_build(stream.data_ptr(), stream.numel(), plan.header_bits % 8, nsym, idx.data_ptr())
+            got = torch.empty(n_total + 16, dtype=torch.uint8, device=dev)
+            codec.decode(stream, nsym, idx, got)
+            ref = torch.empty(n_total, dtype=torch.uint8, device=dev)
+            codec.dev.generate(ref.data_ptr(), n_total, offset=0, kind=kind, alpha=1.1, seed=42)
+            codec.sync()
+            res["whole_stream_decoded_bit_exact"] = bool(torch.equal(got[:n_total], ref))
+            del idx, got, ref
+        del stream
+    dist.barrier()
+    return res
 
 
 def main():
@@ -200,6 +240,9 @@ def main():
     index_build = {"ms": round(codec.dev.kernel_ms(STAGE_INDEX), 3),
                    "matches_pack_index": bool(torch.equal(rebuilt[:nidx], state["index"][:nidx]))}
     del rebuilt
+    reassembly = None
+    if world > 1 and not args.no_reassemble:
+        reassembly = reassemble(codec, plan, state["payload"], rank, world, n_total, kind, args, dev)
     C = plan.payload_bits // 8
     if world > 1:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
@@ -263,6 +306,7 @@ def main():
             "host_decode_tables_ms_overlapped": round(float(np.mean(host_dec_ms)), 3),
             "encode_GBps_kernels": round(N / (enc_ms / 1e3) / 1e9, 1),
             "decode_GBps_kernel": round(N / (avg["decode"] / 1e3) / 1e9, 1),
+            "reassembly_outside_step": reassembly,
             "roofline": {
                 "kernel": dom,
                 "bound": "hbm",

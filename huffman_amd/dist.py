@@ -89,3 +89,73 @@ def gather_to(payload, nbytes_local, dst=0, group=None):
     if bufs is None:
         return None
     return [b[:int(s)].cpu().numpy() for b, s in zip(bufs, sizes)]
+
+
+def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_host=False):
+    """gather every shard's word-aligned payload buffer
+    into ONE payload stream on rank `dst`, on the device.
+
+    payload: uint8 CUDA tensor of this shard (word 0 = global payload word `word0`);
+    local_bytes: its bytes that hold bits. Shard bodies (bytes [4, n)) land in
+    place by point-to-point receives (RCCL over xGMI, all posted at once); the
+    shards' first words, which share bits with the previous shard's last word,
+    are ORed in afterwards. via_host: the same exchange through host copies
+    (gloo; bench.py --rehearse on one GPU). Returns the stream tensor on dst
+    (None elsewhere) and the stream's byte count."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = payload.device
+    mine = torch.tensor([local_bytes, word0], dtype=torch.int64)
+    if via_host:
+        parts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        meta = torch.stack(parts)
+    else:
+        meta = torch.zeros(world, 2, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(meta.view(-1), mine.to(dev), group=group)
+        meta = meta.cpu()
+    nb = [int(v) for v in meta[:, 0]]
+    w0 = [int(v) for v in meta[:, 1]]
+    total = max(4 * w + n for w, n in zip(w0, nb))
+    head_n = [min(4, n) for n in nb]
+    if rank != dst:
+        if via_host:
+            if nb[rank] > 4:
+                dist.send(payload[4:nb[rank]].cpu(), dst, group=group)
+            dist.send(payload[:4].cpu(), dst, group=group)
+        else:
+            ops = [dist.P2POp(dist.isend, payload[:4], dst, group=group)]
+            if nb[rank] > 4:
+                ops.append(dist.P2POp(dist.isend, payload[4:nb[rank]], dst, group=group))
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+        return None, total
+    out = torch.zeros((total + 3) // 4 * 4, dtype=torch.uint8, device=dev)
+    heads = torch.zeros(world, 4, dtype=torch.uint8, device=dev)
+    ops = []
+    for r in range(world):
+        body = out[4 * w0[r] + 4:4 * w0[r] + nb[r]] if nb[r] > 4 else None
+        if r == dst:
+            heads[r] = payload[:4]
+            if body is not None:
+                body.copy_(payload[4:nb[r]])
+        elif via_host:
+            if body is not None:
+                tmp = torch.empty(body.numel(), dtype=torch.uint8)
+                dist.recv(tmp, r, group=group)
+                body.copy_(tmp)
+            tmp = torch.empty(4, dtype=torch.uint8)
+            dist.recv(tmp, r, group=group)
+            heads[r] = tmp
+        else:
+            ops.append(dist.P2POp(dist.irecv, heads[r], r, group=group))
+            if body is not None:
+                ops.append(dist.P2POp(dist.irecv, body, r, group=group))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    for r in range(world):  # after every body: heads OR into the previous shard's last word
+        if head_n[r]:
+            seg = out[4 * w0[r]:4 * w0[r] + head_n[r]]
+            seg.bitwise_or_(heads[r, :head_n[r]])
+    return out, total

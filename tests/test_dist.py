@@ -48,13 +48,16 @@ def _worker(rank, world, port, n_total, kind, result_path):
             header, pend_bits, pend = huffman_amd.write_header(cb, n_total, int(data[-1]) if n_total % 2 else 0)
             buf[0] |= pend
         nbytes = (start + pbits + 7) // 8
+        # the device-side reassembly's exchange (bench.py N > 1), through host copies here
+        stream, total = hd.reassemble_on_device(torch.from_numpy(buf.copy()), nbytes, word0, dst=0, via_host=True)
         shards = hd.gather_to(torch.from_numpy(buf), nbytes, dst=0)
         if rank == 0:
             # every shard's global word offset from the gathered totals
             word0s = [hd.local_geometry(hb, sum(totals[:g]), totals[g], g == 0)[0] for g in range(world)]
             payload = hd.reassemble(shards, word0s, sum(totals), hb)
             blob = header + payload.tobytes()
-            ok = blob == oracle_lib.encode(data)
+            ref = oracle_lib.encode(data)
+            ok = blob == ref and total == len(ref) - len(header) and header + stream[:total].numpy().tobytes() == ref
             with open(result_path, "w") as f:
                 f.write("ok" if ok else "mismatch")
     finally:
