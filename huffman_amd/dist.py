@@ -91,6 +91,17 @@ def gather_to(payload, nbytes_local, dst=0, group=None):
     return [b[:int(s)].cpu().numpy() for b, s in zip(bufs, sizes)]
 
 
+_P2P_CHUNK = 1 << 30  # bytes per point-to-point message
+
+
+def _chunks(a, b):
+    """[a, b) in messages of at most _P2P_CHUNK bytes (the same split on both sides)."""
+    while a < b:
+        e = min(b, a + _P2P_CHUNK)
+        yield a, e
+        a = e
+
+
 def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_host=False):
     """gather every shard's word-aligned payload buffer
     into ONE payload stream on rank `dst`, on the device.
@@ -125,8 +136,8 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
             dist.send(payload[:4].cpu(), dst, group=group)
         else:
             ops = [dist.P2POp(dist.isend, payload[:4], dst, group=group)]
-            if nb[rank] > 4:
-                ops.append(dist.P2POp(dist.isend, payload[4:nb[rank]], dst, group=group))
+            for a, b in _chunks(4, nb[rank]):
+                ops.append(dist.P2POp(dist.isend, payload[a:b], dst, group=group))
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
         return None, total
@@ -149,8 +160,8 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
             heads[r] = tmp
         else:
             ops.append(dist.P2POp(dist.irecv, heads[r], r, group=group))
-            if body is not None:
-                ops.append(dist.P2POp(dist.irecv, body, r, group=group))
+            for a, b in _chunks(4, nb[r]):
+                ops.append(dist.P2POp(dist.irecv, out[4 * w0[r] + a:4 * w0[r] + b], r, group=group))
     if ops:
         for q in dist.batch_isend_irecv(ops):
             q.wait()

@@ -50,6 +50,11 @@ def _worker(rank, world, port, n_total, kind, result_path):
         nbytes = (start + pbits + 7) // 8
         # the device-side reassembly's exchange (bench.py N > 1), through host copies here
         stream, total = hd.reassemble_on_device(torch.from_numpy(buf.copy()), nbytes, word0, dst=0, via_host=True)
+        # the RCCL code path (batched isend/irecv into views of the stream), here over gloo on CPU tensors
+        hd._P2P_CHUNK = 4096  # several messages per shard
+        stream2, total2 = hd.reassemble_on_device(torch.from_numpy(buf.copy()), nbytes, word0, dst=0)
+        if rank == 0:
+            assert total2 == total and torch.equal(stream2, stream)
         shards = hd.gather_to(torch.from_numpy(buf), nbytes, dst=0)
         if rank == 0:
             # every shard's global word offset from the gathered totals
