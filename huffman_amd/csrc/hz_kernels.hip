@@ -1248,6 +1248,40 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
     r1.gi = (eb >> 31) ? 0u : (eb & 0x3ffffffu) + ((Wb << Db) >> (32 - gb));
 }
 
+// The LDS steps of NC chains at once (dec_pipe_lds2 generalised): all window
+// reads, then all level-1 reads, then all LDS-second-level reads in flight
+// together, so NC chain steps cost three LDS round trips.
+template <int NC>
+HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, const uint32_t* pos,
+                          PipeLane* r) {
+    const uint32_t k = (uint32_t)a.k;
+    uint32_t W[NC], e[NC], x[NC], D[NC];
+    bool h[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t p1 = pos[c] - 1u;  // >= 127 (staging pad)
+        const uint32_t* w = stg + (p1 >> 5);
+        W[c] = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) e[c] = lds[W[c] >> (32 - k)];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        h[c] = (e[c] >> 30) == 1u;
+        const uint32_t nb = (e[c] >> 26) & 15u;
+        const uint32_t i = h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u;
+        D[c] = h[c] ? k + nb : k;
+        x[c] = lds[i];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t ee = h[c] ? x[c] : e[c];
+        const uint32_t g = (ee >> 26) & 15u;
+        r[c].e = ee;
+        r[c].gi = (ee >> 31) ? 0u : (ee & 0x3ffffffu) + ((W[c] << D[c]) >> (32 - g));
+    }
+}
+
 // Block metadata of the pipelined decoder: start and end bit, the lane's chain offsets.
 struct PipeMeta {
     uint64_t b0, b1, sub;
@@ -1321,6 +1355,9 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
 #endif
 #ifndef HZ_PIPE_PAIR
 #define HZ_PIPE_PAIR 1
+#endif
+#ifndef HZ_DEC_QUAD
+#define HZ_DEC_QUAD 1
 #endif
 // Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
 // staging chunks of the next block and the metadata of the one after are
@@ -1467,6 +1504,30 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             if (q & 1) pk[c / kChainsPerLane][i] |= sym << 16;
             else pk[c / kChainsPerLane][i] = sym;
         };
+#if HZ_DEC_QUAD
+        // two quads (one per block): a quad's gathers land behind the other quad's walk
+        auto issue4 = [&](int c) {
+            dec_pipe_ldsn<4>(a, lds, stg, pos + c, st + c);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) g[c + t] = a.l2[st[c + t].gi];
+        };
+        issue4(0);
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+            issue4(4);
+            if (q == HZ_PF_STEP) {  // the next two blocks' staging chunks, the metadata after them
+#pragma unroll
+                for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) dec_meta_load(a, b + 2 * stride + j, lane, mn2[j]);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) finish(c, q);
+            if (q + 1 < kChainSyms) issue4(0);
+#pragma unroll
+            for (int c = 4; c < 8; ++c) finish(c, q);
+        }
+#else
         auto issue2 = [&](int c) {
             dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
             g[c] = a.l2[st[c].gi];
@@ -1493,6 +1554,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             finish(6, q);
             finish(7, q);
         }
+#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -1507,9 +1569,13 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
     }
 }
 
+#ifndef HZ_DEC_P2_THREADS
+#define HZ_DEC_P2_THREADS 512
+#endif
+constexpr int kDecPipe2Threads = HZ_DEC_P2_THREADS;  // two staging slots per wave
 // PIPE: 0 plain block loop, 1 pipelined (one block per wave), 2 pipelined, two blocks per wave
 template <int MODE, bool WIDE, int PIPE>
-__global__ __launch_bounds__(PIPE == 2 ? 512 : 1024) void k_decode(DecArgs a) {
+__global__ __launch_bounds__(PIPE == 2 ? kDecPipe2Threads : 1024) void k_decode(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
@@ -1633,7 +1699,8 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
         const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
         if (room <= table + est) continue;
         int w = (int)((room - table) / est);
-        w = w > kDecMaxWaves ? kDecMaxWaves : w;
+        const int maxw = PIPE == 2 ? 2 * kDecPipe2Threads / 64 : kDecMaxWaves;  // slots
+        w = w > maxw ? maxw : w;
         if (g * w > best_g * best_w) { best_w = w; best_g = g; }
     }
     if (best_w == 0) return hipErrorInvalidValue;
@@ -1646,8 +1713,10 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
     uint64_t wgs = (a.nblocks + best_w - 1) / best_w;
     const uint64_t cap = (uint64_t)ncu * best_g;
     if (wgs > cap) wgs = cap;
-    // PIPE 2: a wave takes two slots (at most 8 waves, up to 256 VGPRs each)
-    const int threads = PIPE == 2 ? (64 * best_w < 512 ? 64 * best_w : 512) : 64 * best_w;
+    // PIPE 2: a wave takes two slots
+    const int threads = PIPE == 2 ? (64 * ((best_w + 1) / 2) < kDecPipe2Threads ? 64 * ((best_w + 1) / 2)
+                                                                                 : kDecPipe2Threads)
+                                  : 64 * best_w;
     hipLaunchKernelGGL((k_decode<MODE, WIDE, PIPE>), dim3(wgs), dim3(threads), lds, s, b);
     return hipGetLastError();
 }
