@@ -1781,22 +1781,52 @@ constexpr uint32_t kSegBits = 4096;
 constexpr int kSyncThreads = 1024;
 constexpr uint32_t kSegWords = kSegBits / 32;
 
+// Per-lane bit reader over the payload. Words come from 16-byte chunks with
+// the next chunk always in flight (128 bits of lookahead, a quarter of the
+// load instructions of word reads); past the payload it reads zeros.
 struct BitReader {
     uint64_t buf;
     uint32_t nb;
     uint32_t nxt;
-    uint64_t wpos;  // index of the word after nxt
+    uint4 cur, ahead;   // current chunk (raw words), the next one (in flight)
+    uint32_t ci;        // next word of cur
+    uint64_t abase;     // word index of `ahead`
 };
 
-HZ_DEV uint32_t ld_word(const DecArgs& a, uint64_t w) { return w < a.nwords ? bswap32(a.words[w]) : 0u; }
+HZ_DEV uint4 ld_chunk(const DecArgs& a, uint64_t w) {  // w % 4 == 0
+    if (w + 4 <= a.nwords) return *reinterpret_cast<const uint4*>(a.words + w);
+    uint4 v;
+    v.x = w < a.nwords ? a.words[w] : 0u;
+    v.y = w + 1 < a.nwords ? a.words[w + 1] : 0u;
+    v.z = w + 2 < a.nwords ? a.words[w + 2] : 0u;
+    v.w = 0u;
+    return v;
+}
+
+HZ_DEV uint32_t br_word(BitReader& r, const DecArgs& a) {
+    const uint32_t v = pick4(r.cur, r.ci);
+    if (++r.ci == 4) {
+        r.cur = r.ahead;
+        r.ci = 0;
+        r.abase += 4;
+        r.ahead = ld_chunk(a, r.abase);
+    }
+    return bswap32(v);
+}
 
 HZ_DEV void br_init(BitReader& r, const DecArgs& a, uint64_t p) {
     const uint64_t w = p >> 5;
     const uint32_t sh = (uint32_t)(p & 31);
-    r.buf = (((uint64_t)ld_word(a, w) << 32) | ld_word(a, w + 1)) << sh;
+    const uint64_t base = w & ~3ull;
+    r.cur = ld_chunk(a, base);
+    r.abase = base + 4;
+    r.ahead = ld_chunk(a, r.abase);
+    r.ci = (uint32_t)(w & 3);
+    const uint32_t w0 = br_word(r, a);
+    const uint32_t w1 = br_word(r, a);
+    r.buf = (((uint64_t)w0 << 32) | w1) << sh;
     r.nb = 64 - sh;
-    r.nxt = ld_word(a, w + 2);
-    r.wpos = w + 3;
+    r.nxt = br_word(r, a);
 }
 
 // Length (and symbol) of the codeword at the reader, then advance past it.
@@ -1805,7 +1835,7 @@ HZ_DEV uint32_t br_next(BitReader& r, const DecArgs& a, const uint32_t* lds, uin
     if (r.nb <= 32) {
         r.buf |= (uint64_t)r.nxt << (32 - r.nb);
         r.nb += 32;
-        r.nxt = ld_word(a, r.wpos++);
+        r.nxt = br_word(r, a);
     }
     const uint64_t win = r.nb >= 56 ? r.buf : (r.buf | ((uint64_t)r.nxt >> (r.nb - 32)));
     uint32_t L;
@@ -1817,7 +1847,7 @@ HZ_DEV uint32_t br_next(BitReader& r, const DecArgs& a, const uint32_t* lds, uin
         const uint32_t rr = L - r.nb;
         r.buf = (uint64_t)r.nxt << (32 + rr);
         r.nb = 32 - rr;
-        r.nxt = ld_word(a, r.wpos++);
+        r.nxt = br_word(r, a);
     }
     return L;
 }
@@ -1841,14 +1871,27 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
-        uint32_t* bm = y.bmp + k * kSegWords;
+        // bitmap words leave four at a time (16-byte stores): every store is a
+        // vmcnt entry that later load waits queue behind
+        uint4* bm = reinterpret_cast<uint4*>(y.bmp + k * kSegWords);
         BitReader r;
         br_init(r, a, s0 + a.bit_adj);
         uint64_t pos = s0, n = 0;
         uint32_t cw = 0, cur = 0;  // bitmap word being filled
+        uint4 q = make_uint4(0, 0, 0, 0);
+        auto put = [&]() {
+            const uint32_t j = cw & 3;
+            q.x = j == 0 ? cur : q.x;
+            q.y = j == 1 ? cur : q.y;
+            q.z = j == 2 ? cur : q.z;
+            q.w = j == 3 ? cur : q.w;
+            if (j == 3) bm[cw >> 2] = q;
+            cur = 0;
+            ++cw;
+        };
         while (pos < s1) {
             const uint32_t d = (uint32_t)(pos - s0);
-            while ((d >> 5) != cw) { bm[cw++] = cur; cur = 0; }
+            while ((d >> 5) != cw) put();
             cur |= 1u << (d & 31);
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
@@ -1856,7 +1899,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
             pos += L;
             ++n;
         }
-        for (; cw < kSegWords; ++cw) { bm[cw] = cur; cur = 0; }
+        while (cw < kSegWords) put();
         y.exit0[k] = pos;
         y.cnt0[k] = n;
     }
@@ -1926,15 +1969,39 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_emit(DecArgs a, SyncArgs 
         uint64_t pos = k ? exits[k - 1] : y.start;
         BitReader r;
         br_init(r, a, pos + a.bit_adj);
+        // chain positions leave four at a time (8-byte stores) when this lane
+        // wrote the whole group of four; a group split with a neighbouring
+        // segment is flushed slot by slot
+        uint64_t acc = 0, g = ~0ull;
+        uint32_t have = 0;
+        auto flush = [&]() {
+            for (uint32_t t = 0; t < 4; ++t)
+                if (have & (1u << t)) subs[4 * g + t] = (uint16_t)(acc >> (16 * t));
+            have = 0;
+        };
         while (pos < s1 && i < a.nsym) {
             if (i % kBlockSyms == 0) starts[i / kBlockSyms] = pos;
-            if (i % kChainSyms == 0) subs[i / kChainSyms] = (uint16_t)pos;
+            if (i % kChainSyms == 0) {
+                const uint64_t c = i / kChainSyms;
+                if ((c >> 2) != g) {
+                    flush();
+                    g = c >> 2;
+                    acc = 0;
+                }
+                acc |= (uint64_t)(uint16_t)pos << (16 * (c & 3));
+                have |= 1u << (c & 3);
+                if (have == 15u) {
+                    reinterpret_cast<uint64_t*>(subs)[g] = acc;
+                    have = 0;
+                }
+            }
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
             pos += L;
             ++i;
         }
+        flush();
         if (i == a.nsym) starts[a.nblocks] = pos;
     }
 }
@@ -2041,6 +2108,7 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.ex[1] = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     unsigned long long* first = p; p += y.nseg;
+    p += (reinterpret_cast<uintptr_t>(p) >> 3) & 1;  // 16-byte aligned bitmap rows (uint4 stores)
     y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kSegWords / 2);
     y.dirty[0] = reinterpret_cast<uint32_t*>(p);
     y.dirty[1] = y.dirty[0] + y.nseg;
