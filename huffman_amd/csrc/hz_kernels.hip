@@ -1779,7 +1779,11 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
 // ===========================================================================
 constexpr uint32_t kSegBits = 4096;
 constexpr int kSyncThreads = 1024;
-constexpr uint32_t kSegWords = kSegBits / 32;
+// The scan keeps the boundary bitmap of a segment's first kBmpBits only: the
+// true path lands on a scan-path boundary after a median 81 bits (p99 600,
+// Zipf); one that has not within the prefix walks on to the segment's end.
+constexpr uint32_t kBmpBits = 1024;
+constexpr uint32_t kBmpWords = kBmpBits / 32;
 
 // Per-lane bit reader over the payload. Words come from 16-byte chunks with
 // the next chunk always in flight (128 bits of lookahead, a quarter of the
@@ -1857,7 +1861,7 @@ struct SyncArgs {
     uint64_t nseg;
     unsigned long long* exit0;      // scan path: first boundary >= segment end
     unsigned long long* cnt0;       // scan path: codewords inside the segment
-    uint32_t* bmp;                  // scan path: boundaries, kSegWords per segment
+    uint32_t* bmp;                  // scan path: boundaries in the first kBmpBits, kBmpWords per segment
     unsigned long long* ex[2];      // true exits, ping-pong between iterations
     unsigned long long* cnt;        // true counts
     uint32_t* dirty[2];             // entry changed in the previous iteration
@@ -1873,7 +1877,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
         // bitmap words leave four at a time (16-byte stores): every store is a
         // vmcnt entry that later load waits queue behind
-        uint4* bm = reinterpret_cast<uint4*>(y.bmp + k * kSegWords);
+        uint4* bm = reinterpret_cast<uint4*>(y.bmp + k * kBmpWords);
         BitReader r;
         br_init(r, a, s0 + a.bit_adj);
         uint64_t pos = s0, n = 0;
@@ -1891,15 +1895,17 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
         };
         while (pos < s1) {
             const uint32_t d = (uint32_t)(pos - s0);
-            while ((d >> 5) != cw) put();
-            cur |= 1u << (d & 31);
+            if (cw < kBmpWords) {
+                while ((d >> 5) != cw && cw < kBmpWords) put();
+                cur |= 1u << (d & 31);  // past the prefix: never stored
+            }
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
             pos += L;
             ++n;
         }
-        while (cw < kSegWords) put();
+        while (cw < kBmpWords) put();
         y.exit0[k] = pos;
         y.cnt0[k] = n;
     }
@@ -1918,7 +1924,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs 
         if (k == 0) { if (it == 0) { exw[0] = y.exit0[0]; y.cnt[0] = y.cnt0[0]; } else exw[0] = exr[0]; continue; }
         if (it > 0 && !dr[k]) { exw[k] = exr[k]; continue; }
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
-        const uint32_t* bm = y.bmp + k * kSegWords;
+        const uint32_t* bm = y.bmp + k * kBmpWords;
         uint64_t p = it == 0 ? y.exit0[k - 1] : exr[k - 1];
         uint64_t walked = 0, ex = 0, n = 0;
         bool landed = false;
@@ -1926,7 +1932,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs 
         br_init(r, a, p + a.bit_adj);
         while (p < s1) {
             const uint32_t d = (uint32_t)(p - s0);
-            if ((bm[d >> 5] >> (d & 31)) & 1u) { landed = true; break; }
+            if (d < kBmpBits && ((bm[d >> 5] >> (d & 31)) & 1u)) { landed = true; break; }
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
@@ -2035,8 +2041,8 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // exit0, cnt0, ex[2], cnt, first (u64), bitmap (kSegWords u32), dirty[2] (u32), counter, tiles
-    return nseg * (6 + kSegWords / 2 + 1) + 1 + ntiles + 8;
+    // exit0, cnt0, ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
+    return nseg * (6 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
 }
 
 template <int MODE>
@@ -2109,7 +2115,7 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.cnt = p; p += y.nseg;
     unsigned long long* first = p; p += y.nseg;
     p += (reinterpret_cast<uintptr_t>(p) >> 3) & 1;  // 16-byte aligned bitmap rows (uint4 stores)
-    y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kSegWords / 2);
+    y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kBmpWords / 2);
     y.dirty[0] = reinterpret_cast<uint32_t*>(p);
     y.dirty[1] = y.dirty[0] + y.nseg;
     p += y.nseg;
