@@ -1911,6 +1911,186 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
     }
 }
 
+// Two segments per lane in lockstep (codebooks the pipelined decoder takes:
+// codes <= 32 bits, every global lookup a leaf): both streams' LUT walks and
+// gathers are in flight together, so one stream's lookup latency hides the
+// other's. Same outputs as the one-segment kernels.
+HZ_DEV void br_refill(BitReader& r, const DecArgs& a) {
+    if (r.nb <= 32) {
+        r.buf |= (uint64_t)r.nxt << (32 - r.nb);
+        r.nb += 32;
+        r.nxt = br_word(r, a);
+    }
+}
+
+// Lengths of the codewords at two readers (top 32 bits of each window).
+HZ_DEV void lut_len2(const DecArgs& a, const uint32_t* lds, const BitReader (&r)[2], uint32_t (&L)[2]) {
+    const uint32_t k = (uint32_t)a.k;
+    uint32_t W[2], e[2], x[2], D[2], gi[2];
+    bool h[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) W[c] = (uint32_t)(r[c].buf >> 32);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) e[c] = lds[W[c] >> (32 - k)];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        h[c] = (e[c] >> 30) == 1u;
+        const uint32_t nb = (e[c] >> 26) & 15u;
+        const uint32_t i = h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u;
+        D[c] = h[c] ? k + nb : k;
+        x[c] = lds[i];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        e[c] = h[c] ? x[c] : e[c];
+        const uint32_t g = (e[c] >> 26) & 15u;
+        gi[c] = (e[c] >> 31) ? 0u : (e[c] & 0x3ffffffu) + ((W[c] << D[c]) >> (32 - g));
+    }
+    const uint32_t g0 = a.l2[gi[0]], g1 = a.l2[gi[1]];
+    L[0] = (((e[0] >> 31) ? e[0] : g0) >> 16) & 63u;
+    L[1] = (((e[1] >> 31) ? e[1] : g1) >> 16) & 63u;
+}
+
+__global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k0 < y.nseg; k0 += 2 * stride) {
+        BitReader r[2];
+        uint64_t s0[2], pos[2], n[2];
+        uint32_t cw[2], cur[2];
+        uint4 q[2];
+        bool act[2];
+        uint4* bm[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint64_t k = k0 + c * stride;
+            act[c] = k < y.nseg;
+            s0[c] = y.start + (act[c] ? k : k0) * kSegBits;
+            pos[c] = s0[c];
+            n[c] = 0;
+            cw[c] = cur[c] = 0;
+            q[c] = make_uint4(0, 0, 0, 0);
+            bm[c] = reinterpret_cast<uint4*>(y.bmp + (act[c] ? k : k0) * kBmpWords);
+            br_init(r[c], a, s0[c] + a.bit_adj);
+        }
+        auto put = [&](int c) {
+            const uint32_t j = cw[c] & 3;
+            q[c].x = j == 0 ? cur[c] : q[c].x;
+            q[c].y = j == 1 ? cur[c] : q[c].y;
+            q[c].z = j == 2 ? cur[c] : q[c].z;
+            q[c].w = j == 3 ? cur[c] : q[c].w;
+            if (j == 3) bm[c][cw[c] >> 2] = q[c];
+            cur[c] = 0;
+            ++cw[c];
+        };
+        while (act[0] || act[1]) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (act[c] && cw[c] < kBmpWords) {
+                    const uint32_t d = (uint32_t)(pos[c] - s0[c]);
+                    while ((d >> 5) != cw[c] && cw[c] < kBmpWords) put(c);
+                    cur[c] |= 1u << (d & 31);
+                }
+                br_refill(r[c], a);
+            }
+            uint32_t L[2];
+            lut_len2(a, lds, r, L);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (!act[c]) continue;
+                if (L[c] == 0) { atomicOr(a.err, 2u); act[c] = false; continue; }
+                r[c].buf <<= L[c];
+                r[c].nb -= L[c];
+                pos[c] += L[c];
+                ++n[c];
+                act[c] = pos[c] < s0[c] + kSegBits;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint64_t k = k0 + c * stride;
+            if (k >= y.nseg) continue;
+            while (cw[c] < kBmpWords) put(c);
+            y.exit0[k] = pos[c];
+            y.cnt0[k] = n[c];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSyncThreads) void k_sync_emit2(DecArgs a, SyncArgs y, const unsigned long long* exits,
+                                                  const unsigned long long* first, unsigned long long* starts,
+                                                  uint16_t* subs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k0 < y.nseg; k0 += 2 * stride) {
+        BitReader r[2];
+        uint64_t i[2], pos[2], s1[2], acc[2], g[2];
+        uint32_t have[2];
+        bool act[2], live[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint64_t k = k0 + c * stride;
+            const uint64_t kk = k < y.nseg ? k : k0;
+            i[c] = first[kk];
+            act[c] = live[c] = k < y.nseg && i[c] < a.nsym;
+            s1[c] = y.start + (kk + 1) * kSegBits;
+            pos[c] = kk ? exits[kk - 1] : y.start;
+            acc[c] = 0;
+            g[c] = ~0ull;
+            have[c] = 0;
+            br_init(r[c], a, pos[c] + a.bit_adj);
+        }
+        auto flush = [&](int c) {
+            for (uint32_t t = 0; t < 4; ++t)
+                if (have[c] & (1u << t)) subs[4 * g[c] + t] = (uint16_t)(acc[c] >> (16 * t));
+            have[c] = 0;
+        };
+        while (act[0] || act[1]) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (act[c]) {
+                    if (i[c] % kBlockSyms == 0) starts[i[c] / kBlockSyms] = pos[c];
+                    if (i[c] % kChainSyms == 0) {
+                        const uint64_t ch = i[c] / kChainSyms;
+                        if ((ch >> 2) != g[c]) {
+                            flush(c);
+                            g[c] = ch >> 2;
+                            acc[c] = 0;
+                        }
+                        acc[c] |= (uint64_t)(uint16_t)pos[c] << (16 * (ch & 3));
+                        have[c] |= 1u << (ch & 3);
+                        if (have[c] == 15u) {
+                            reinterpret_cast<uint64_t*>(subs)[g[c]] = acc[c];
+                            have[c] = 0;
+                        }
+                    }
+                }
+                br_refill(r[c], a);
+            }
+            uint32_t L[2];
+            lut_len2(a, lds, r, L);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (!act[c]) continue;
+                if (L[c] == 0) { atomicOr(a.err, 2u); act[c] = false; continue; }
+                r[c].buf <<= L[c];
+                r[c].nb -= L[c];
+                pos[c] += L[c];
+                ++i[c];
+                act[c] = pos[c] < s1[c] && i[c] < a.nsym;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (!live[c]) continue;
+            flush(c);
+            if (i[c] == a.nsym) starts[a.nblocks] = pos[c];
+        }
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -2062,7 +2242,21 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     uint64_t wgs = (y.nseg + kSyncThreads - 1) / kSyncThreads;
     const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 2 ? 1 : 2) : 2);
     wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
-    hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
+    // two segments per lane where the pipelined decoder's table shape holds
+    static const int two_env = [] { const char* v = getenv("HZ_SYNC_TWO"); return v ? atoi(v) : 1; }();
+    const bool two = two_env && MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + kDecLevelBits;
+    static bool attr2 = false;
+    if (two && !attr2) {
+        for (const void* f : {(const void*)k_sync_scan2, (const void*)k_sync_emit2}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            if (e != hipSuccess) return e;
+        }
+        attr2 = true;
+    }
+    if (two)
+        hipLaunchKernelGGL(k_sync_scan2, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
+    else
+        hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
     // resolve entries until no exit changes (host loop; typically 1-3 passes)
     int it = 0;
     for (;; ++it) {
@@ -2085,8 +2279,12 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     // end bit = all ones unless the payload holds nsym codewords (k_sync_emit writes it then)
     hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits, (const unsigned long long*)first,
-                       d_index, subs);
+    if (two)
+        hipLaunchKernelGGL(k_sync_emit2, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits,
+                           (const unsigned long long*)first, d_index, subs);
+    else
+        hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits,
+                           (const unsigned long long*)first, d_index, subs);
     e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
     if (e != hipSuccess) return e;
     uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
