@@ -508,7 +508,11 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
 #ifndef HZ_PACK_THREADS
 #define HZ_PACK_THREADS 512
 #endif
-constexpr int kPackWriteThreads = HZ_PACK_THREADS;  // <= 8 waves: room for a block of registers in flight per lane
+constexpr int kPackWriteThreads = HZ_PACK_THREADS;
+#ifndef HZ_PACK_STATIC_COPY
+#define HZ_PACK_STATIC_COPY 1
+#endif
+constexpr int kPackCopyIters = 16;  // slot copy-out: 16 x 64 words covers a 1024-word slot  // <= 8 waves: room for a block of registers in flight per lane
 
 // One block of a wave between its lookup and its emit: the lane's 32 entries,
 // the entry of one of the previous block's last 32 symbols, the lane's bits,
@@ -600,8 +604,21 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
         const uint32_t h = (uint32_t)(o & 31);
         if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
         __builtin_amdgcn_wave_barrier();
-        if (fits)
+        if (fits) {
+#if HZ_PACK_STATIC_COPY
+            if constexpr (MODE != ENC_WIDE) {  // host: slot_words <= kPackCopyIters * kWave
+                // a fixed count of full-wave stores (lanes past the block rewrite its last
+                // word with the same value), so later load waits count them statically
+#pragma unroll
+                for (int it = 0; it < kPackCopyIters; ++it) {
+                    uint32_t w = (uint32_t)lane + (uint32_t)it * kWave;
+                    w = w < nwords ? w : nwords - 1;
+                    a.out[wfirst + w] = bswap32(slot[w]);
+                }
+            } else
+#endif
             for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+        }
         __builtin_amdgcn_wave_barrier();
     } else {
         // direct path: each lane needs the 32 bits before its run from the
@@ -887,6 +904,8 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     a.slot_words = 0;
     if (waves >= 6) a.slot_words = free_words / waves;
     else waves = kMaxWaves;  // no room for slots: lanes store directly
+    if (t.enc_mode != ENC_WIDE && a.slot_words > (uint32_t)(kPackCopyIters * kWave))
+        a.slot_words = kPackCopyIters * kWave;  // larger blocks take the direct path
     const int threads = (int)waves * 64;
     uint64_t wgs = (nblocks + waves - 1) / waves;
     const uint32_t lds = 4 * (table_words + waves * a.slot_words);
