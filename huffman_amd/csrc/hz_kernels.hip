@@ -254,6 +254,9 @@ hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_
 // Code tables live in LDS (DENSE 17-bit sentinel entries, or HOT tagged
 // slots) and are loaded once per workgroup of a grid-stride kernel.
 // ===========================================================================
+#ifndef HZ_PACK_STATIC_ESC
+#define HZ_PACK_STATIC_ESC 1
+#endif
 struct PackArgs {
     const uint8_t* in;
     uint64_t nsym;
@@ -361,6 +364,24 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
         const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
         xe = (T)xx;
+#if HZ_PACK_STATIC_ESC
+        // Every lane issues all 33 escape loads (lanes without a miss read
+        // esc[0], one coalesced address): a fixed load count keeps the waits
+        // of later loads and stores static. The escape table holds entries in
+        // the register format, so each load lands in its e[k] directly.
+        (void)any;
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            const bool miss = (uint32_t)e[k] >> 31;
+            const uint32_t v = a.esc[miss ? (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu : 0u];
+            e[k] = miss ? (T)v : e[k];
+        }
+        {
+            const bool miss = xx >> 31;
+            const uint32_t v = a.esc[miss ? xs : 0u];
+            xe = miss ? (T)v : xe;
+        }
+#else
         if ((any | xx) >> 31) {
             // The escape table holds entries in the register format, so each
             // load lands in its e[k] directly and the single wait falls at the
@@ -370,6 +391,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
                 if ((uint32_t)e[k] >> 31) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
             if (xx >> 31) xe = (T)a.esc[xs];
         }
+#endif
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
