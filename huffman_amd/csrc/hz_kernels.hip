@@ -727,28 +727,32 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
     if (!fits && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.err, 4u);
     const bool vec_out = (W0 & 3) == 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += stride) {
+    // the lane's 64 input bytes of run j (full runs; 0 past them), loaded one
+    // iteration ahead so a load is always in flight beside the table lookups
+    auto load_run = [&](uint64_t j, uint32_t (&raw)[kSPT / 2]) {
+        const uint64_t ls = j < nl && (j + 1) * kSPT <= a.nsym ? j * kSPT : 0;
+        const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ls);
+#pragma unroll
+        for (int q = 0; q < kSPT / 8; ++q) {
+            const uint4 v = p[q];
+            raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+        }
+    };
+    uint32_t nraw[kSPT / 2];
+    const uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    load_run(j0, nraw);
+    for (uint64_t j = j0; j < nl; j += stride) {  // the loop is uniform except in the last round
         const uint64_t sym0 = j * kSPT;
         const int nvalid = a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0);
         uint32_t raw[kSPT / 2];
-        if (nvalid == kSPT) {
-            const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * sym0);
 #pragma unroll
-            for (int q = 0; q < kSPT / 8; ++q) {
-                const uint4 v = p[q];
-                raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
-            }
-        } else {
+        for (int k = 0; k < kSPT / 2; ++k) raw[k] = nraw[k];
+        load_run(j + stride, nraw);
+        if (nvalid != kSPT) {
 #pragma unroll
             for (int k = 0; k < kSPT / 2; ++k) raw[k] = 0;
             for (int k = 0; k < nvalid; ++k)
                 raw[k >> 1] |= ((uint32_t)a.in[2 * (sym0 + k)] | ((uint32_t)a.in[2 * (sym0 + k) + 1] << 8)) << (16 * (k & 1));
-        }
-        // the previous lane's last code pair (or the header's pending bits)
-        uint32_t prev = a.lead;
-        if (j > 0) {
-            const uint32_t pr = *reinterpret_cast<const uint32_t*>(a.in + 2 * (sym0 - 2));
-            prev = ((uint32_t)c16[pr & 0xffffu] << 16) | c16[pr >> 16];
         }
         uint32_t v[kSPT / 2];
 #pragma unroll
@@ -756,6 +760,14 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
             const uint32_t lo = (uint32_t)c16[raw[t] & 0xffffu], hi = (uint32_t)c16[raw[t] >> 16];
             v[t] = (2 * t < nvalid ? lo << 16 : 0u) | (2 * t + 1 < nvalid ? hi : 0u);
         }
+        // the previous run's last code pair (or the header's pending bits): from
+        // lane - 1 by DPP (run j - 1 when that lane is active in this round), else loaded
+        uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[kSPT / 2 - 1], kDppWaveShr1, 0xf, 0xf, false);
+        if ((threadIdx.x & 63) == 0 && j > 0) {
+            const uint32_t pr = *reinterpret_cast<const uint32_t*>(a.in + 2 * (sym0 - 2));
+            prev = ((uint32_t)c16[pr & 0xffffu] << 16) | c16[pr >> 16];
+        }
+        if (j == 0) prev = a.lead;
         uint32_t o[kSPT / 2];
 #pragma unroll
         for (int t = 0; t < kSPT / 2; ++t) {
