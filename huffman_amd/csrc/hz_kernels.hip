@@ -1304,6 +1304,17 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
 // The LDS steps of NC chains at once (dec_pipe_lds2 generalised): all window
 // reads, then all level-1 reads, then all LDS-second-level reads in flight
 // together, so NC chain steps cost three LDS round trips.
+// Phase fences of the NC-chain walk (build knob): keep each phase's LDS reads
+// issued together whatever the scheduler would do (the decoder is order-sensitive).
+#ifndef HZ_WALK_FENCES
+#define HZ_WALK_FENCES 1
+#endif
+#if HZ_WALK_FENCES
+#define HZ_WALK_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define HZ_WALK_FENCE() ((void)0)
+#endif
+
 template <int NC>
 HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, const uint32_t* pos,
                           PipeLane* r) {
@@ -1316,8 +1327,10 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
         const uint32_t* w = stg + (p1 >> 5);
         W[c] = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
     }
+    HZ_WALK_FENCE();
 #pragma unroll
     for (int c = 0; c < NC; ++c) e[c] = lds[W[c] >> (32 - k)];
+    HZ_WALK_FENCE();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         h[c] = (e[c] >> 30) == 1u;
@@ -1326,6 +1339,7 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
         D[c] = h[c] ? k + nb : k;
         x[c] = lds[i];
     }
+    HZ_WALK_FENCE();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t ee = h[c] ? x[c] : e[c];
