@@ -109,6 +109,9 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 // ===========================================================================
 constexpr int kHistThreads = 1024;
 constexpr int kHistUnroll = 1;
+#ifndef HZ_HIST_SWEEP
+#define HZ_HIST_SWEEP 1  // 1: grid-stride sweep (all workgroups read neighbouring 16 KiB pieces); 0: a chunk per workgroup
+#endif
 
 // LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
 // their low bits (the first byte), which alone would pick the LDS bank: the
@@ -147,11 +150,19 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
     if (VEC) {
         const uint4* in4 = reinterpret_cast<const uint4*>(in);
         const uint64_t nvec = nsym / 8;
+#if HZ_HIST_SWEEP
+        // the whole chip sweeps the input together, as the count pass does
+        static_assert(kHistUnroll == 1, "sweep reads one vector per lane per step");
+        const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+        const uint64_t beg = (uint64_t)blockIdx.x * blockDim.x;
+        const uint64_t end = nvec;
+#else
         const uint64_t step = (uint64_t)blockDim.x * kHistUnroll;
         uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
         per = (per + step - 1) / step * step;
         const uint64_t beg = blockIdx.x * per;
         const uint64_t end = beg + per < nvec ? beg + per : nvec;
+#endif
         // software pipelined: the next iteration's loads are in flight while
         // this one's LDS atomics run (loads and LDS ops use separate counters)
         uint4 nx[kHistUnroll];
