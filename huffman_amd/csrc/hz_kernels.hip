@@ -116,8 +116,19 @@ constexpr int kHistUnroll = 1;
 // LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
 // their low bits (the first byte), which alone would pick the LDS bank: the
 // second byte's low bits are XORed into the bank bits (a bijection).
+#ifndef HZ_HIST_SWZ
+#define HZ_HIST_SWZ 1
+#endif
+#if HZ_HIST_SWZ
+// The second byte times 13 (odd: distinct small bytes land on distinct, spread
+// banks) XORed into word bits 0-5; it depends only on word bits 7-14, which
+// the XOR leaves alone, so the map is a bijection.
+HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ (((s >> 8) * 13u) & 0x3fu); }
+HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ (((w >> 7) * 13u) & 0x3fu); }
+#else
 HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ ((s >> 8) & 0x3fu); }
 HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ ((w >> 7) & 0x3fu); }
+#endif
 
 // Fix-up after `old = atomicAdd(&lds[hist_word(s)], inc)`; rare (once per 65 536 adds of a bin).
 HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old) {
