@@ -51,8 +51,11 @@ enum DecMode : int {
     DEC_LUT = 1,    // 2^K1 u32 level-1 entries in LDS, deeper levels in global
     DEC_FIXED16 = 2 // every code 16 bits: u16 symbol per code in LDS, positions are arithmetic
 };
-constexpr int kDecLutMaxK1 = 14;
-constexpr int kDecLevelBits = 8;
+constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-bit codes
+#ifndef HZ_DEC_LEVEL_BITS
+#define HZ_DEC_LEVEL_BITS 9
+#endif
+constexpr int kDecLevelBits = HZ_DEC_LEVEL_BITS;  // bits per global subtable level
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
