@@ -16,7 +16,7 @@ HZ_MAXLEN = 56
 
 STATUS = {
     0: "HZ_OK", -1: "HZ_EINVAL", -2: "HZ_ENOMEM", -3: "HZ_EHIP", -4: "HZ_ETOOLONG",
-    -5: "HZ_EFORMAT", -6: "HZ_ECAP", -7: "HZ_ETIMEOUT", -8: "HZ_EIO", -9: "HZ_ENODEV",
+    -5: "HZ_EFORMAT", -6: "HZ_ECAP", -7: "HZ_ETIMEOUT", -8: "HZ_EIO", -9: "HZ_ENODEV", -10: "HZ_ENOENT",
 }
 STAGE_HIST, STAGE_PACK, STAGE_DECODE, STAGE_INDEX = 0, 1, 2, 3
 

@@ -1,7 +1,7 @@
 // `extract <file.compressed>` -> ./DECOMPRESSED_FILE, the reference decoder CLI
 // (Decompressor.cu:47-114) with the decode on the gfx950 kernels of
 // libhuffman_amd. Exit codes follow the reference: 1 on usage error, 0 on a
-// missing file (Decompressor.cu:51-63); 2 when the codec itself fails.
+// missing file (Decompressor.cu:51-63); 2 when the codec or any other I/O fails.
 #include <iostream>
 
 #include "huffman_amd.h"
@@ -13,6 +13,6 @@ int main(int argc, char* argv[]) {
         return 1;
     }
     const int rc = hz_extract_file(argv[1], nullptr, 0, 1);
-    if (rc == HZ_EIO || rc == HZ_OK) return 0;
+    if (rc == HZ_ENOENT || rc == HZ_OK) return 0;
     return 2;
 }

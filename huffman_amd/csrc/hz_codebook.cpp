@@ -446,14 +446,13 @@ static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t 
 // weight 2^-L of a code stands in for its frequency, so each global entry of
 // an nb-bit subtable under level 1 carries mass 2^-(K1+nb).
 static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, const std::vector<uint32_t>& l2, int K1) {
-    static const long env = getenv("HZ_DEC_L2LDS") ? atol(getenv("HZ_DEC_L2LDS")) : -1;  // tuning: words
     double kbits = 0.0;
     for (uint32_t s = 0; s < HZ_NSYM; ++s)
         if (cb->len[s]) kbits += ldexp((double)cb->len[s], -(int)cb->len[s]);
     const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
     const long room = (long)(kLdsBytes / 4) - (long)img.size() -
                       (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64;
-    long budget = env >= 0 ? env : room;
+    long budget = room;
     if (budget < 64) return;
     struct Head { uint32_t q, nb, off, c; };
     std::vector<Head> heads;
@@ -515,8 +514,7 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
-    static const int k1_env = getenv("HZ_DEC_K1") ? atoi(getenv("HZ_DEC_K1")) : 0;  // tuning experiments
-    K1 = std::min<int>((int)cb->max_len, k1_env > 0 && k1_env <= kDecLutMaxK1 ? k1_env : kDecLutMaxK1);
+    K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
     img.assign(1u << K1, 0u);
     l2.clear();

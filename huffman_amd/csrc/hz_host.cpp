@@ -37,6 +37,19 @@ using namespace hz;
 
 #define HZ_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return HZ_EHIP; } while (0)
 
+// No C++ exception crosses the C ABI: entry points that allocate host
+// containers run their body through this guard.
+template <typename F>
+static int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return HZ_ENOMEM;
+    } catch (...) {
+        return HZ_EINVAL;
+    }
+}
+
 // Pinned host staging for table uploads (see hz_codebook_upload_encode).
 struct Staging {
     uint8_t* p = nullptr;
@@ -74,6 +87,7 @@ extern "C" const char* hz_strerror(int st) {
         case HZ_ETIMEOUT: return "device wait timed out";
         case HZ_EIO: return "file I/O error";
         case HZ_ENODEV: return "no usable gfx950 device";
+        case HZ_ENOENT: return "input file does not exist";
         default: return "unknown error";
     }
 }
@@ -224,7 +238,7 @@ static int stage_copy(hz_ctx* c, Staging& st, T** dptr, size_t* dcap, const std:
     return HZ_OK;
 }
 
-extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
+static int hz_codebook_upload_encode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (!c || !cb) return HZ_EINVAL;
     if (cb->max_len > HZ_MAXLEN) return HZ_ETOOLONG;
     HZ_TRY(hipSetDevice(c->device));
@@ -267,7 +281,11 @@ extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
     return HZ_OK;
 }
 
-extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
+extern "C" int hz_codebook_upload_encode(hz_ctx* c, const hz_codebook* cb) {
+    return guarded([&] { return hz_codebook_upload_encode_impl(c, cb); });
+}
+
+static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (!c || !cb) return HZ_EINVAL;
     if (cb->max_len > HZ_MAXLEN) return HZ_ETOOLONG;
     HZ_TRY(hipSetDevice(c->device));
@@ -295,6 +313,10 @@ extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
     HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
     t.dec_mode = mode;
     return HZ_OK;
+}
+
+extern "C" int hz_codebook_upload_decode(hz_ctx* c, const hz_codebook* cb) {
+    return guarded([&] { return hz_codebook_upload_decode_impl(c, cb); });
 }
 
 extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
@@ -361,6 +383,9 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     if (!d_payload || !d_index) return HZ_EINVAL;
     if (c->t.dec_mode < 0) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
+    // nsym codewords end within nsym * max_len bits: the rest of a longer buffer is never walked
+    const uint64_t reach = (start_bit + nsym * (uint64_t)std::max(c->t.dec_max_len, 1) + 7) / 8 + 8;
+    if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
     int rc = ensure_scratch(c, index_scratch_words(payload_bytes, start_bit));
     if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][0], c->stream));
@@ -494,13 +519,21 @@ int decode_image(const uint8_t* f, uint64_t len, std::vector<uint8_t>& out) {
     int rc = hz_header_parse(f, len, cb.get(), &info);
     if (rc) return rc;
     const uint64_t nsym = info.n / 2;
-    out.assign(2 * nsym + (info.is_odd ? 1 : 0), 0);
+    const uint64_t pay = len - info.payload_byte;
+    // every codeword is >= min_len bits: a header claiming more symbols than the
+    // payload can hold is malformed (checked before anything is allocated)
+    const uint64_t pay_bits = pay * 8 > info.payload_bit ? pay * 8 - info.payload_bit : 0;
+    if (nsym > 0 && nsym > pay_bits / std::max<uint32_t>(cb->min_len, 1)) return HZ_EFORMAT;
+    try {
+        out.assign(2 * nsym + (info.is_odd ? 1 : 0), 0);
+    } catch (const std::bad_alloc&) {
+        return HZ_ENOMEM;
+    }
     if (nsym > 0) {
         hz_ctx* c;
         if ((rc = default_ctx(&c))) return rc;
         HZ_TRY(hipSetDevice(c->device));
         if ((rc = hz_codebook_upload(c, cb.get()))) return rc;
-        const uint64_t pay = len - info.payload_byte;
         DevBuf dpay, didx, dout;
         if ((rc = dpay.alloc(pay + 16))) return rc;
         HZ_TRY(hipMemsetAsync(dpay.p, 0, pay + 16, c->stream));
@@ -508,7 +541,14 @@ int decode_image(const uint8_t* f, uint64_t len, std::vector<uint8_t>& out) {
         if ((rc = didx.alloc(hz_index_bytes(nsym)))) return rc;
         if ((rc = dout.alloc(2 * nsym + 16))) return rc;
         if ((rc = hz_index_build(c, (const uint8_t*)dpay.p, pay, info.payload_bit, nsym, (uint64_t*)didx.p))) return rc;
-        if ((rc = hz_decode(c, (const uint8_t*)dpay.p, pay, nsym, (const uint64_t*)didx.p, (uint8_t*)dout.p))) return rc;
+        // the index builder leaves the end bit at all ones when the payload holds
+        // fewer than nsym codewords (truncated or corrupt file): reject before decoding
+        uint64_t end_bit = 0;
+        HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(nsym), 8, hipMemcpyDeviceToHost,
+                              c->stream));
+        if ((rc = hz_ctx_sync(c))) return rc;
+        if (end_bit > pay * 8) return HZ_EFORMAT;
+        if ((rc = hz_decode(c, (const uint8_t*)dpay.p, (end_bit + 7) / 8, nsym, (const uint64_t*)didx.p, (uint8_t*)dout.p))) return rc;
         HZ_TRY(hipMemcpyAsync(out.data(), dout.p, 2 * nsym, hipMemcpyDeviceToHost, c->stream));
         if ((rc = hz_ctx_sync(c))) return rc;
     }
@@ -555,11 +595,11 @@ int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
 
 }  // namespace
 
-extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+static int hz_archive_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     if (!in_path || !out_path || chunk_bytes < 64) return HZ_EINVAL;
     chunk_bytes &= ~(uint64_t)15;  // even (whole symbols) and 16-byte aligned device reads
     struct stat st;
-    if (stat(in_path, &st) != 0) return HZ_EIO;
+    if (stat(in_path, &st) != 0) return HZ_ENOENT;
     const uint64_t n = (uint64_t)st.st_size;
     hz_ctx* c;
     int rc = default_ctx(&c);
@@ -676,16 +716,20 @@ extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint
     return HZ_OK;
 }
 
+extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+    return guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+}
+
 // Streaming extract: the payload passes through a device window of chunk_bytes.
 // Each round decodes as many symbols as the window surely holds (the file's
 // mean code length with a margin; a round whose codes overrun the window is
 // redone at the max_len bound), writes them out, and moves the unconsumed
 // tail of the window to the front of the other buffer before refilling it.
-extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+static int hz_extract_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     if (!in_path || !out_path || chunk_bytes < 4096) return HZ_EINVAL;
     chunk_bytes &= ~(uint64_t)15;
     struct stat st;
-    if (stat(in_path, &st) != 0) return HZ_EIO;
+    if (stat(in_path, &st) != 0) return HZ_ENOENT;
     const uint64_t fsize = (uint64_t)st.st_size;
     FILE* fp = fopen(in_path, "rb");
     if (!fp) return HZ_EIO;
@@ -740,7 +784,9 @@ extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint
             } else {
                 k = (uint64_t)((double)avail / (mean * 1.03));
                 k = std::min(std::min(left, sym_cap), k);
-                if (k < left) k = std::max<uint64_t>(k / kBlockSyms * kBlockSyms, 1);
+                // whole blocks when the window holds at least one; a smaller window keeps k
+                if (k < left && k >= (uint64_t)kBlockSyms) k = k / kBlockSyms * kBlockSyms;
+                k = std::max<uint64_t>(k, 1);
             }
             uint64_t end_bit = 0;
             for (int attempt = 0;; ++attempt) {
@@ -788,7 +834,11 @@ extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint
     return HZ_OK;
 }
 
-extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+    return guarded([&] { return hz_extract_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+}
+
+static int hz_encode_host_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     if ((!in && n) || !out_len) return HZ_EINVAL;
     std::vector<uint8_t> img;
     int rc = encode_image(in, n, img, nullptr);
@@ -799,7 +849,11 @@ extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint6
     return HZ_OK;
 }
 
-extern "C" int hz_encoded_size(const uint8_t* in, uint64_t n, uint64_t* out_len) {
+extern "C" int hz_encode_host(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    return guarded([&] { return hz_encode_host_impl(in, n, out, cap, out_len); });
+}
+
+static int hz_encoded_size_impl(const uint8_t* in, uint64_t n, uint64_t* out_len) {
     if ((!in && n) || !out_len) return HZ_EINVAL;
     hz_ctx* c;
     int rc = default_ctx(&c);
@@ -814,7 +868,11 @@ extern "C" int hz_encoded_size(const uint8_t* in, uint64_t n, uint64_t* out_len)
     return HZ_OK;
 }
 
-extern "C" int hz_decode_host(const uint8_t* file, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* out_n) {
+extern "C" int hz_encoded_size(const uint8_t* in, uint64_t n, uint64_t* out_len) {
+    return guarded([&] { return hz_encoded_size_impl(in, n, out_len); });
+}
+
+static int hz_decode_host_impl(const uint8_t* file, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* out_n) {
     if (!file || !out_n) return HZ_EINVAL;
     std::vector<uint8_t> dec;
     int rc = decode_image(file, len, dec);
@@ -825,17 +883,24 @@ extern "C" int hz_decode_host(const uint8_t* file, uint64_t len, uint8_t* out, u
     return HZ_OK;
 }
 
+extern "C" int hz_decode_host(const uint8_t* file, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* out_n) {
+    return guarded([&] { return hz_decode_host_impl(file, len, out, cap, out_n); });
+}
+
 // Compressor.cu:315-632, stdout lines kept (:335-336,385,612-631).
 extern "C" int hz_archive_file(const char* path, int verbose) {
     if (!path) return HZ_EINVAL;
     struct stat st;
     if (stat(path, &st) != 0) {
         if (verbose) std::cout << path << " file does not exist" << std::endl << "Process has been terminated" << std::endl;
-        return HZ_EIO;
+        return HZ_ENOENT;
     }
     const std::string outname = std::string(path) + ".compressed";
     const int rc = hz_archive_stream(path, outname.c_str(), kArchiveChunk, verbose);
-    if (rc && verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;
+    if (rc) {
+        remove(outname.c_str());  // never leave a truncated archive behind
+        if (verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;
+    }
     return rc;
 }
 
@@ -845,7 +910,7 @@ extern "C" int hz_extract_file(const char* path, char* out_name, size_t out_name
     struct stat st;
     if (stat(path, &st) != 0) {
         if (verbose) std::cout << path << " does not exist" << std::endl;
-        return HZ_EIO;
+        return HZ_ENOENT;
     }
     std::string name = output_name();
     int rc = hz_extract_stream(path, name.c_str(), kArchiveChunk, 0);

@@ -9,13 +9,33 @@
 // Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
 #include <stdlib.h>
 
+#include <mutex>
+#include <set>
 #include <type_traits>
+#include <utility>
 
 #include "hz_internal.h"
 
 namespace hz {
 
 #define HZ_DEV __device__ __forceinline__
+
+// Dynamic-LDS limit of a kernel: hipFuncSetAttribute is per device, so the
+// (kernel, device) pairs already raised are remembered under a lock (any
+// number of contexts on any devices, from any host threads).
+static hipError_t ensure_lds_limit(const void* fn, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    static std::mutex mu;
+    static std::set<std::pair<std::pair<const void*, int>, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(std::make_pair(fn, dev), bytes);
+    if (done.count(key)) return hipSuccess;
+    if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess) return e;
+    done.insert(key);
+    return hipSuccess;
+}
 
 HZ_DEV uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -109,26 +129,15 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 // ===========================================================================
 constexpr int kHistThreads = 1024;
 constexpr int kHistUnroll = 1;
-#ifndef HZ_HIST_SWEEP
-#define HZ_HIST_SWEEP 1  // 1: grid-stride sweep (all workgroups read neighbouring 16 KiB pieces); 0: a chunk per workgroup
-#endif
 
 // LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
 // their low bits (the first byte), which alone would pick the LDS bank: the
 // second byte's low bits are XORed into the bank bits (a bijection).
-#ifndef HZ_HIST_SWZ
-#define HZ_HIST_SWZ 1
-#endif
-#if HZ_HIST_SWZ
 // The second byte times 13 (odd: distinct small bytes land on distinct, spread
 // banks) XORed into word bits 0-5; it depends only on word bits 7-14, which
 // the XOR leaves alone, so the map is a bijection.
 HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ (((s >> 8) * 13u) & 0x3fu); }
 HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ (((w >> 7) * 13u) & 0x3fu); }
-#else
-HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ ((s >> 8) & 0x3fu); }
-HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ ((w >> 7) & 0x3fu); }
-#endif
 
 // Fix-up after `old = atomicAdd(&lds[hist_word(s)], inc)`; rare (once per 65 536 adds of a bin).
 HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old) {
@@ -161,19 +170,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
     if (VEC) {
         const uint4* in4 = reinterpret_cast<const uint4*>(in);
         const uint64_t nvec = nsym / 8;
-#if HZ_HIST_SWEEP
-        // the whole chip sweeps the input together, as the count pass does
+        // the whole chip sweeps the input together (neighbouring 16 KiB pieces)
         static_assert(kHistUnroll == 1, "sweep reads one vector per lane per step");
         const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
         const uint64_t beg = (uint64_t)blockIdx.x * blockDim.x;
         const uint64_t end = nvec;
-#else
-        const uint64_t step = (uint64_t)blockDim.x * kHistUnroll;
-        uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
-        per = (per + step - 1) / step * step;
-        const uint64_t beg = blockIdx.x * per;
-        const uint64_t end = beg + per < nvec ? beg + per : nvec;
-#endif
         // software pipelined: the next iteration's loads are in flight while
         // this one's LDS atomics run (loads and LDS ops use separate counters)
         uint4 nx[kHistUnroll];
@@ -246,12 +247,8 @@ hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_
     if (nsym == 0) return hipSuccess;
     const bool vec = (((uintptr_t)d_in) & 15) == 0;
     const void* fn = vec ? (const void*)k_hist16<true> : (const void*)k_hist16<false>;
-    static bool attr_done[2] = {false, false};
-    if (!attr_done[vec]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-        if (e != hipSuccess) return e;
-        attr_done[vec] = true;
-    }
+    hipError_t e = ensure_lds_limit(fn, 131072);
+    if (e != hipSuccess) return e;
     // One workgroup per CU; fewer for small inputs (every WG zeroes + flushes 128 KiB).
     uint64_t want = (nsym + 65535) / 65536;
     unsigned grid = (unsigned)(want < (uint64_t)ncu ? (want ? want : 1) : ncu);
@@ -276,9 +273,6 @@ hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_
 // Code tables live in LDS (DENSE 17-bit sentinel entries, or HOT tagged
 // slots) and are loaded once per workgroup of a grid-stride kernel.
 // ===========================================================================
-#ifndef HZ_PACK_STATIC_ESC
-#define HZ_PACK_STATIC_ESC 1
-#endif
 struct PackArgs {
     const uint8_t* in;
     uint64_t nsym;
@@ -386,7 +380,6 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
         const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
         xe = (T)xx;
-#if HZ_PACK_STATIC_ESC
         // Every lane issues all 33 escape loads (lanes without a miss read
         // esc[0], one coalesced address): a fixed load count keeps the waits
         // of later loads and stores static. The escape table holds entries in
@@ -403,17 +396,6 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             const uint32_t v = a.esc[miss ? xs : 0u];
             xe = miss ? (T)v : xe;
         }
-#else
-        if ((any | xx) >> 31) {
-            // The escape table holds entries in the register format, so each
-            // load lands in its e[k] directly and the single wait falls at the
-            // first use.
-#pragma unroll
-            for (int k = 0; k < kSPT; ++k)
-                if ((uint32_t)e[k] >> 31) e[k] = (T)a.esc[(raw[k >> 1] >> (16 * (k & 1))) & 0xffffu];
-            if (xx >> 31) xe = (T)a.esc[xs];
-        }
-#endif
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
@@ -549,14 +531,8 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
     }
 }
 
-#ifndef HZ_PACK_THREADS
-#define HZ_PACK_THREADS 512
-#endif
-constexpr int kPackWriteThreads = HZ_PACK_THREADS;
-#ifndef HZ_PACK_STATIC_COPY
-#define HZ_PACK_STATIC_COPY 1
-#endif
-constexpr int kPackCopyIters = 16;  // slot copy-out: 16 x 64 words covers a 1024-word slot  // <= 8 waves: room for a block of registers in flight per lane
+constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
+constexpr int kPackCopyIters = 16;       // slot copy-out: 16 x 64 words covers a 1024-word slot
 
 // One block of a wave between its lookup and its emit: the lane's 32 entries,
 // the entry of one of the previous block's last 32 symbols, the lane's bits,
@@ -649,7 +625,6 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
         if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
         __builtin_amdgcn_wave_barrier();
         if (fits) {
-#if HZ_PACK_STATIC_COPY
             if constexpr (MODE != ENC_WIDE) {  // host: slot_words <= kPackCopyIters * kWave
                 // a fixed count of full-wave stores (lanes past the block rewrite its last
                 // word with the same value), so later load waits count them statically
@@ -659,9 +634,9 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
                     w = w < nwords ? w : nwords - 1;
                     a.out[wfirst + w] = bswap32(slot[w]);
                 }
-            } else
-#endif
-            for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+            } else {
+                for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+            }
         }
         __builtin_amdgcn_wave_barrier();
     } else {
@@ -935,13 +910,8 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
         if (e != hipSuccess) return e;
     }
     if (t.enc_mode == ENC_FIXED16) {
-        static bool attr_fixed = false;
-        if (!attr_fixed) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_pack_fixed16, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               kFixed16LdsBytes);
-            if (e != hipSuccess) return e;
-            attr_fixed = true;
-        }
+        hipError_t e = ensure_lds_limit((const void*)k_pack_fixed16, kFixed16LdsBytes);
+        if (e != hipSuccess) return e;
         const uint64_t nl = (nsym + kSPT - 1) / kSPT;
         uint64_t wgs = (nl + kPackThreads - 1) / kPackThreads;
         if (wgs > (uint64_t)ncu) wgs = ncu;  // 128 KiB table: one workgroup per CU
@@ -967,20 +937,12 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t lds = 4 * (table_words + waves * a.slot_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
-    static bool attr[3] = {false, false, false};
-    static bool attr_count = false;
-    if (!attr_count) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_pack_count, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           kLen8LdsBytes);
+    {
+        hipError_t e = ensure_lds_limit((const void*)k_pack_count, kLen8LdsBytes);
         if (e != hipSuccess) return e;
-        attr_count = true;
-    }
-    if (!attr[t.enc_mode]) {
         const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE>, (const void*)k_pack_write<ENC_HOT>,
                              (const void*)k_pack_write<ENC_WIDE>};
-        hipError_t e = hipFuncSetAttribute(fw[t.enc_mode], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr[t.enc_mode] = true;
+        if ((e = ensure_lds_limit(fw[t.enc_mode], kLdsBytes)) != hipSuccess) return e;
     }
     {
         const uint64_t cw = kCountThreads / 64;
@@ -1326,16 +1288,9 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
 // The LDS steps of NC chains at once (dec_pipe_lds2 generalised): all window
 // reads, then all level-1 reads, then all LDS-second-level reads in flight
 // together, so NC chain steps cost three LDS round trips.
-// Phase fences of the NC-chain walk (build knob): keep each phase's LDS reads
-// issued together whatever the scheduler would do (the decoder is order-sensitive).
-#ifndef HZ_WALK_FENCES
-#define HZ_WALK_FENCES 1
-#endif
-#if HZ_WALK_FENCES
+// Phase fences of the NC-chain walk: keep each phase's LDS reads issued
+// together whatever the scheduler would do (the decoder is order-sensitive).
 #define HZ_WALK_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define HZ_WALK_FENCE() ((void)0)
-#endif
 
 template <int NC>
 HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, const uint32_t* pos,
@@ -1436,18 +1391,7 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
     }
 }
 
-#ifndef HZ_PF_STEP
-#define HZ_PF_STEP 4
-#endif
-#ifndef HZ_PIPE_QUARTER
-#define HZ_PIPE_QUARTER 0
-#endif
-#ifndef HZ_PIPE_PAIR
-#define HZ_PIPE_PAIR 1
-#endif
-#ifndef HZ_DEC_QUAD
-#define HZ_DEC_QUAD 1
-#endif
+constexpr int kPfStep = 4;  // chain step at which the next block's staging loads issue (2-6 measured equal)
 // Persistent pipelined decoder of one wave: blocks b, b + stride, ... The
 // staging chunks of the next block and the metadata of the one after are
 // loaded halfway through this block's steps, so no block waits on HBM.
@@ -1481,28 +1425,6 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
             if (q & 1) pk[i] |= sym << 16;
             else pk[i] = sym;
         };
-#if HZ_PIPE_QUARTER
-        // each chain's gathers are consumed after the other three chains' LDS steps
-        auto issue = [&](int c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; };
-        issue(0);
-        issue(1);
-        issue(2);
-#pragma unroll
-        for (int q = 0; q < kChainSyms; ++q) {
-            issue(3);
-            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
-                dec_stage_prefetch(a, mn, lane, sn);
-                dec_meta_load(a, b + 2 * stride, lane, mn2);
-            }
-            finish(0, q);
-            if (q + 1 < kChainSyms) issue(0);
-            finish(1, q);
-            if (q + 1 < kChainSyms) issue(1);
-            finish(2, q);
-            if (q + 1 < kChainSyms) issue(2);
-            finish(3, q);
-        }
-#elif HZ_PIPE_PAIR
         auto issue2 = [&](int c) {
             dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
             g[c] = a.l2[st[c].gi];
@@ -1512,7 +1434,7 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
             issue2(2);
-            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
+            if (q == kPfStep) {  // next block's staging chunks, the metadata after it
                 dec_stage_prefetch(a, mn, lane, sn);
                 dec_meta_load(a, b + 2 * stride, lane, mn2);
             }
@@ -1522,27 +1444,6 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
             finish(2, q);
             finish(3, q);
         }
-#else
-#pragma unroll
-        for (int c = 0; c < 2; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
-#pragma unroll
-        for (int q = 0; q < kChainSyms; ++q) {
-#pragma unroll
-            for (int c = 2; c < 4; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
-            if (q == HZ_PF_STEP) {  // next block's staging chunks, the metadata after it
-                dec_stage_prefetch(a, mn, lane, sn);
-                dec_meta_load(a, b + 2 * stride, lane, mn2);
-            }
-            finish(0, q);
-            finish(1, q);
-            if (q + 1 < kChainSyms) {
-#pragma unroll
-                for (int c = 0; c < 2; ++c) { st[c] = dec_pipe_lds(a, lds, stg, pos[c]); g[c] = a.l2[st[c].gi]; }
-            }
-            finish(2, q);
-            finish(3, q);
-        }
-#endif
         __builtin_amdgcn_wave_barrier();
         dec_store(a, b, lane, pk);
         mc = mn;
@@ -1593,7 +1494,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             if (q & 1) pk[c / kChainsPerLane][i] |= sym << 16;
             else pk[c / kChainsPerLane][i] = sym;
         };
-#if HZ_DEC_QUAD
         // two quads (one per block): a quad's gathers land behind the other quad's walk
         auto issue4 = [&](int c) {
             dec_pipe_ldsn<4>(a, lds, stg, pos + c, st + c);
@@ -1604,7 +1504,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
             issue4(4);
-            if (q == HZ_PF_STEP) {  // the next two blocks' staging chunks, the metadata after them
+            if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
 #pragma unroll
@@ -1616,34 +1516,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
             for (int c = 4; c < 8; ++c) finish(c, q);
         }
-#else
-        auto issue2 = [&](int c) {
-            dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
-            g[c] = a.l2[st[c].gi];
-            g[c + 1] = a.l2[st[c + 1].gi];
-        };
-        issue2(0);
-        issue2(2);
-        issue2(4);
-#pragma unroll
-        for (int q = 0; q < kChainSyms; ++q) {
-            issue2(6);
-            if (q == HZ_PF_STEP) {  // the next two blocks' staging chunks, the metadata after them
-#pragma unroll
-                for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) dec_meta_load(a, b + 2 * stride + j, lane, mn2[j]);
-            }
-#pragma unroll
-            for (int c = 0; c < 6; c += 2) {
-                finish(c, q);
-                finish(c + 1, q);
-                if (q + 1 < kChainSyms) issue2(c);
-            }
-            finish(6, q);
-            finish(7, q);
-        }
-#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -1658,10 +1530,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
     }
 }
 
-#ifndef HZ_DEC_P2_THREADS
-#define HZ_DEC_P2_THREADS 512
-#endif
-constexpr int kDecPipe2Threads = HZ_DEC_P2_THREADS;  // two staging slots per wave
+constexpr int kDecPipe2Threads = 512;  // two staging slots per wave (1024 with smaller hot heads: 15.2 ms vs 13.1)
 // PIPE: 0 plain block loop, 1 pipelined (one block per wave), 2 pipelined, two blocks per wave
 template <int MODE, bool WIDE, int PIPE>
 __global__ __launch_bounds__(PIPE == 2 ? kDecPipe2Threads : 1024) void k_decode(DecArgs a) {
@@ -1772,16 +1641,16 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
 // more waves.
 template <int MODE, bool WIDE, int PIPE>
 static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_decode<MODE, WIDE, PIPE>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    {
+        hipError_t e = ensure_lds_limit((const void*)k_decode<MODE, WIDE, PIPE>, kLdsBytes);
         if (e != hipSuccess) return e;
-        attr = true;
     }
-    const uint64_t avg = (payload_bits + a.nblocks - 1) / a.nblocks;
-    const uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
+    // a block never exceeds 2048 x max_len bits, whatever follows the stream in the buffer
+    uint64_t avg = (payload_bits + a.nblocks - 1) / a.nblocks;
+    avg = avg < (uint64_t)kBlockSyms * (uint32_t)a.max_len ? avg : (uint64_t)kBlockSyms * (uint32_t)a.max_len;
     const uint32_t worst = dec_slot_words_max(a.max_len);
+    uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
+    est = est < worst ? est : worst;
     const uint32_t table = a.lds_words;
     int best_w = 0, best_g = 1;
     for (int g = 1; g <= 2; ++g) {
@@ -1820,13 +1689,8 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     a.subs = d_index + index_sub_offset(a.nblocks);
     a.out = d_out; a.err = d_err;
     if (t.dec_mode == DEC_FIXED16) {
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_decode_fixed16, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               kFixed16LdsBytes);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        hipError_t e = ensure_lds_limit((const void*)k_decode_fixed16, kFixed16LdsBytes);
+        if (e != hipSuccess) return e;
         const uint64_t nl = (nsym + kSPT - 1) / kSPT;
         uint64_t wgs = (nl + 1023) / 1024;
         if (wgs > (uint64_t)ncu) wgs = ncu;
@@ -2317,30 +2181,21 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
 template <int MODE>
 static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* first, unsigned long long* tiles,
                             unsigned long long* d_index, uint32_t* h_changed, uint32_t lds, int ncu, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        const void* fns[3] = {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>,
-                              (const void*)k_sync_emit<MODE>};
-        for (const void* f : fns) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-            if (e != hipSuccess) return e;
-        }
-        attr = true;
+    for (const void* f : {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>, (const void*)k_sync_emit<MODE>}) {
+        hipError_t e = ensure_lds_limit(f, kLdsBytes);
+        if (e != hipSuccess) return e;
     }
     // 16-wave workgroups: one table copy per workgroup, as many waves as a CU holds
     uint64_t wgs = (y.nseg + kSyncThreads - 1) / kSyncThreads;
     const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 2 ? 1 : 2) : 2);
     wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
     // two segments per lane where the pipelined decoder's table shape holds
-    static const int two_env = [] { const char* v = getenv("HZ_SYNC_TWO"); return v ? atoi(v) : 1; }();
-    const bool two = two_env && MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + kDecLevelBits;
-    static bool attr2 = false;
-    if (two && !attr2) {
+    const bool two = MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + kDecLevelBits;
+    if (two) {
         for (const void* f : {(const void*)k_sync_scan2, (const void*)k_sync_emit2}) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            hipError_t e = ensure_lds_limit(f, kLdsBytes);
             if (e != hipSuccess) return e;
         }
-        attr2 = true;
     }
     if (two)
         hipLaunchKernelGGL(k_sync_scan2, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);

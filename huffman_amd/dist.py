@@ -11,7 +11,9 @@ small exchange steps, plus an optional reassembly:
      at most one 32-bit boundary word, merged with OR.
 
 Shard g holds the bytes [g*S, (g+1)*S) of the input with S even, so no
-symbol straddles two ranks. Decode needs no collective: each rank decodes
+symbol straddles two ranks; the last shard takes the rest, and when the
+stream is odd its final raw byte is broadcast to rank 0 for the header
+(odd_last_byte). Decode needs no collective: each rank decodes
 its own symbols from its own payload (its index holds absolute local bits).
 Over RCCL ("nccl" backend on ROCm) the exchanges ride xGMI; the tests use gloo.
 """
@@ -26,6 +28,28 @@ def shard_range(n_total, world, rank):
     beg = per * rank
     end = n_total if rank == world - 1 else beg + per
     return beg, end
+
+
+def odd_last_byte(shard, n_total, group=None):
+    """The raw trailing byte of an odd-length stream, on every rank.
+
+    With n_total odd the last rank's shard ends in the byte that is not coded
+    (Compressor.cu:339-351); rank 0 writes it into the header
+    (Compressor.cu:438-443), so it is broadcast from the last rank. 0 when
+    n_total is even. `shard`: this rank's bytes (numpy array or tensor)."""
+    if n_total % 2 == 0:
+        return 0
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = shard.device if isinstance(shard, torch.Tensor) else torch.device("cpu")
+    if dist.get_backend(group) == "nccl" and dev.type != "cuda":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    v = torch.zeros(1, dtype=torch.int64, device=dev)
+    if rank == world - 1:
+        assert len(shard) % 2 == 1, "the last shard of an odd stream holds the odd byte"
+        v[0] = int(shard[-1])
+    dist.broadcast(v, src=world - 1, group=group)
+    return int(v.item())
 
 
 def global_histogram(hist_local, group=None):

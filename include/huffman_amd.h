@@ -40,7 +40,8 @@ enum {
     HZ_ECAP = -6,      /* output capacity too small */
     HZ_ETIMEOUT = -7,  /* a device-side wait exceeded its bound (reserved) */
     HZ_EIO = -8,       /* file I/O error */
-    HZ_ENODEV = -9     /* no usable gfx950 device */
+    HZ_ENODEV = -9,    /* no usable gfx950 device */
+    HZ_ENOENT = -10    /* input file does not exist (the reference CLIs exit 0 on it) */
 };
 
 /* Codebook in the reference's order and bit conventions. */

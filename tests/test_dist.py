@@ -44,8 +44,10 @@ def _worker(rank, world, port, n_total, kind, result_path):
         word0, start, words = hd.local_geometry(hb, off, pbits, rank == 0)
         _, ln, code = huffman_amd.codebook_arrays(cb)
         buf = oracle_lib.pack_range(shard, 0, shard.size // 2, ln, code, start, words * 4 + 8)
+        # the odd trailing byte travels from the last rank (its shard) to rank 0's header
+        last = hd.odd_last_byte(shard, n_total)
         if rank == 0:
-            header, pend_bits, pend = huffman_amd.write_header(cb, n_total, int(data[-1]) if n_total % 2 else 0)
+            header, pend_bits, pend = huffman_amd.write_header(cb, n_total, last)
             buf[0] |= pend
         nbytes = (start + pbits + 7) // 8
         # the device-side reassembly's exchange (bench.py N > 1), through host copies here
@@ -70,7 +72,8 @@ def _worker(rank, world, port, n_total, kind, result_path):
 
 
 @pytest.mark.parametrize("world,n_total,kind", [(2, 1 << 20, 1), (2, (1 << 20) + 3, 0), (3, 300001, 1),
-                                                (4, 4 * 4096 + 2, 1)])
+                                                (4, 4 * 4096 + 2, 1), (8, 8 * 65536 + 4097, 1),
+                                                (8, 8 * 8192 + 2, 0)])
 def test_sharded_stream_equals_single_stream(tmp_path, world, n_total, kind):
     result = str(tmp_path / "result.txt")
     mp.start_processes(_worker, args=(world, _free_port(), n_total, kind, result), nprocs=world, join=True,

@@ -323,3 +323,75 @@ def test_pipeline_4gib_roundtrip_properties(codec):
     assert torch.equal(out[:n], x[:n])
     del x, out, payload
     torch.cuda.empty_cache()
+
+
+# ---- malformed input: clean errors, no hang ------------------------------------------
+def _set_n(blob, n):
+    """Rewrite the header's 64-bit N (8 LE bytes, each MSB-first, starting at the
+    header's bit position) of an oracle file: re-encode with the same codebook."""
+    import huffman_amd
+    cb, info = huffman_amd.parse_header(blob)
+    head, pbits, pend = huffman_amd.write_header(cb, n, info.last_byte)
+    return head + bytes([(pend & (0xff << (8 - pbits))) | (blob[len(head)] & (0xff >> pbits))]) \
+        + blob[len(head) + 1:] if pbits else head + blob[len(head):]
+
+
+def _extract_rc(hz, tmp_path, blob):
+    d = tmp_path / "x"
+    d.mkdir(exist_ok=True)
+    (d / "bad.compressed").write_bytes(blob)
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "bad.compressed"], cwd=d, capture_output=True,
+                       text=True, timeout=120)
+    return r.returncode, (d / "DECOMPRESSED_FILE")
+
+
+@pytest.mark.parametrize("cut", [1, 7, 1000, "half"])
+def test_truncated_file_is_rejected(hz, tmp_path, cut):
+    data = _zipf_bytes((1 << 20) + 1, 3)
+    blob = oracle_lib.encode(data)
+    bad = blob[:len(blob) // 2] if cut == "half" else blob[:-cut]
+    with pytest.raises(hz.HZError):
+        hz.decode(bad)
+    rc, out = _extract_rc(hz, tmp_path, bad)
+    assert rc == 2 and not out.exists()   # codec failure: exit 2, no partial output left behind
+
+
+def test_header_n_larger_than_payload_is_rejected(hz, tmp_path):
+    data = _zipf_bytes(1 << 20, 4)
+    blob = oracle_lib.encode(data)
+    bad = _set_n(blob, 1 << 40)
+    with pytest.raises(hz.HZError):
+        hz.decode(bad)
+    rc, out = _extract_rc(hz, tmp_path, bad)
+    assert rc == 2 and not out.exists()
+
+
+def test_header_n_smaller_decodes_prefix(hz):
+    data = _zipf_bytes(1 << 20, 5)
+    blob = oracle_lib.encode(data)
+    short = _set_n(blob, 1000)
+    assert hz.decode(short) == data[:1000]
+
+
+@pytest.mark.parametrize("where", ["payload", "header"])
+def test_bit_flips_end_cleanly(hz, tmp_path, where):
+    """A flipped bit either decodes (to some bytes) or is rejected; never a hang
+    or a fault. Same outcome through the library and the CLI."""
+    data = _zipf_bytes(1 << 20, 6)
+    blob = bytearray(oracle_lib.encode(data))
+    cb, info = hz.parse_header(bytes(blob))
+    rng = np.random.default_rng(1)
+    for trial in range(4):
+        b = bytearray(blob)
+        pos = int(rng.integers(info.payload_byte + 1, len(b))) if where == "payload" else int(rng.integers(4, 40))
+        b[pos] ^= 1 << int(rng.integers(0, 8))
+        try:
+            out = hz.decode(bytes(b))
+            ok = True
+        except hz.HZError:
+            ok = False
+        rc, f = _extract_rc(hz, tmp_path, bytes(b))
+        assert rc == (0 if ok else 2)
+        if ok:
+            assert f.read_bytes() == out
+            f.unlink()

@@ -1,0 +1,104 @@
+"""The sharded path on the HIP kernels: an N-rank rehearsal on
+one GPU (every rank on cuda:0, gloo collectives through host copies).
+
+Each rank generates its shard of one global stream on the device, runs the
+device histogram, joins the histogram all-reduce and the payload-bit
+all-gather (huffman_amd/dist.py), packs its shard with hz_pack at its global
+bit offset, decodes it back through the pack index, and ships its payload to
+rank 0 through dist.reassemble_on_device. Rank 0's header + reassembled stream
+must equal the CPU oracle's encoding of the whole stream byte for byte, and
+decode whole on the device (index rebuilt from the stream alone). The 8-rank
+geometry is the 128 GiB config's (8 x MI355X) at test size, with a ragged,
+odd-length final shard whose raw byte travels to rank 0's header.
+
+Tolerance: none (bit-exact)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, kind, result_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    status = "error"
+    try:
+        import huffman_amd
+        from huffman_amd import dist as hd
+        from huffman_amd.pipeline import StreamCodec
+        codec = StreamCodec(0)
+        dev = codec.device
+        beg, end = hd.shard_range(n_total, world, rank)
+        n = end - beg
+        x = torch.empty(max(n, 16), dtype=torch.uint8, device=dev)[:n]
+        codec.dev.generate(x.data_ptr(), n, offset=beg, kind=kind, alpha=1.1, seed=42)
+        codec.histogram(x)
+        hl = codec.hist.cpu()
+        h = hl.clone()
+        dist.all_reduce(h)                                         # 1. histogram all-reduce
+        h_np = h.numpy().view(np.uint64)
+        hl_np = hl.numpy().view(np.uint64)
+        cb = huffman_amd.build_codebook(h_np)
+        pbits = huffman_amd.payload_bits(cb, hl_np)
+        off, totals = hd.shard_bit_offsets(pbits, torch.device("cpu"))   # 2. bit-offset all-gather
+        last = hd.odd_last_byte(x.cpu().numpy(), n_total)
+        plan = codec.make_plan(h_np, n_total, hist_local=hl_np, first_shard=(rank == 0), shard_bit_offset=off,
+                               last_byte=last, cb=cb)
+        nsym = n // 2
+        payload, index = codec.alloc_payload(plan, nsym)
+        codec.pack(x, plan, payload, index)                        # 3. pack at the global offset
+        codec.upload_decode(plan)
+        out = torch.empty(2 * nsym + 16, dtype=torch.uint8, device=dev)
+        codec.decode(payload, nsym, index, out)
+        codec.sync()
+        local_ok = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+        word0, start, words = hd.local_geometry(plan.header_bits, off, pbits, rank == 0)
+        assert start == plan.start_bit and words == plan.words
+        nbytes = (plan.start_bit + pbits + 7) // 8
+        stream, total = hd.reassemble_on_device(payload, nbytes, word0, dst=0, via_host=True)
+        flags = torch.tensor([0 if local_ok else 1], dtype=torch.int64)
+        dist.all_reduce(flags)
+        if rank == 0:
+            data = oracle_lib.generate(n_total, offset=0, kind=kind, seed=42)
+            ref = oracle_lib.encode(data)
+            blob = plan.header + stream[:total].cpu().numpy().tobytes()
+            checks = {
+                "per_rank_roundtrip": int(flags.item()) == 0,
+                "file_equals_oracle": blob == ref,
+                "whole_stream_decodes": huffman_amd.decode(blob) == data.tobytes(),
+            }
+            status = ",".join(k for k, v in checks.items() if not v) or "ok"
+        else:
+            status = "ok"
+    finally:
+        with open(os.path.join(result_dir, f"rank{rank}.txt"), "w") as f:
+            f.write(status)
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n_total,kind", [(8, 8 * (1 << 20) + 4097, 1), (8, 8 * (256 << 10) + 2, 0),
+                                                (3, (3 << 20) + 1, 1)])
+def test_sharded_rehearsal_equals_single_stream(tmp_path, world, n_total, kind):
+    mp.start_processes(_worker, args=(world, _free_port(), n_total, kind, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = [open(tmp_path / f"rank{r}.txt").read() for r in range(world)]
+    assert got == ["ok"] * world, got
