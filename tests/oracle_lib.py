@@ -17,7 +17,8 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(ORACLE_DIR, "hz_oracle.c")):
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("hz_oracle.c", "compressor_literal.c")]
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
     lib = ctypes.CDLL(LIB)
     P, U64 = ctypes.c_void_p, ctypes.c_uint64
@@ -33,6 +34,12 @@ def load():
     lib.hzo_encoded_bits.restype = U64
     lib.hzo_zipf_thresholds.argtypes = [ctypes.c_double, P]
     lib.hzo_gen.argtypes = [P, U64, U64, ctypes.c_int, U64, P]
+    I64 = ctypes.c_int64
+    lib.hzl_archive.argtypes = [P, U64, P, ctypes.c_uint32, P, P, P, U64, P, ctypes.POINTER(I64), ctypes.POINTER(I64)]
+    lib.hzl_archive.restype = I64
+    lib.hzl_header.argtypes = [U64, ctypes.c_uint8, P, ctypes.c_uint32, P, P, P, U64, ctypes.POINTER(ctypes.c_uint32),
+                               ctypes.POINTER(ctypes.c_uint8)]
+    lib.hzl_header.restype = I64
     _lib = lib
     return lib
 
@@ -84,6 +91,42 @@ def decode(blob, cap=None):
     if rc:
         raise RuntimeError(f"hzo_decode {rc}")
     return out[:n.value].tobytes()
+
+
+def reference_archive(data, order, ln, code):
+    """Literal Compressor.cu file writer (oracle/compressor_literal.c), defects
+    B1/B2 included: -> (file bytes, undefined-byte flags, B1 byte offset or -1,
+    B2 byte offset or -1). order/ln/code: the codebook as the reference host
+    holds it (header order; length and right-aligned code per symbol value)."""
+    a = as_u8(data)
+    order = np.ascontiguousarray(order, dtype=np.uint16)
+    ln = np.ascontiguousarray(ln, dtype=np.uint8)
+    code = np.ascontiguousarray(code, dtype=np.uint64)
+    cap = 3 * a.size + 400000
+    out = np.zeros(cap, dtype=np.uint8)
+    flags = np.zeros(cap, dtype=np.uint8)
+    b1, b2 = ctypes.c_int64(), ctypes.c_int64()
+    n = load().hzl_archive(_p(a), a.size, _p(order), order.size, _p(ln), _p(code), _p(out), cap, _p(flags),
+                           ctypes.byref(b1), ctypes.byref(b2))
+    if n < 0:
+        raise RuntimeError(f"hzl_archive {n}")
+    return out[:n].tobytes(), flags[:n].copy(), b1.value, b2.value
+
+
+def reference_header(n, last_byte, order, ln, code):
+    """Literal Compressor.cu header writer (:431-487) -> (complete header bytes,
+    pending bit count, pending bits MSB-aligned)."""
+    order = np.ascontiguousarray(order, dtype=np.uint16)
+    ln = np.ascontiguousarray(ln, dtype=np.uint8)
+    code = np.ascontiguousarray(code, dtype=np.uint64)
+    cap = 16 + order.size * 11
+    out = np.zeros(cap, dtype=np.uint8)
+    pb, pend = ctypes.c_uint32(), ctypes.c_uint8()
+    k = load().hzl_header(n, last_byte, _p(order), order.size, _p(ln), _p(code), _p(out), cap, ctypes.byref(pb),
+                          ctypes.byref(pend))
+    if k < 0:
+        raise RuntimeError(f"hzl_header {k}")
+    return out[:k].tobytes(), pb.value, pend.value
 
 
 def pack_range(data, sym0, count, ln, code, bit0, nbytes):

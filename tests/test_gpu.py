@@ -4,6 +4,7 @@ fixtures, the reference decoder, and size-independent properties at scale.
 Tolerance: none -- every check is bit-exact (integer/bit work)."""
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -395,3 +396,65 @@ def test_bit_flips_end_cleanly(hz, tmp_path, where):
         if ok:
             assert f.read_bytes() == out
             f.unlink()
+
+
+# ---- encoder parity at scale: literal GenerateCL codebooks, literal Compressor.cu writer ----
+sys.path.insert(0, GOLD)
+import make_scale_golden as msg  # noqa: E402
+
+SCALE = msg.load_fixture()
+
+
+@pytest.mark.parametrize("name,kind", [("zipf_256MiB", 1), ("uniform_256MiB", 0)])
+def test_scale_codebook_on_device(hz, codec, name, kind):
+    """Device histogram of the bench stream's first 256 MiB -> product codebook
+    and header == the literal GenerateCL / Compressor.cu writer fixture."""
+    import torch
+    n = SCALE[name]["n"]
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=42)
+    codec.histogram(x)
+    h = codec.hist.cpu().numpy().view(np.uint64).copy()
+    assert msg.sha(h.astype("<u8").tobytes()) == SCALE[name]["hist_sha256"]
+    cb = hz.build_codebook(h)
+    order, ln, code = hz.codebook_arrays(cb)
+    got = msg.digest(order, ln, code, h, n, 0, header=hz.write_header(cb, n, 0))
+    assert got == msg.codebook_keys(SCALE[name])
+    del x
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name", ["tie_dense", "tie_ragged"])
+def test_scale_tie_streams(hz, name):
+    """Tie-dense streams through the whole host API: codebook/header == the
+    literal fixture, file == the literal Compressor.cu writer (except B1/B2)."""
+    data = msg.tie_stream(name)
+    blob = hz.encode(data)
+    cb, info = hz.parse_header(blob)
+    order, ln, code = hz.codebook_arrays(cb)
+    h = oracle_lib.hist16(data)
+    n = SCALE[name]["n"]
+    last = int(data[-1]) if n % 2 else 0
+    assert msg.digest(order, ln, code, h, n, last) == msg.codebook_keys(SCALE[name])
+    diff, allowed, _ = msg.literal_divergence(data, blob, order, ln, code)
+    assert set(diff) <= set(allowed)
+
+
+def test_product_equals_literal_writer_except_b1_b2(hz):
+    """hz.encode against the literal Compressor.cu writer: byte for byte equal
+    except at the reference's B1/B2 bytes (and the sweep does hit both)."""
+    hits = {"B1": 0, "B2": 0}
+    for n in list(range(2, 160)) + [1001, 4097, 65537, (16 << 20) + 1]:
+        for kind in (0, 1):
+            data = oracle_lib.generate(n, offset=7 * n, kind=kind, seed=3)
+            h = oracle_lib.hist16(data)
+            if np.count_nonzero(h) < 2:
+                continue
+            blob = hz.encode(data)
+            cb, _ = hz.parse_header(blob)
+            order, ln, code = hz.codebook_arrays(cb)
+            diff, allowed, undef = msg.literal_divergence(data, blob, order, ln, code)
+            assert set(diff) <= set(allowed), (n, kind, diff, allowed)
+            for p in diff:
+                hits[allowed[p]] += 1
+    assert hits["B1"] > 0 and hits["B2"] > 0, hits
