@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=16 << 30, help="input bytes per GPU")
     ap.add_argument("--dist", default="zipf", choices=["zipf", "uniform"])
-    ap.add_argument("--cpu-sample-mib", type=int, default=128)
+    ap.add_argument("--cpu-sample-mib", type=int, default=128, help="one-process CPU baseline sample")
+    ap.add_argument("--cpu-par-sample-mib", type=int, default=48, help="per-process sample, all-core CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--no-reassemble", action="store_true", help="N>1: skip the (untimed-in-step) stream reassembly")
@@ -46,43 +47,84 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(sample_bytes, kind):
-    """Reference baseline/ encoder+decoder (built from the reference sources by
-    oracle/Makefile) on a bounded sample of the same stream, 1 process."""
+def _cpu_info():
+    """Cores this process may use (the box's CPU share) and the host CPU model."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, model
+
+
+def _baseline_run(args):
+    """One reference baseline encode + decode of `sample.bin` in its own CWD
+    (the reference decoder always writes ./DECOMPRESSED_FILE); wall times."""
+    enc_exe, dec_exe, td, data_bytes = args
+    t0 = time.perf_counter()
+    subprocess.run([enc_exe, "sample.bin"], cwd=td, check=True, capture_output=True)
+    t1 = time.perf_counter()
+    subprocess.run([dec_exe, "sample.bin.compressed"], cwd=td, check=True, capture_output=True)
+    t2 = time.perf_counter()
+    with open(os.path.join(td, "DECOMPRESSED_FILE"), "rb") as f:
+        ok = f.read() == data_bytes
+    return t1 - t0, t2 - t1, t2 - t0, ok
+
+
+def cpu_baseline(sample_bytes, kind, par_sample_bytes):
+    """Reference baseline/ encoder + decoder (built from the reference sources by
+    oracle/Makefile) on bounded samples of the same stream:
+    (i) one process on the first sample_bytes, (ii) one process per core this
+    job may use, all at once, each on its own slice of par_sample_bytes in its
+    own CWD. `value` is the all-core aggregate; the one-process rate is beside it."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-    data = oracle_lib.generate(sample_bytes, offset=0, kind=kind, seed=42)
+    from concurrent.futures import ThreadPoolExecutor
+    cores, model = _cpu_info()
     enc_exe, dec_exe = oracle_lib.ref_binary("archive_baseline"), oracle_lib.ref_binary("extract_baseline")
-    with tempfile.TemporaryDirectory() as td:
-        src = os.path.join(td, "sample.bin")
-        data.tofile(src)
-        if enc_exe and dec_exe:
-            kind_s = "reference"
-            t0 = time.perf_counter()
-            subprocess.run([enc_exe, "sample.bin"], cwd=td, check=True, capture_output=True)
-            t1 = time.perf_counter()
-            subprocess.run([dec_exe, "sample.bin.compressed"], cwd=td, check=True, capture_output=True)
-            t2 = time.perf_counter()
-            with open(os.path.join(td, "DECOMPRESSED_FILE"), "rb") as f:
-                ok = f.read() == data.tobytes()
-        else:  # restatement in C (port), same work
-            kind_s = "port"
-            t0 = time.perf_counter()
-            blob = oracle_lib.encode(data)
-            t1 = time.perf_counter()
-            ok = oracle_lib.decode(blob) == data.tobytes()
-            t2 = time.perf_counter()
-    enc_s, dec_s = t1 - t0, t2 - t1
+    if not (enc_exe and dec_exe):  # restatement in C (port): one process, same work
+        data = oracle_lib.generate(sample_bytes, offset=0, kind=kind, seed=42)
+        t0 = time.perf_counter()
+        blob = oracle_lib.encode(data)
+        ok = oracle_lib.decode(blob) == data.tobytes()
+        t = time.perf_counter() - t0
+        return {"value": round(sample_bytes / t / 1e9, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+                "sample": f"{sample_bytes >> 20} MiB prefix, oracle encode + decode, one process; round trip "
+                          f"{'ok' if ok else 'FAILED'}", "cpu_model": model}
+    with tempfile.TemporaryDirectory() as root:
+        def stage(i, nbytes):
+            d = os.path.join(root, f"p{i}")
+            os.makedirs(d)
+            data = oracle_lib.generate(nbytes, offset=i * nbytes, kind=kind, seed=42)
+            data.tofile(os.path.join(d, "sample.bin"))
+            return (enc_exe, dec_exe, d, data.tobytes())
+        one = _baseline_run(stage(0, sample_bytes))
+        jobs = [stage(1000 + i, par_sample_bytes) for i in range(cores)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=cores) as ex:
+            res = list(ex.map(_baseline_run, jobs))
+        wall = time.perf_counter() - t0
+    ok = one[3] and all(r[3] for r in res)
+    agg = cores * par_sample_bytes / wall / 1e9
     return {
-        "value": round(sample_bytes / (enc_s + dec_s) / 1e9, 5),
+        "value": round(agg, 5),
         "unit": "GB/s",
-        "cores": 1,
-        "kind": kind_s,
-        "sample": f"{sample_bytes >> 20} MiB prefix of the same synthetic stream (seed 42), "
-                  f"baseline/Compressor.cu then baseline/Decompressor.cu, one process, wall clock; "
-                  f"encode {enc_s:.2f} s, decode {dec_s:.2f} s, round trip {'ok' if ok else 'FAILED'}",
-        "encode_GBps": round(sample_bytes / enc_s / 1e9, 5),
-        "decode_GBps": round(sample_bytes / dec_s / 1e9, 5),
+        "cores": cores,
+        "kind": "reference",
+        "cpu_model": model,
+        "sample": f"reference baseline/Compressor.cu then baseline/Decompressor.cu (g++ -O3) on the same synthetic "
+                  f"stream (seed 42): {cores} concurrent processes, one per core, each its own "
+                  f"{par_sample_bytes >> 20} MiB slice in its own CWD ({wall:.2f} s wall); one process on the "
+                  f"first {sample_bytes >> 20} MiB: encode {one[0]:.2f} s, decode {one[1]:.2f} s; round trips "
+                  f"{'ok' if ok else 'FAILED'}",
+        "one_process_GBps": round(sample_bytes / one[2] / 1e9, 5),
+        "one_process_encode_GBps": round(sample_bytes / one[0] / 1e9, 5),
+        "one_process_decode_GBps": round(sample_bytes / one[1] / 1e9, 5),
     }
 
 
@@ -161,6 +203,7 @@ def main():
         out.copy_(torch.cat(parts))
 
     from huffman_amd.codec import build_codebook, payload_bits
+    from huffman_amd._lib import build_id
     from huffman_amd.pipeline import StreamCodec
 
     codec = StreamCodec(local)
@@ -264,7 +307,8 @@ def main():
                 with open(args.profile_json) as f:
                     pmc = json.load(f)
                 ent = pmc.get(args.dist, {}).get(dom)
-                if ent and ent.get("size") == N:
+                # only counters of this very build (same sources) and this input size count
+                if ent and ent.get("size") == N and ent.get("build_id") == build_id():
                     traffic = ent["hbm_bytes_per_launch"]
                     pmc_src = os.path.relpath(args.profile_json, ROOT)
             except Exception:
@@ -306,6 +350,15 @@ def main():
             "host_decode_tables_ms_overlapped": round(float(np.mean(host_dec_ms)), 3),
             "encode_GBps_kernels": round(N / (enc_ms / 1e3) / 1e9, 1),
             "decode_GBps_kernel": round(N / (avg["decode"] / 1e3) / 1e9, 1),
+            # what `extract` of a real (index-less) file costs beside the encode: hist -> pack ->
+            # index rebuilt from the payload alone -> decode (kernel times, data resident)
+            "file_roundtrip": {
+                "ms": round(avg["hist"] + avg["pack"] + index_build["ms"] + avg["decode"], 3),
+                "GBps_of_input": round(N / ((avg["hist"] + avg["pack"] + index_build["ms"] + avg["decode"]) / 1e3)
+                                       / 1e9, 1),
+                "extract_ms": round(index_build["ms"] + avg["decode"], 3),
+                "extract_GBps_of_output": round(N / ((index_build["ms"] + avg["decode"]) / 1e3) / 1e9, 1),
+            },
             "reassembly_outside_step": reassembly,
             "roofline": {
                 "kernel": dom,
@@ -316,11 +369,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
                 "traffic_source": pmc_src,
+                "build_id": build_id(),
                 "algorithmic_bytes_per_launch": algo[dom],
             },
         }
         if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, kind)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, kind, args.cpu_par_sample_mib << 20)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -93,6 +93,16 @@ PROTOTYPES = [
 _lib = None
 
 
+def build_id():
+    """Source hash the in-tree library was built from (huffman_amd/build.py), or None."""
+    path = os.path.join(os.path.dirname(LIB_PATH), "BUILD_ID")
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def load():
     """Load libhuffman_amd.so (building nothing). Raises ImportError if absent."""
     global _lib

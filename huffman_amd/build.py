@@ -5,6 +5,7 @@ Outputs (git-ignored, shipped to the GPU box with the tree):
   huffman_amd/bin/archive             drop-in for the reference `archive`
   huffman_amd/bin/extract             drop-in for the reference `extract`
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -15,6 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 OBJ = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "lib", "libhuffman_amd.so")
+BUILD_ID = os.path.join(PKG, "lib", "BUILD_ID")  # hash of the sources the library was built from
 BIN = os.path.join(PKG, "bin")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -43,6 +45,15 @@ def _run(cmd, verbose):
         sys.stderr.write(r.stdout + r.stderr)
 
 
+def source_id():
+    """sha256 (16 hex digits) of every source and header the library is built from."""
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in LIB_SOURCES] + HEADERS:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def build(verbose=False, force=False):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -57,6 +68,10 @@ def build(verbose=False, force=False):
             _run([HIPCC] + CFLAGS + lang + ["-c", path, "-o", obj], verbose)
     if force or _stale(LIB, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs, verbose)
+    sid = source_id()
+    if not os.path.exists(BUILD_ID) or open(BUILD_ID).read().strip() != sid:
+        with open(BUILD_ID, "w") as f:
+            f.write(sid + "\n")
     for name in ("archive", "extract"):
         src = os.path.join(CSRC, f"cli_{name}.cpp")
         out = os.path.join(BIN, name)

@@ -1,6 +1,6 @@
 """Profiling harness: encode one synthetic stream on the device, then run
 pack and decode R more times (rocprofv3 --pmc passes attribute counters per kernel).
-usage: python tools/debug/stage_loop.py [bytes] [reps] [zipf|uniform] [stages]"""
+usage: python tools/debug/stage_loop.py [bytes] [reps] [zipf|uniform] [stages: h p d i]"""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
@@ -21,6 +21,9 @@ for r in range(reps):
         c.pack(x, plan, pay, idx)
     if "d" in stages:
         c.decode(pay, n // 2, idx, out)
+    if "i" in stages:
+        c.dev.index_build(pay.data_ptr(), pay.numel(), plan.start_bit, n // 2, idx.data_ptr())
     c.sync()
-    print("rep", r, c.kernel_ms(), flush=True)
+    from huffman_amd._lib import STAGE_INDEX
+    print("rep", r, c.kernel_ms(), "index", c.dev.kernel_ms(STAGE_INDEX), flush=True)
 print('ok', torch.equal(out[:n - (n & 1)], x[:n - (n & 1)]))

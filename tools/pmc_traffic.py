@@ -29,6 +29,9 @@ STAGES = {
     "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16"),
              ("k_pack_write", "k_pack_fixed16")),
     "decode": (("k_decode", "k_decode_fixed16"), ("k_decode", "k_decode_fixed16")),
+    "index": (("k_idx_scan", "k_idx_iter", "k_idx_emit", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2",
+               "k_sync_iter", "k_sync_emit", "k_sync_emit2", "k_sync_subs"),
+              ("k_idx_emit", "k_idx_fixed16", "k_sync_emit", "k_sync_emit2")),
 }
 
 
@@ -71,6 +74,11 @@ def main():
     fetch, fcalls = read_counter(a.fetch, "FETCH_SIZE")
     write, wcalls = read_counter(a.write, "WRITE_SIZE")
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        bid = open(os.path.join(root, "huffman_amd", "lib", "BUILD_ID")).read().strip()
+    except OSError:
+        bid = None
     ent = {}
     for st in STAGES:
         if st not in fetch or st not in write:
@@ -85,6 +93,7 @@ def main():
             "hbm_bytes_per_launch": round(f + w),
             "dispatches": {"fetch_pass": fcalls.get(st, 0), "write_pass": wcalls.get(st, 0)},
             "correction": "fetch = 2 x FETCH_SIZE (gfx950 wide-read undercount); write = WRITE_SIZE",
+            "build_id": bid,
         }
     res[a.dist] = ent
     with open(a.out, "w") as f:
