@@ -30,6 +30,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,6 +55,16 @@ def parse():
 def _cpu_info():
     """Cores this process may use (the box's CPU share) and the host CPU model."""
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # the CPU share of this job: the cgroup quota, else OMP_NUM_THREADS (affinity shows the whole machine)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            cores = min(cores, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -104,6 +119,7 @@ def cpu_baseline(sample_bytes, kind, par_sample_bytes):
             data.tofile(os.path.join(d, "sample.bin"))
             return (enc_exe, dec_exe, d, data.tobytes())
         one = _baseline_run(stage(0, sample_bytes))
+        log(f"CPU baseline: one process done ({one[2]:.1f} s); {cores} concurrent processes")
         jobs = [stage(1000 + i, par_sample_bytes) for i in range(cores)]
         t0 = time.perf_counter()
         with ThreadPoolExecutor(max_workers=cores) as ex:
@@ -247,9 +263,11 @@ def main():
         state["header"] = plan.header  # the .compressed header, written on the host while the GPU runs
         state["plan"] = plan
 
+    log(f"rank {rank}: {N} bytes generated; {args.warmup} warmup steps")
     for _ in range(args.warmup):
         step()
     codec.sync()
+    log(f"rank {rank}: {args.steps} timed steps")
     kms = {"hist": [], "pack": [], "decode": []}
     host_ms = []
     host_dec_ms = []
@@ -271,6 +289,7 @@ def main():
     codec.sync()  # surfaces device-side errors (capacity, format)
     ok = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
     plan = state["plan"]
+    log(f"rank {rank}: {elapsed * 1e3 / args.steps:.3f} ms/step; index rebuild from the payload")
     # Index-less decode path (reference-produced files): rebuild the block index
     # from the payload alone, outside the timed loop, and check it against pack's.
     from huffman_amd import index_bytes
@@ -374,6 +393,7 @@ def main():
             },
         }
         if not args.no_cpu_baseline:
+            log("CPU baseline (reference baseline/ encoder + decoder)")
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, kind, args.cpu_par_sample_mib << 20)
         print(json.dumps(line), flush=True)
     if world > 1:

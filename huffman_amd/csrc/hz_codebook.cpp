@@ -534,121 +534,4 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     return HZ_OK;
 }
 
-// Length-only table for the index builder's walks (they need code lengths,
-// never symbols), three levels, all of it in one CU's LDS:
-//   level 1: 2^K1 u32. A leaf is its length L <= K1. A link is
-//            bit 31 | header word << 3 | nb2 (nb2 = min(K2, deepest code
-//            below the prefix - K1) <= 6).
-//   header : three words -- a 64-bit mask of the level-2 entries that go
-//            deeper, and the level-3 base (nibble index) | md3 << 28 -- then
-//            the prefix's 2^nb2 level-2 nibbles: L - K1, or 15 for "deeper".
-//   level 3: per deeper level-2 entry (in order, found by a popcount of the
-//            mask below it) 2^md3 nibbles L - K1 - nb2.
-// K1, K2 are the pair whose image is smallest; HZ_ENOMEM when even that
-// exceeds max_bytes (the walks then use the symbol LUT with global levels).
-// Unused windows of an incomplete code read as length 1, so a walk always
-// advances.
-int build_len_table(const hz_codebook* cb, uint32_t max_bytes, std::vector<uint32_t>& img, int& K1_out,
-                    uint32_t& l1_words) {
-    const int maxL = (int)cb->max_len;
-    if (maxL < 1 || maxL > 32) return HZ_ENOMEM;
-    std::vector<uint32_t> syms;
-    for (uint32_t s = 0; s < HZ_NSYM; ++s)
-        if (cb->len[s]) syms.push_back(s);
-    struct Pre { int md = 0, nb2 = 0, md3 = 0; uint64_t mask = 0; };
-    auto plan = [&](int k1, int k2, std::vector<Pre>& pre) -> uint64_t {
-        pre.assign(1u << k1, Pre());
-        for (uint32_t s : syms) {
-            const int L = cb->len[s];
-            if (L <= k1) continue;
-            Pre& p = pre[(uint32_t)(cb->code[s] >> (L - k1))];
-            p.md = std::max(p.md, L - k1);
-        }
-        for (auto& p : pre) p.nb2 = std::min(p.md, k2);
-        for (uint32_t s : syms) {
-            const int L = cb->len[s];
-            if (L <= k1) continue;
-            Pre& p = pre[(uint32_t)(cb->code[s] >> (L - k1))];
-            const int r = L - k1;
-            if (r <= p.nb2) continue;
-            const uint32_t r2 = (uint32_t)(cb->code[s] >> (r - p.nb2)) & ((1u << p.nb2) - 1);
-            p.mask |= 1ull << r2;
-            p.md3 = std::max(p.md3, r - p.nb2);
-        }
-        uint64_t words = 1ull << k1, nib3 = 0;
-        for (auto& p : pre) {
-            if (!p.md) continue;
-            if (p.md3 > 15) return ~0ull;
-            words += 3 + ((1ull << p.nb2) + 7) / 8;
-            nib3 += (uint64_t)__builtin_popcountll(p.mask) << p.md3;
-        }
-        return 4 * words + (nib3 + 1) / 2;
-    };
-    int bk1 = -1, bk2 = -1;
-    uint64_t best = ~0ull;
-    std::vector<Pre> pre;
-    for (int k1 = 1; k1 <= std::min(maxL, 14); ++k1)
-        for (int k2 = 1; k2 <= 6; ++k2) {
-            const uint64_t b = plan(k1, k2, pre);
-            if (b < best) { best = b; bk1 = k1; bk2 = k2; }
-        }
-    if (bk1 < 0 || best + 16 > max_bytes) return HZ_ENOMEM;
-    const int k1 = bk1;
-    plan(k1, bk2, pre);
-    // layout: level 1, then header + level 2 per link prefix, then level 3
-    std::vector<uint32_t> hdr_word(1u << k1, 0u);
-    uint64_t words = 1ull << k1;
-    for (uint32_t q = 0; q < (1u << k1); ++q)
-        if (pre[q].md) { hdr_word[q] = (uint32_t)words; words += 3 + ((1ull << pre[q].nb2) + 7) / 8; }
-    uint64_t nib3 = 8 * words;  // level 3 starts right after, addressed in nibbles from the image start
-    std::vector<uint64_t> base3(1u << k1, 0);
-    for (uint32_t q = 0; q < (1u << k1); ++q)
-        if (pre[q].md) { base3[q] = nib3; nib3 += (uint64_t)__builtin_popcountll(pre[q].mask) << pre[q].md3; }
-    if (nib3 >= (1ull << 28)) return HZ_ENOMEM;
-    img.assign((nib3 + 7) / 8 + 4, 0u);
-    uint8_t* b8 = reinterpret_cast<uint8_t*>(img.data());
-    auto put_nib = [&](uint64_t j, uint32_t v) { b8[j >> 1] = (uint8_t)((b8[j >> 1] & ~(0xfu << ((j & 1) * 4))) | (v << ((j & 1) * 4))); };
-    for (uint32_t q = 0; q < (1u << k1); ++q) {
-        const Pre& p = pre[q];
-        if (!p.md) continue;
-        img[q] = 0x80000000u | (hdr_word[q] << 3) | (uint32_t)p.nb2;
-        img[hdr_word[q]] = (uint32_t)p.mask;
-        img[hdr_word[q] + 1] = (uint32_t)(p.mask >> 32);
-        img[hdr_word[q] + 2] = (uint32_t)base3[q] | ((uint32_t)p.md3 << 28);
-        const uint64_t n2 = 8ull * (hdr_word[q] + 3);
-        for (uint32_t r2 = 0; r2 < (1u << p.nb2); ++r2) put_nib(n2 + r2, ((p.mask >> r2) & 1) ? 15u : 1u);
-        const uint32_t ndeep = (uint32_t)__builtin_popcountll(p.mask);
-        for (uint64_t j = 0; j < ((uint64_t)ndeep << p.md3); ++j) put_nib(base3[q] + j, 1u);
-    }
-    for (uint32_t s : syms) {
-        const int L = cb->len[s];
-        const uint64_t c = cb->code[s];
-        if (L <= k1) {
-            for (uint64_t e = c << (k1 - L); e < (c + 1) << (k1 - L); ++e) img[e] = (uint32_t)L;
-            continue;
-        }
-        const uint32_t q = (uint32_t)(c >> (L - k1));
-        const Pre& p = pre[q];
-        const int r = L - k1;
-        const uint64_t n2 = 8ull * (hdr_word[q] + 3);
-        if (r <= p.nb2) {
-            const uint64_t bits = c & ((1ull << r) - 1);
-            for (uint64_t e = bits << (p.nb2 - r); e < (bits + 1) << (p.nb2 - r); ++e) put_nib(n2 + e, (uint32_t)r);
-        } else {
-            const uint32_t r2 = (uint32_t)(c >> (r - p.nb2)) & ((1u << p.nb2) - 1);
-            const uint32_t rank = (uint32_t)__builtin_popcountll(p.mask & ((1ull << r2) - 1));
-            const int r3 = r - p.nb2;
-            const uint64_t bits = c & ((1ull << r3) - 1);
-            const uint64_t b3 = base3[q] + ((uint64_t)rank << p.md3);
-            for (uint64_t e = bits << (p.md3 - r3); e < (bits + 1) << (p.md3 - r3); ++e) put_nib(b3 + e, (uint32_t)r3);
-        }
-    }
-    for (uint32_t q = 0; q < (1u << k1); ++q)
-        if (!img[q]) img[q] = 1u;   // filler: advance one bit
-    while (img.size() & 3) img.push_back(0u);
-    K1_out = k1;
-    l1_words = 1u << k1;
-    return HZ_OK;
-}
-
 }  // namespace hz

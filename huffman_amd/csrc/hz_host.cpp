@@ -31,8 +31,6 @@ std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
-int build_len_table(const hz_codebook* cb, uint32_t max_bytes, std::vector<uint32_t>& img, int& K1_out,
-                    uint32_t& l1_words);
 }  // namespace hz
 
 using namespace hz;
@@ -74,8 +72,7 @@ struct hz_ctx {
     hipEvent_t ev[4][2] = {};
     bool ev_used[4] = {false, false, false, false};
     Staging stage_enc, stage_dec;
-    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0,
-           cap_len_lds = 0;
+    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0;
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -104,7 +101,6 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_len8);
     (void)hipFree(t.d_dec_lds);
     (void)hipFree(t.d_dec_l2);
-    (void)hipFree(t.d_len_lds);
     t = Tables();
 }
 
@@ -314,19 +310,6 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
-    // length-only table of the index builder's walks, when it fits one CU's LDS
-    t.len_bytes = 0;
-    if (mode != DEC_FIXED16) {
-        std::vector<uint32_t> limg;
-        int lk = 0;
-        uint32_t l1w = 0;
-        if (build_len_table(cb, kLenTableMaxBytes, limg, lk, l1w) == HZ_OK) {
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_len_lds, &c->cap_len_lds, limg))) return rc;
-            t.len_bytes = (uint32_t)(limg.size() * 4);
-            t.len_l1_words = l1w;
-            t.len_k = lk;
-        }
-    }
     HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
     t.dec_mode = mode;
     return HZ_OK;

@@ -93,12 +93,7 @@ struct Tables {
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
     uint64_t dec_l2_entries = 0;
-    uint32_t* d_len_lds = nullptr; // index builder: length-only table image (0 bytes: none fits LDS)
-    uint32_t len_bytes = 0;
-    uint32_t len_l1_words = 0;
-    int len_k = 0;
 };
-constexpr uint32_t kLenTableMaxBytes = 160u * 1024u;  // length-only table: all of it in one CU's LDS
 
 // Count-pass length table layout: the high byte is XORed into the bank bits
 // so skewed symbol sets (small high and low bytes) spread over LDS banks.

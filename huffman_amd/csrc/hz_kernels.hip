@@ -2174,333 +2174,12 @@ __global__ __launch_bounds__(256) void k_sync_subs(uint64_t nsym, uint64_t nbloc
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(starts + nblocks + 1, mx);
 }
 
-// ---------------------------------------------------------------------------
-// Index builder on a length-only LDS table (hz_codebook.cpp build_len_table):
-// the walks need code lengths, never symbols, and the whole length table of
-// the configs' codebooks fits one CU's LDS, so no walk step leaves the CU.
-//   k_idx_scan : per 4096-bit segment, decode from its first bit to the first
-//                boundary past its end -> exit0, cnt0 (no bitmap)
-//   k_idx_iter : the true path enters at the previous exit; walk it and the
-//                scan path together (the one behind advances) until they meet
-//                (then count and exit follow from the scan) or the true path
-//                leaves the segment; host loop until no exit changes
-//   k_scan_*   : first codeword number per segment
-//   k_idx_emit : decode each segment from its true entry, recording block
-//                starts and the position of every 8th codeword (a u64 store of
-//                four positions per 32 codewords once aligned)
-//   k_sync_subs: positions relative to their block, largest block
-// Each lane walks four segments in lockstep, branch-free. Its bits come from
-// a register ring of 16-byte chunks (two being read, one ready, one in
-// flight): every fourth step each chain issues exactly one chunk load -- the
-// next chunk when it rotated its ring, else the same chunk again -- so every
-// load wait is static.
-// ---------------------------------------------------------------------------
-constexpr int kWalkChains = 4;
-constexpr uint32_t kWalkSegBits = 1024;  // segment of the length-table walks
-constexpr int kWalkThreads = 768;      // scan: 160 VGPRs, three waves per SIMD
-constexpr int kEmitThreads = 768;
-
-struct LenArgs {
-    const uint32_t* words;   // payload view (64-byte aligned), as DecArgs
-    uint64_t nwords;
-    uint32_t bit_adj;
-    const uint32_t* img;     // length table image: l1 u32[l1_words], then l2 nibbles
-    uint32_t img_words;
-    uint32_t l1_words;
-    uint32_t k;
-    uint64_t start;          // stream bit of the first codeword
-    uint64_t nseg;
-    uint32_t seg;            // segment bits
-    uint64_t nsym;
-    uint64_t nblocks;
-    uint32_t* err;
-};
-
-// Length of the codeword at the top of W from the three-level length table
-// (hz_codebook.cpp build_len_table), branch-free: lanes that stop at level 1
-// or 2 read word 0 / nibble 0 (broadcast) for the levels they skip.
-HZ_DEV uint32_t len_of(const uint32_t* img, uint32_t k, uint32_t W) {
-    const uint8_t* b8 = reinterpret_cast<const uint8_t*>(img);
-    const uint32_t e = img[W >> (32 - k)];
-    const bool link = e >> 31;
-    const uint32_t nb2 = link ? (e & 7u) : 1u;
-    const uint32_t hw = link ? (e >> 3) & 0x0fffffffu : 0u;
-    const uint32_t r2 = (W << k) >> (32 - nb2);
-    const uint32_t m0 = img[hw], m1 = img[hw + 1], b3 = img[hw + 2];
-    const uint32_t n2 = (hw + 3) * 8 + r2;
-    const uint32_t v2 = ((uint32_t)b8[n2 >> 1] >> ((n2 & 1u) << 2)) & 15u;
-    const bool deep = link && v2 == 15u;
-    const uint32_t lo = r2 >= 32 ? m0 : (m0 & ((1u << r2) - 1u));
-    const uint32_t hi = r2 <= 32 ? 0u : (m1 & ((1u << (r2 - 32)) - 1u));
-    const uint32_t rank = (uint32_t)__popc(lo) + (uint32_t)__popc(hi);
-    const uint32_t md3 = deep ? (b3 >> 28) : 1u;
-    const uint32_t r3 = (W << (k + nb2)) >> (32 - md3);
-    const uint32_t n3 = deep ? (b3 & 0x0fffffffu) + (rank << md3) + r3 : 0u;
-    const uint32_t v3 = ((uint32_t)b8[n3 >> 1] >> ((n3 & 1u) << 2)) & 15u;
-    return !link ? (e & 63u) : (!deep ? k + v2 : k + nb2 + v3);
-}
-
-// Chunk q (16 raw payload bytes): always exactly one load. Chunks past the
-// payload read its last chunk again, and the words of that chunk past the
-// payload are whatever the allocation holds there (the same 16-byte aligned
-// chunk, so never another page): either only ever feeds walks past the
-// stream's last codeword, whose results are discarded.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native vector: SROA keeps the ring in VGPRs
-
-HZ_DEV u32x4 walk_load(const LenArgs& a, uint64_t q) {
-    const uint64_t qmax = (a.nwords - 1) >> 2;
-    return *reinterpret_cast<const u32x4*>(a.words + 4 * (q < qmax ? q : qmax));
-}
-
-struct Walk {
-    uint64_t buf;   // next bits, MSB first; nb of them valid (>= 32 between steps)
-    uint32_t nb;
-    uint32_t wi;    // next ring word to shift in (0..7)
-    u32x4 c0, c1;   // ring: chunks q0 and q0 + 1 (raw words)
-    u32x4 c2;       // chunk q0 + 2
-    u32x4 inc;      // chunk q0 + 3, in flight
-    uint64_t q0;
-};
-
-HZ_DEV uint32_t sel8(const u32x4& lo, const u32x4& hi, uint32_t i) {
-    const bool b0 = i & 1u, b1 = i & 2u, b2 = i & 4u;
-    const uint32_t a0 = b0 ? lo.y : lo.x, a1 = b0 ? lo.w : lo.z, a2 = b0 ? hi.y : hi.x, a3 = b0 ? hi.w : hi.z;
-    const uint32_t d0 = b1 ? a1 : a0, d1 = b1 ? a3 : a2;
-    return b2 ? d1 : d0;
-}
-
-// Issue a chain's first loads (view bit p); walk_start consumes them.
-HZ_DEV void walk_issue(const LenArgs& a, uint64_t p, Walk& r) {
-    r.q0 = (p >> 5) >> 2;
-    r.c0 = walk_load(a, r.q0);
-    r.c1 = walk_load(a, r.q0 + 1);
-    r.c2 = walk_load(a, r.q0 + 2);
-    r.inc = walk_load(a, r.q0 + 3);
-}
-
-HZ_DEV void walk_start(uint64_t p, Walk& r) {
-    const uint32_t wi = (uint32_t)((p >> 5) & 3), sh = (uint32_t)(p & 31);
-    const uint64_t two = ((uint64_t)bswap32(sel8(r.c0, r.c1, wi)) << 32) | bswap32(sel8(r.c0, r.c1, wi + 1));
-    r.buf = two << sh;
-    r.nb = 64 - sh;
-    r.wi = wi + 2;
-}
-
-// Static point (every fourth step): rotate the ring once chunk q0 is used up,
-// then one chunk load per chain.
-HZ_DEV void walk_rotate(const LenArgs& a, Walk& r) {
-#ifdef HZ_WALK_VMCNT0
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // DEBUG: vmcnt(0)
-#endif
-    const bool rot = r.wi >= 4;
-    r.c0 = rot ? r.c1 : r.c0;
-    r.c1 = rot ? r.c2 : r.c1;
-    r.c2 = rot ? r.inc : r.c2;
-    r.q0 += rot ? 1 : 0;
-    r.wi -= rot ? 4u : 0u;
-    r.inc = walk_load(a, r.q0 + 3);
-}
-
-HZ_DEV uint32_t walk_window(const Walk& r) { return (uint32_t)(r.buf >> 32); }
-
-// Consume L bits (when `go`) and top the buffer back up to >= 32 bits.
-HZ_DEV void walk_adv(Walk& r, uint32_t L, bool go) {
-    L = go ? L : 0u;
-    const uint64_t b = r.buf << L;
-    const uint32_t nb = r.nb - L;
-    const bool need = nb < 32;
-    const uint32_t w = bswap32(sel8(r.c0, r.c1, r.wi & 7u));
-    r.buf = need ? (b | ((uint64_t)w << (32 - nb))) : b;
-    r.nb = need ? nb + 32 : nb;
-    r.wi += need ? 1u : 0u;
-}
-
-HZ_DEV void len_table_to_lds(uint32_t* lds, const LenArgs& a) {
-    const uint4* src = reinterpret_cast<const uint4*>(a.img);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
-    for (uint32_t i = threadIdx.x; i < a.img_words / 4; i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(kWalkThreads) void k_idx_scan(LenArgs a, unsigned long long* exit0,
-                                                          unsigned long long* cnt0) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    constexpr int C = kWalkChains;
-    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t groups = (a.nseg + C - 1) / C;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += lanes) {
-        Walk r[C];
-        uint64_t s0[C];
-        uint32_t x[C], n[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const uint64_t k = C * g + c < a.nseg ? C * g + c : a.nseg - 1;
-            s0[c] = a.start + k * a.seg;
-            x[c] = C * g + c < a.nseg ? 0u : a.seg;  // past the last segment: never active
-            n[c] = 0;
-            walk_issue(a, s0[c] + a.bit_adj, r[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) walk_start(s0[c] + a.bit_adj, r[c]);
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < C; ++c) any |= x[c] < a.seg;
-            if (!__any(any)) break;
-#pragma unroll
-            for (int c = 0; c < C; ++c) walk_rotate(a, r[c]);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                uint32_t L[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) L[c] = len_of(lds, a.k, walk_window(r[c]));
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const bool act = x[c] < a.seg;
-                    x[c] += act ? L[c] : 0u;
-                    n[c] += act ? 1u : 0u;
-                    walk_adv(r[c], L[c], true);
-                }
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            if (C * g + c < a.nseg) {
-                exit0[C * g + c] = s0[c] + x[c];
-                cnt0[C * g + c] = n[c];
-            }
-    }
-}
-
-// Length of the codeword at a per-lane BitReader, then advance past it.
-HZ_DEV uint32_t br_len_next(BitReader& r, const LenArgs& a, const uint32_t* lds) {
-    br_refill(r, a);
-    const uint32_t L = len_of(lds, a.k, (uint32_t)(r.buf >> 32));
-    if (L < r.nb) {
-        r.buf <<= L;
-        r.nb -= L;
-    } else {
-        const uint32_t rr = L - r.nb;
-        r.buf = (uint64_t)r.nxt << (32 + rr);
-        r.nb = 32 - rr;
-        r.nxt = br_word(r, a);
-    }
-    return L;
-}
-
-// Entry fix-up: the true path (from the previous segment's exit) and the scan
-// path (from the segment's first bit) advance, the one behind first, until
-// they meet on a boundary (from there both paths agree) or the true path
-// leaves the segment. Iteration 0 takes every segment; later iterations only
-// the worklist of segments whose entry changed (dirty[it & 1], `nwork` long).
-__global__ __launch_bounds__(1024) void k_idx_iter(LenArgs a, SyncArgs y, int it, uint32_t nwork) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    const unsigned long long* exr = y.ex[it & 1];
-    unsigned long long* exw = y.ex[(it + 1) & 1];
-    const uint32_t* work = y.dirty[it & 1];
-    uint32_t* next = y.dirty[(it + 1) & 1];
-    const uint64_t n_items = it == 0 ? y.nseg : nwork;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_items; w += stride) {
-        const uint64_t k = it == 0 ? w : work[w];
-        if (k == 0) { exw[0] = y.exit0[0]; y.cnt[0] = y.cnt0[0]; continue; }
-        const uint64_t s0 = a.start + k * a.seg, s1 = s0 + a.seg;
-        uint64_t pa = it == 0 ? y.exit0[k - 1] : exr[k - 1], pb = s0;
-        uint64_t na = 0, nb = 0, ex, n;
-        BitReader ra, rb;
-        br_init(ra, a, pa + a.bit_adj);
-        br_init(rb, a, pb + a.bit_adj);
-        for (;;) {
-            if (pa == pb) { n = y.cnt0[k] - nb + na; ex = y.exit0[k]; break; }
-            if (pa >= s1) { n = na; ex = pa; break; }
-            if (pb < pa) { pb += br_len_next(rb, a, lds); ++nb; }
-            else { pa += br_len_next(ra, a, lds); ++na; }
-        }
-        y.cnt[k] = n;
-        const uint64_t prev = it == 0 ? y.exit0[k] : exr[k];
-        // both exit buffers carry every segment's latest exit (readers of the next iteration use exw)
-        exw[k] = ex;
-        if (it > 0) y.ex[it & 1][k] = ex;
-        if (ex != prev && k + 1 < y.nseg) next[atomicAdd(y.changed, 1u)] = (uint32_t)(k + 1);
-    }
-}
-
-// Decode each segment from its true entry; codeword i (global) starts at pos:
-// every 8th codeword's position goes to sub[] (a u16 store), every 2048th to
-// start[]. A chain walks exactly the codewords its segment holds (at most
-// nsym in all), so the walks end together within a few steps.
-__global__ __launch_bounds__(kEmitThreads) void k_idx_emit(LenArgs a, const unsigned long long* exits,
-                                                          const unsigned long long* cnt,
-                                                          const unsigned long long* first,
-                                                          unsigned long long* starts, uint16_t* subs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    constexpr int C = kWalkChains;
-    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t groups = (a.nseg + C - 1) / C;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += lanes) {
-        Walk r[C];
-        uint64_t e[C], i0[C];
-        uint32_t x[C], j[C], m[C];  // bits and codewords walked from the entry; codewords to walk
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const uint64_t k = C * g + c < a.nseg ? C * g + c : a.nseg - 1;
-            e[c] = k ? exits[k - 1] : a.start;
-            i0[c] = first[k];
-            const uint64_t avail = i0[c] < a.nsym ? a.nsym - i0[c] : 0;
-            m[c] = C * g + c < a.nseg ? (uint32_t)(cnt[k] < avail ? cnt[k] : avail) : 0u;
-            x[c] = 0;
-            j[c] = 0;
-            walk_issue(a, e[c] + a.bit_adj, r[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) walk_start(e[c] + a.bit_adj, r[c]);
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < C; ++c) any |= j[c] < m[c];
-            if (!__any(any)) break;
-#pragma unroll
-            for (int c = 0; c < C; ++c) walk_rotate(a, r[c]);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                uint32_t L[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) L[c] = len_of(lds, a.k, walk_window(r[c]));
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const bool go = j[c] < m[c];
-                    const uint64_t i = i0[c] + j[c];
-                    if (go && (i & (kChainSyms - 1)) == 0) {
-                        const uint64_t pos = e[c] + x[c];
-                        subs[i / kChainSyms] = (uint16_t)pos;
-                        if ((i & (kBlockSyms - 1)) == 0) starts[i / kBlockSyms] = pos;
-                    }
-                    x[c] += go ? L[c] : 0u;
-                    j[c] += go ? 1u : 0u;
-                    walk_adv(r[c], L[c], go);
-                }
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            if (m[c] > 0 && i0[c] + m[c] == a.nsym) starts[a.nblocks] = e[c] + x[c];
-    }
-}
-
-constexpr uint32_t kWalkSegBitsMin = 256;  // smallest segment the length-table walks use
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // symbol-LUT walks: exit0, cnt0, ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
-    const uint64_t lut = nseg * (6 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
-    // length-table walks: the same without the bitmap, over segments as small as kWalkSegBitsMin
-    const uint64_t nw = (bits + kWalkSegBitsMin - 1) / kWalkSegBitsMin;
-    const uint64_t len = nw * 7 + 1 + (nw + kScanTile - 1) / kScanTile + 8;
-    return lut > len ? lut : len;
+    // exit0, cnt0, ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
+    return nseg * (6 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
 }
 
 template <int MODE>
@@ -2562,134 +2241,6 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_idx_emit_br(LenArgs a, const unsigned long long* exits,
-                                                     const unsigned long long* cnt, const unsigned long long* first,
-                                                     unsigned long long* starts, uint16_t* subs) {  // DEBUG
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nseg; k += stride) {
-        uint64_t pos = k ? exits[k - 1] : a.start, i = first[k];
-        const uint64_t avail = i < a.nsym ? a.nsym - i : 0;
-        uint64_t rem = cnt[k] < avail ? cnt[k] : avail;
-        const bool last = rem && i + rem == a.nsym;
-        BitReader r;
-        br_init(r, a, pos + a.bit_adj);
-        for (; rem; --rem) {
-            if ((i & 7) == 0) subs[i / 8] = (uint16_t)pos;
-            if ((i & 2047) == 0) starts[i / 2048] = pos;
-            pos += br_len_next(r, a, lds);
-            ++i;
-        }
-        if (last) starts[a.nblocks] = pos;
-    }
-}
-
-// The same walks on per-chain BitReaders (a 16-byte chunk in flight while the
-// previous one is used: about ten codewords of lookahead per load).
-template <int NC>
-__global__ __launch_bounds__(kWalkThreads) void k_idx_scan_r(LenArgs a, unsigned long long* exit0,
-                                                            unsigned long long* cnt0) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t groups = (a.nseg + NC - 1) / NC;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += lanes) {
-        BitReader r[NC];
-        uint64_t s0[NC];
-        uint32_t x[NC], n[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const uint64_t k = NC * g + c < a.nseg ? NC * g + c : a.nseg - 1;
-            s0[c] = a.start + k * a.seg;
-            x[c] = NC * g + c < a.nseg ? 0u : a.seg;
-            n[c] = 0;
-            br_init(r[c], a, s0[c] + a.bit_adj);
-        }
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) any |= x[c] < a.seg;
-            if (!__any(any)) break;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) br_refill(r[c], a);
-            uint32_t L[NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) L[c] = len_of(lds, a.k, (uint32_t)(r[c].buf >> 32));
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const bool act = x[c] < a.seg;
-                r[c].buf <<= L[c];
-                r[c].nb -= L[c];
-                x[c] += act ? L[c] : 0u;
-                n[c] += act ? 1u : 0u;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-            if (NC * g + c < a.nseg) {
-                exit0[NC * g + c] = s0[c] + x[c];
-                cnt0[NC * g + c] = n[c];
-            }
-    }
-}
-
-template <int NC>
-__global__ __launch_bounds__(kEmitThreads) void k_idx_emit_r(LenArgs a, const unsigned long long* exits,
-                                                            const unsigned long long* cnt,
-                                                            const unsigned long long* first,
-                                                            unsigned long long* starts, uint16_t* subs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    len_table_to_lds(lds, a);
-    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t groups = (a.nseg + NC - 1) / NC;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += lanes) {
-        BitReader r[NC];
-        uint64_t e[NC], i0[NC];
-        uint32_t x[NC], j[NC], m[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const uint64_t k = NC * g + c < a.nseg ? NC * g + c : a.nseg - 1;
-            e[c] = k ? exits[k - 1] : a.start;
-            i0[c] = first[k];
-            const uint64_t avail = i0[c] < a.nsym ? a.nsym - i0[c] : 0;
-            m[c] = NC * g + c < a.nseg ? (uint32_t)(cnt[k] < avail ? cnt[k] : avail) : 0u;
-            x[c] = 0;
-            j[c] = 0;
-            br_init(r[c], a, e[c] + a.bit_adj);
-        }
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) any |= j[c] < m[c];
-            if (!__any(any)) break;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) br_refill(r[c], a);
-            uint32_t L[NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) L[c] = len_of(lds, a.k, (uint32_t)(r[c].buf >> 32));
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const bool go = j[c] < m[c];
-                const uint64_t i = i0[c] + j[c];
-                if (go && (i & (kChainSyms - 1)) == 0) {
-                    const uint64_t pos = e[c] + x[c];
-                    subs[i / kChainSyms] = (uint16_t)pos;
-                    if ((i & (kBlockSyms - 1)) == 0) starts[i / kBlockSyms] = pos;
-                }
-                const uint32_t l = go ? L[c] : 0u;
-                r[c].buf <<= l;
-                r[c].nb -= l;
-                x[c] += l;
-                j[c] += go ? 1u : 0u;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-            if (m[c] > 0 && i0[c] + m[c] == a.nsym) starts[a.nblocks] = e[c] + x[c];
-    }
-}
-
 // Every code 16 bits: codeword i starts at start + 16 i, so the index is
 // arithmetic (no walk). Same layout as k_pack_fixed16 writes.
 __global__ __launch_bounds__(256) void k_idx_fixed16(uint64_t start, uint64_t nsym, uint64_t nblocks,
@@ -2714,99 +2265,6 @@ __global__ __launch_bounds__(256) void k_idx_fixed16(uint64_t start, uint64_t ns
             index[nblocks + 1] = 16ull * (nsym < (uint64_t)kBlockSyms ? nsym : (uint64_t)kBlockSyms);
         }
     }
-}
-
-static hipError_t run_index_len(const Tables& t, const DecArgs& d, SyncArgs y, uint32_t seg, unsigned long long* first,
-                                unsigned long long* tiles, unsigned long long* d_index, uint32_t* h_changed, int ncu,
-                                hipStream_t s) {
-    LenArgs a;
-    a.words = d.words; a.nwords = d.nwords; a.bit_adj = d.bit_adj;
-    a.img = t.d_len_lds; a.img_words = t.len_bytes / 4; a.l1_words = t.len_l1_words; a.k = (uint32_t)t.len_k;
-    a.start = y.start; a.nseg = y.nseg; a.seg = seg; a.nsym = d.nsym; a.nblocks = d.nblocks; a.err = d.err;
-    const uint32_t lds = t.len_bytes;
-    for (const void* f : {(const void*)k_idx_scan, (const void*)k_idx_iter, (const void*)k_idx_emit}) {
-        hipError_t e = ensure_lds_limit(f, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    const uint64_t per_cu = lds <= kLdsBytes / 2 ? 2 : 1;
-    const uint64_t groups = (y.nseg + kWalkChains - 1) / kWalkChains;
-    uint64_t wgs = (groups + kWalkThreads - 1) / kWalkThreads;
-    wgs = wgs < (uint64_t)ncu * per_cu ? (wgs ? wgs : 1) : (uint64_t)ncu * per_cu;
-    static const int walk_kind = getenv("HZ_IDX_WALK") ? atoi(getenv("HZ_IDX_WALK")) : 0;  // DEBUG A/B
-    const void* scan_fn = walk_kind == 1 ? (const void*)k_idx_scan_r<1> : walk_kind == 2 ? (const void*)k_idx_scan_r<2> : walk_kind == 4 ? (const void*)k_idx_scan_r<4>
-                                                                                          : (const void*)k_idx_scan;
-    const void* emit_fn = walk_kind == 1 ? (const void*)k_idx_emit_r<1> : walk_kind == 2 ? (const void*)k_idx_emit_r<2> : walk_kind == 4 ? (const void*)k_idx_emit_r<4>
-                                                                                          : (const void*)k_idx_emit;
-    (void)ensure_lds_limit(scan_fn, (int)lds);
-    (void)ensure_lds_limit(emit_fn, (int)lds);
-    const uint64_t nc = walk_kind ? (uint64_t)walk_kind : (uint64_t)kWalkChains;
-    static const int wthreads = getenv("HZ_IDX_THREADS") ? atoi(getenv("HZ_IDX_THREADS")) : kWalkThreads;  // DEBUG
-    uint64_t swgs = ((y.nseg + nc - 1) / nc + wthreads - 1) / wthreads;
-    swgs = swgs < (uint64_t)ncu * per_cu ? (swgs ? swgs : 1) : (uint64_t)ncu * per_cu;
-    {
-        unsigned long long* e0 = y.exit0;
-        unsigned long long* c0 = y.cnt0;
-        void* args[] = {&a, &e0, &c0};
-        hipError_t e = hipLaunchKernel(scan_fn, dim3(swgs), dim3(wthreads), args, lds, s);
-        if (e != hipSuccess) return e;
-    }
-    uint64_t iw = (y.nseg + 1023) / 1024;
-    iw = iw < (uint64_t)ncu * per_cu ? (iw ? iw : 1) : (uint64_t)ncu * per_cu;
-    int it = 0;
-    uint32_t nwork = 0;
-    for (;; ++it) {
-        hipError_t e = hipMemsetAsync(y.changed, 0, 4, s);
-        if (e != hipSuccess) return e;
-        uint64_t w = it == 0 ? iw : (nwork + 1023) / 1024;
-        w = w < iw ? (w ? w : 1) : iw;
-        hipLaunchKernelGGL(k_idx_iter, dim3(w), dim3(1024), lds, s, a, y, it, nwork);
-        if (it == 0) {  // iteration 0 wrote every exit to ex[1]; later ones read and write both
-            e = hipMemcpyAsync(y.ex[0], y.ex[1], 8 * y.nseg, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) return e;
-        }
-        if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        nwork = *h_changed;
-        if (nwork == 0 || it > (int)y.nseg) break;
-    }
-    const unsigned long long* exits = y.ex[(it + 1) & 1];
-    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       tiles);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
-    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       (const unsigned long long*)tiles, first);
-    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(d.nblocks));
-    hipError_t e = hipMemsetAsync(d_index + d.nblocks, 0xff, 8, s);  // end bit: all ones unless nsym codewords
-    if (e != hipSuccess) return e;
-    uint64_t ewgs = (groups + kEmitThreads - 1) / kEmitThreads;
-    ewgs = ewgs < (uint64_t)ncu * per_cu ? (ewgs ? ewgs : 1) : (uint64_t)ncu * per_cu;
-    if (getenv("HZ_IDX_BR_EMIT")) {  // DEBUG
-        (void)ensure_lds_limit((const void*)k_idx_emit_br, (int)lds);
-        hipLaunchKernelGGL(k_idx_emit_br, dim3((y.nseg + 255) / 256), dim3(256), lds, s, a, exits,
-                           (const unsigned long long*)y.cnt, (const unsigned long long*)first, d_index, subs);
-    } else if (getenv("HZ_IDX_OLD_EMIT")) {  // DEBUG
-        DecArgs dd = d;
-        dd.lds_img = t.d_dec_lds; dd.lds_words = t.dec_lds_bytes / 4; dd.k = t.dec_k; dd.l2 = t.d_dec_l2;
-        (void)ensure_lds_limit((const void*)k_sync_emit2, kLdsBytes);
-        hipLaunchKernelGGL(k_sync_emit2, dim3(ewgs), dim3(kSyncThreads), t.dec_lds_bytes, s, dd, y, exits,
-                           (const unsigned long long*)first, d_index, subs);
-    } else {
-        uint64_t ew = ((y.nseg + nc - 1) / nc + wthreads - 1) / wthreads;
-        ew = ew < (uint64_t)ncu * per_cu ? (ew ? ew : 1) : (uint64_t)ncu * per_cu;
-        const unsigned long long* ex = exits;
-        const unsigned long long* cn = y.cnt;
-        const unsigned long long* fi = first;
-        unsigned long long* st = d_index;
-        void* args[] = {&a, &ex, &cn, &fi, &st, &subs};
-        hipError_t e2 = hipLaunchKernel(emit_fn, dim3(ew), dim3(wthreads), args, lds, s);
-        if (e2 != hipSuccess) return e2;
-    }
-    if ((e = hipMemsetAsync(d_index + d.nblocks + 1, 0, 8, s)) != hipSuccess) return e;
-    uint64_t sw = (d.nblocks * kChainsPerBlock + 255) / 256;
-    sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
-    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, d.nsym, d.nblocks, d_index, subs);
-    return hipGetLastError();
 }
 
 hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
@@ -2840,27 +2298,6 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
         w = w < (uint64_t)ncu * 8 ? (w ? w : 1) : (uint64_t)ncu * 8;
         hipLaunchKernelGGL(k_idx_fixed16, dim3(w), dim3(256), 0, s, start_bit, nsym, a.nblocks, d_index);
         return hipGetLastError();
-    }
-    static const bool len_on = getenv("HZ_INDEX_LEN") != nullptr;  // experiment: slower than the LUT walks
-    if (t.len_bytes && a.nwords >= 4 && len_on) {
-        static const int seg_env = getenv("HZ_IDX_SEG") ? atoi(getenv("HZ_IDX_SEG")) : 0;  // DEBUG
-        const uint32_t seg = seg_env >= (int)kWalkSegBitsMin ? (uint32_t)seg_env : kWalkSegBits;
-        SyncArgs z;
-        z.start = start_bit;
-        z.nseg = (bits + seg - 1) / seg;
-        unsigned long long* q = d_scratch;
-        z.exit0 = q; q += z.nseg;
-        z.cnt0 = q; q += z.nseg;
-        z.ex[0] = q; q += z.nseg;
-        z.ex[1] = q; q += z.nseg;
-        z.cnt = q; q += z.nseg;
-        unsigned long long* zfirst = q; q += z.nseg;
-        z.bmp = nullptr;
-        z.dirty[0] = reinterpret_cast<uint32_t*>(q);
-        z.dirty[1] = z.dirty[0] + z.nseg;
-        q += z.nseg;
-        z.changed = reinterpret_cast<uint32_t*>(q); q += 1;
-        return run_index_len(t, a, z, seg, zfirst, q, d_index, h_scratch, ncu, s);
     }
     const uint32_t lds = t.dec_lds_bytes;
     if (t.dec_mode == DEC_DENSE) return run_index<DEC_DENSE>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
