@@ -65,6 +65,9 @@ PROTOTYPES = [
     ("hz_ctx_sync", _I, [_P]),
     ("hz_hist16", _I, [_P, _P, _U64, _P, _I]),
     ("hz_codebook_build", _I, [_P, ctypes.POINTER(Codebook)]),
+    ("hz_codebook_build_device", _I, [_P, _P, _P]),
+    ("hz_header_write_device", _I, [_P, _P, _U64, ctypes.c_uint8, _P, _U64, _P]),
+    ("hz_header_parse_device", _I, [_P, _P, _U64, _P, _P]),
     ("hz_header_bits", _I, [ctypes.POINTER(Codebook), _U64, ctypes.POINTER(_U64)]),
     ("hz_payload_bits", _I, [ctypes.POINTER(Codebook), _P, ctypes.POINTER(_U64)]),
     ("hz_header_write", _I, [ctypes.POINTER(Codebook), _U64, ctypes.c_uint8, _P, _U64, ctypes.POINTER(_U64),

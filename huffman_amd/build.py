@@ -21,7 +21,7 @@ BIN = os.path.join(PKG, "bin")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-LIB_SOURCES = ["hz_kernels.hip", "hz_codebook.cpp", "hz_host.cpp"]
+LIB_SOURCES = ["hz_kernels.hip", "hz_codebook_gpu.hip", "hz_codebook.cpp", "hz_host.cpp"]
 HEADERS = [os.path.join(CSRC, "hz_internal.h"), os.path.join(INCLUDE, "huffman_amd.h")]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}",
           f"-I{INCLUDE}", f"-I{CSRC}"]

@@ -167,6 +167,18 @@ class Device:
     def hist16(self, d_in, n, d_hist, accumulate=False):
         check(self.lib.hz_hist16(self.h, d_in, n, d_hist, int(accumulate)), "hz_hist16")
 
+    def codebook_build(self, d_hist, d_cb):
+        """Device codebook: d_hist (u64 x 65536) -> d_cb (sizeof(Codebook) bytes)."""
+        check(self.lib.hz_codebook_build_device(self.h, d_hist, d_cb), "hz_codebook_build_device")
+
+    def header_write(self, d_cb, n, last_byte, d_out, cap, d_info):
+        """Device header writer; d_info: 4 x u64 (bytes, pending bits, pending byte, bits)."""
+        check(self.lib.hz_header_write_device(self.h, d_cb, n, last_byte, d_out, cap, d_info), "hz_header_write_device")
+
+    def header_parse(self, d_file, length, d_cb, d_info):
+        """Device header parser; d_info: 6 x u64 (n, payload byte, payload bit, odd, last, nsym)."""
+        check(self.lib.hz_header_parse_device(self.h, d_file, length, d_cb, d_info), "hz_header_parse_device")
+
     def upload(self, cb):
         check(self.lib.hz_codebook_upload(self.h, ctypes.byref(cb)), "hz_codebook_upload")
 

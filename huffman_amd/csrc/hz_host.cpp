@@ -68,6 +68,7 @@ struct hz_ctx {
     uint32_t* d_err = nullptr;
     uint32_t* h_err = nullptr;      // pinned
     unsigned long long* d_thr = nullptr;
+    unsigned long long* d_cbws = nullptr;  // hz_codebook_build_device workspace
     double thr_alpha = -1.0;
     hipEvent_t ev[4][2] = {};
     bool ev_used[4] = {false, false, false, false};
@@ -143,6 +144,7 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
     (void)hipFree(c->d_desc);
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_thr);
+    (void)hipFree(c->d_cbws);
     (void)hipHostFree(c->h_err);
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 2; ++j) (void)hipEventDestroy(c->ev[i][j]);
@@ -170,7 +172,7 @@ extern "C" int hz_ctx_sync(hz_ctx* c) {
         const uint32_t e = *c->h_err;
         *c->h_err = 0;
         HZ_TRY(hipMemset(c->d_err, 0, 16));
-        return (e & 4u) ? HZ_ECAP : (e & 8u) ? HZ_ETIMEOUT : HZ_EFORMAT;
+        return (e & 4u) ? HZ_ECAP : (e & 8u) ? HZ_ETIMEOUT : (e & 16u) ? HZ_EINVAL : (e & 32u) ? HZ_ETOOLONG : HZ_EFORMAT;
     }
     return HZ_OK;
 }
@@ -196,6 +198,31 @@ extern "C" int hz_hist16(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
     c->ev_used[HZ_STAGE_HIST] = true;
     return HZ_OK;
+}
+
+extern "C" int hz_codebook_build_device(hz_ctx* c, const uint64_t* d_hist, hz_codebook* d_cb) {
+    if (!c || !d_hist || !d_cb) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    if (!c->d_cbws) HZ_TRY(hipMalloc(&c->d_cbws, codebook_ws_words() * sizeof(unsigned long long)));
+    HZ_TRY(launch_codebook(reinterpret_cast<const unsigned long long*>(d_hist), d_cb, c->d_cbws, c->d_err, c->stream));
+    return arm_err_check(c);
+}
+
+extern "C" int hz_header_write_device(hz_ctx* c, const hz_codebook* d_cb, uint64_t n, uint8_t last_byte,
+                                      uint8_t* d_out, uint64_t cap, uint64_t* d_info) {
+    if (!c || !d_cb || !d_out || !d_info || (((uintptr_t)d_out) & 3)) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(launch_header_write(d_cb, n, last_byte, d_out, cap, reinterpret_cast<unsigned long long*>(d_info), c->d_err,
+                               c->stream));
+    return arm_err_check(c);
+}
+
+extern "C" int hz_header_parse_device(hz_ctx* c, const uint8_t* d_file, uint64_t len, hz_codebook* d_cb,
+                                      uint64_t* d_info) {
+    if (!c || !d_file || !d_cb || !d_info) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(launch_header_parse(d_file, len, d_cb, reinterpret_cast<unsigned long long*>(d_info), c->d_err, c->stream));
+    return arm_err_check(c);
 }
 
 // Device tables live in per-context buffers that only grow; host images are

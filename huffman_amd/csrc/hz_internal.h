@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "huffman_amd.h"
+
 namespace hz {
 
 // ---- pack: one wavefront owns a block of 64 lanes x kSPT symbols ----------
@@ -120,6 +122,13 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
                               unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
                               hipStream_t s);  // synchronises the stream (iterates to a fixed point)
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
+hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
+                           uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
+uint64_t codebook_ws_words();
+hipError_t launch_header_write(const hz_codebook* d_cb, uint64_t n, uint32_t last_byte, uint8_t* d_out, uint64_t cap,
+                               unsigned long long* d_info, uint32_t* d_err, hipStream_t s);
+hipError_t launch_header_parse(const uint8_t* d_file, uint64_t len, hz_codebook* d_cb, unsigned long long* d_info,
+                               uint32_t* d_err, hipStream_t s);
 hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
                            const unsigned long long* d_thr, hipStream_t s);
 

@@ -89,6 +89,13 @@ int hz_hist16(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, in
  * (reference defect B4). */
 int hz_codebook_build(const uint64_t *hist, hz_codebook *cb);
 
+/* The same codebook built on the device: d_hist (u64 x 65536,
+ * device) -> d_cb (a device buffer of sizeof(hz_codebook), the same layout),
+ * stream-ordered on the context's stream, one workgroup, GenerateCL's rounds
+ * (gpuHuffmanConstruction.h:353-494) without a grid barrier. Errors surface at
+ * hz_ctx_sync: HZ_EINVAL (a count >= 2^47), HZ_ETOOLONG (a code > HZ_MAXLEN). */
+int hz_codebook_build_device(hz_ctx *ctx, const uint64_t *d_hist, hz_codebook *d_cb);
+
 /* Header bit length for a codebook and input size: 8*(3 + odd) + sum(24 + L) + 64.
  * The payload starts at that bit (Compressor.cu:431-487). */
 int hz_header_bits(const hz_codebook *cb, uint64_t n, uint64_t *bits);
@@ -103,9 +110,23 @@ int hz_payload_bits(const hz_codebook *cb, const uint64_t *hist, uint64_t *bits)
 int hz_header_write(const hz_codebook *cb, uint64_t n, uint8_t last_byte, uint8_t *out,
                      uint64_t cap, uint64_t *bytes, uint32_t *pending_bits, uint8_t *pending);
 
+/* The header written on the device from a device codebook
+ * (hz_codebook_build_device): d_out (4-byte aligned, cap bytes) receives the
+ * header bit stream -- floor(bits/8) complete bytes, then the pending bits
+ * MSB-aligned in the next byte, zeros after. d_info (device, 4 x u64):
+ * complete bytes, pending bit count, pending byte, header bits. */
+int hz_header_write_device(hz_ctx *ctx, const hz_codebook *d_cb, uint64_t n, uint8_t last_byte, uint8_t *d_out,
+                           uint64_t cap, uint64_t *d_info);
+
 /* Parse a header from the first `len` bytes of a .compressed file.
  * Replaces Decompressor.cu:65-103 (U 0 => 65536 :69-71; L 0 => 65536 :94-95). */
 int hz_header_parse(const uint8_t *file, uint64_t len, hz_codebook *cb, hz_header_info *info);
+
+/* The same parse on the device: d_file (device) -> d_cb
+ * (device hz_codebook) and d_info (device, 6 x u64: n, payload byte, payload
+ * bit, is_odd, last byte, nsym). Malformed headers surface as HZ_EFORMAT at
+ * hz_ctx_sync. */
+int hz_header_parse_device(hz_ctx *ctx, const uint8_t *d_file, uint64_t len, hz_codebook *d_cb, uint64_t *d_info);
 
 /* Upload a codebook's device tables to the context: encode tables (needed by
  * hz_pack), decode tables (needed by hz_decode / hz_index_build), or both.

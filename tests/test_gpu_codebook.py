@@ -1,0 +1,189 @@
+"""SURVEY.md 8f-2 / 8f-4 on the GPU: the device codebook (k_codebook, one
+workgroup, GenerateCL's rounds) and the device header writer / parser against
+the host builder, the literal-GenerateCL scale fixtures and the golden files.
+
+Tolerance: none (bit-exact)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLD)
+import make_scale_golden as msg  # noqa: E402
+
+SCALE = msg.load_fixture()
+
+
+@pytest.fixture(scope="module")
+def env(built_lib):
+    import torch
+    import huffman_amd
+    from huffman_amd.pipeline import StreamCodec
+    codec = StreamCodec(0)
+    return torch, huffman_amd, codec
+
+
+def _device_codebook(env, hist_dev):
+    torch, hz, codec = env
+    from huffman_amd._lib import Codebook
+    d_cb = torch.zeros(ctypes.sizeof(Codebook), dtype=torch.uint8, device="cuda")
+    codec.dev.codebook_build(hist_dev.data_ptr(), d_cb.data_ptr())
+    codec.sync()
+    return Codebook.from_buffer_copy(d_cb.cpu().numpy().tobytes()), d_cb
+
+
+def _same(a, b):
+    import huffman_amd
+    oa, la, ca = huffman_amd.codebook_arrays(a)
+    ob, lb, cb = huffman_amd.codebook_arrays(b)
+    return (a.nsym == b.nsym and a.max_len == b.max_len and a.min_len == b.min_len and np.array_equal(oa, ob)
+            and np.array_equal(la, lb) and np.array_equal(ca, cb))
+
+
+def _hists():
+    rng = np.random.default_rng(3)
+    out = {}
+    for U, hi in [(1, 5), (2, 3), (3, 3), (257, 4), (5000, 1000), (40000, 3), (65536, 2), (65536, 100000)]:
+        h = np.zeros(65536, dtype=np.uint64)
+        h[rng.choice(65536, U, replace=False)] = rng.integers(1, hi, U)
+        out[f"rand_U{U}_hi{hi}"] = h
+    fib = [1, 1]
+    while len(fib) < 41:
+        fib.append(fib[-1] + fib[-2])
+    h = np.zeros(65536, dtype=np.uint64)
+    h[np.arange(41) * 997 + 5] = fib
+    out["fibonacci_41"] = h                      # codes up to 40 bits, one pair per GenerateCL round
+    h = np.zeros(65536, dtype=np.uint64)
+    h[:65536] = 7
+    out["all_equal"] = h
+    out["romeo"] = oracle_lib.hist16(open(os.path.join(GOLD, "romeo.txt"), "rb").read())
+    for name in ("tie_dense", "tie_ragged"):
+        out[name] = msg.case_hist(name)[0]
+    return out
+
+
+HISTS = _hists()
+
+
+@pytest.mark.parametrize("name", sorted(HISTS))
+def test_device_codebook_equals_host(env, name):
+    torch, hz, codec = env
+    h = HISTS[name]
+    dev, _ = _device_codebook(env, torch.from_numpy(h.view(np.int64)).cuda())
+    assert _same(dev, hz.build_codebook(h))
+
+
+def test_device_codebook_empty(env):
+    torch, hz, codec = env
+    dev, _ = _device_codebook(env, torch.zeros(65536, dtype=torch.int64, device="cuda"))
+    assert dev.nsym == 0
+
+
+def test_device_codebook_rejects_huge_counts(env):
+    torch, hz, codec = env
+    h = torch.zeros(65536, dtype=torch.int64, device="cuda")
+    h[5] = 1 << 47
+    h[6] = 1
+    from huffman_amd._lib import Codebook
+    d_cb = torch.zeros(ctypes.sizeof(Codebook), dtype=torch.uint8, device="cuda")
+    codec.dev.codebook_build(h.data_ptr(), d_cb.data_ptr())
+    with pytest.raises(hz.HZError):
+        codec.sync()
+
+
+@pytest.mark.parametrize("name,kind", [("zipf_256MiB", 1), ("uniform_256MiB", 0)])
+def test_device_codebook_matches_literal_fixture(env, name, kind):
+    """Device histogram -> device codebook -> device header == the literal
+    GenerateCL / Compressor.cu writer fixture (tests/golden/scale_codebooks.json)."""
+    torch, hz, codec = env
+    n = SCALE[name]["n"]
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=42)
+    codec.histogram(x)
+    h = codec.hist.cpu().numpy().view(np.uint64).copy()
+    dev, d_cb = _device_codebook(env, codec.hist)
+    order, ln, code = hz.codebook_arrays(dev)
+    head = _device_header(env, d_cb, n, 0)
+    assert msg.digest(order, ln, code, h, n, 0, header=head) == msg.codebook_keys(SCALE[name])
+    del x
+    torch.cuda.empty_cache()
+
+
+def test_device_codebook_16gib_zipf(env):
+    """The bench's 16 GiB Zipf(1.1) histogram: device codebook == host codebook."""
+    torch, hz, codec = env
+    n = 16 << 30
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=42)
+    codec.histogram(x)
+    del x
+    torch.cuda.empty_cache()
+    h = codec.hist.cpu().numpy().view(np.uint64).copy()
+    dev, _ = _device_codebook(env, codec.hist)
+    assert _same(dev, hz.build_codebook(h))
+
+
+def _device_header(env, d_cb, n, last):
+    torch, hz, codec = env
+    cap = 16 + 65536 * 11
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    info = torch.zeros(4, dtype=torch.int64, device="cuda")
+    codec.dev.header_write(d_cb.data_ptr(), n, last, out.data_ptr(), cap, info.data_ptr())
+    codec.sync()
+    nb, pbits, pend, bits = [int(v) for v in info.cpu()]
+    assert bits == nb * 8 + pbits
+    return out[:nb].cpu().numpy().tobytes(), pbits, pend
+
+
+@pytest.mark.parametrize("name", ["romeo", "rand_U257_hi4", "tie_ragged", "fibonacci_41", "rand_U1_hi5"])
+@pytest.mark.parametrize("n_extra", [0, 1])
+def test_device_header_equals_host(env, name, n_extra):
+    torch, hz, codec = env
+    h = HISTS[name]
+    n = 2 * int(h.sum()) + n_extra
+    last = 0x5a if n_extra else 0
+    _, d_cb = _device_codebook(env, torch.from_numpy(h.view(np.int64)).cuda())
+    got = _device_header(env, d_cb, n, last)
+    want = hz.write_header(hz.build_codebook(h), n, last)
+    assert got[0] == want[0] and got[1] == want[1]
+    if got[1]:
+        assert got[2] >> (8 - got[1]) == want[2] >> (8 - want[1])
+
+
+def _device_parse(env, blob):
+    torch, hz, codec = env
+    from huffman_amd._lib import Codebook
+    f = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).cuda()
+    d_cb = torch.zeros(ctypes.sizeof(Codebook), dtype=torch.uint8, device="cuda")
+    info = torch.zeros(6, dtype=torch.int64, device="cuda")
+    codec.dev.header_parse(f.data_ptr(), len(blob), d_cb.data_ptr(), info.data_ptr())
+    codec.sync()
+    return Codebook.from_buffer_copy(d_cb.cpu().numpy().tobytes()), [int(v) for v in info.cpu()]
+
+
+@pytest.mark.parametrize("name", ["romeo.txt.compressed", "romeo.txt.baseline.compressed",
+                                  "synth_unif_65536.bin.compressed", "synth_zipf_65537.bin.baseline.compressed",
+                                  "synth_zipf_4099.bin.compressed"])
+def test_device_header_parse_equals_host(env, name):
+    torch, hz, codec = env
+    blob = open(os.path.join(GOLD, name), "rb").read()
+    dev, info = _device_parse(env, blob)
+    cb, hi = hz.parse_header(blob)
+    assert _same(dev, cb)
+    assert info == [hi.n, hi.payload_byte, hi.payload_bit, hi.is_odd, hi.last_byte, hi.nsym]
+
+
+@pytest.mark.parametrize("cut", [5, 100, 2000])
+def test_device_header_parse_rejects_truncated(env, cut):
+    torch, hz, codec = env
+    blob = open(os.path.join(GOLD, "romeo.txt.compressed"), "rb").read()
+    with pytest.raises(hz.HZError):
+        _device_parse(env, blob[:cut])
