@@ -15,10 +15,10 @@
 //   k_header_write  the header (Compressor.cu:431-487, writers :637-669): one
 //                   thread per codebook entry at its scanned bit offset,
 //                   words ORed together.
-//   k_header_parse  the header (Decompressor.cu:65-103): one wave walks the
-//                   entries (each one's position needs the previous length),
-//                   256 header bytes at a time in registers, entries read by
-//                   lane reads.
+//   k_header_parse  the header (Decompressor.cu:65-103): one wave finds the
+//                   entry positions (each needs the previous length; 256
+//                   header bytes at a time in registers, read by lane reads),
+//                   then the workgroup decodes every entry at its position.
 #include <stdint.h>
 
 #include "huffman_amd.h"
@@ -349,63 +349,95 @@ HZ_DEV uint32_t hdr_bits32(const HdrWin& win, uint64_t p) {
     return sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
 }
 
-__global__ __launch_bounds__(64) void k_header_parse(const uint8_t* __restrict__ f, uint64_t len,
-                                                     hz_codebook* __restrict__ cb, unsigned long long* info,
-                                                     uint32_t* err) {
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t s = lane; s < 65536; s += 64) { cb->len[s] = 0; cb->code[s] = 0; }
+// Bits [p, p + nb) of the file, nb <= 56, read byte-wise (zeros past len).
+HZ_DEV uint64_t file_bits(const uint8_t* f, uint64_t len, uint64_t p, uint32_t nb) {
+    const uint64_t b0 = p >> 3;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v = (v << 8) | (b0 + k < len ? f[b0 + k] : 0u);
+    return (v << (p & 7)) >> (64 - nb);
+}
+
+constexpr int kParseThreads = 1024;
+
+// Phase A, one wave: the entry positions (each needs the previous length),
+// 2048 header bits at a time in registers, read by lane reads. Phase B, the
+// whole workgroup: every entry decoded at its position, duplicates caught by a
+// symbol bitmap.
+__global__ __launch_bounds__(kParseThreads) void k_header_parse(const uint8_t* __restrict__ f, uint64_t len,
+                                                                hz_codebook* __restrict__ cb, unsigned long long* info,
+                                                                uint32_t* ws, uint32_t* err) {
+    __shared__ uint32_t seen[2048];  // 65 536-symbol bitmap
+    __shared__ uint32_t sh_bad, sh_max, sh_min;
+    __shared__ unsigned long long sh_end;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    for (uint32_t s = tid; s < 65536; s += nt) { cb->len[s] = 0; cb->code[s] = 0; }
+    for (uint32_t i = tid; i < 2048; i += nt) seen[i] = 0;
+    if (tid == 0) { sh_bad = 0; sh_max = 0; sh_min = 255; sh_end = 0; }
     __syncthreads();
-    if (len < 3) { if (lane == 0) atomicOr(err, 2u); return; }
+    if (len < 3 || (f[2] != 0 && len < 4)) {
+        if (tid == 0) atomicOr(err, 2u);
+        return;
+    }
     uint32_t U = (uint32_t)f[0] | ((uint32_t)f[1] << 8);  // Decompressor.cu:69-71
     const uint32_t odd = f[2] != 0;                        // :76
-    if (odd && len < 4) { if (lane == 0) atomicOr(err, 2u); return; }
     const uint64_t pre = odd ? 4 : 3;
     if (U == 0) U = (len == pre + 8) ? 0 : 65536;          // U 0 => 65536 (and the empty-file convention)
-    HdrWin win;
-    auto load = [&](uint64_t bit) {                         // window of 64 words starting at the word holding `bit`
-        win.base = bit & ~31ull;
-        win.w = hdr_word_be(f, len, win.base / 8 + 4ull * lane);
-    };
-    uint64_t p = 8 * pre;
-    load(p);
-    uint32_t mx = 0, mn = 255, bad = 0;
-    for (uint32_t i = 0; i < U; ++i) {
-        if (p - win.base > 2048 - 128) load(p);             // room for a whole entry (<= 80 bits) + slack
-        const uint32_t h = hdr_bits32(win, p);
-        const uint32_t sym = h >> 16, L = (h >> 8) & 0xffu;
-        if (L == 0 || L > HZ_MAXLEN) { bad = 1; break; }    // the reference reads 0 as 65536 (:94-95)
-        uint64_t code;
-        if (L <= 32) {
-            code = hdr_bits32(win, p + 24) >> (32 - L);
-        } else {
-            const uint64_t two = ((uint64_t)hdr_bits32(win, p + 24) << 32) | hdr_bits32(win, p + 56);
-            code = two >> (64 - L);
+    if (tid < 64) {
+        HdrWin win;
+        auto load = [&](uint64_t bit) {
+            win.base = bit & ~31ull;
+            win.w = hdr_word_be(f, len, win.base / 8 + 4ull * lane);
+        };
+        uint64_t p = 8 * pre;
+        load(p);
+        uint32_t bad = 0;
+        for (uint32_t i = 0; i < U; ++i) {
+            if (p - win.base > 2048 - 128) load(p);
+            const uint32_t L = (hdr_bits32(win, p) >> 8) & 0xffu;
+            if (L == 0 || L > HZ_MAXLEN || (p + 24 + L + 64 + 7) / 8 > len) { bad = 1; break; }
+            if (lane == 0) ws[i] = (uint32_t)p;  // header < 2^32 bits
+            p += 24 + L;
         }
         if (lane == 0) {
-            if (cb->len[sym]) bad = 1;                       // duplicate symbol
-            cb->order[i] = (uint16_t)sym;
-            cb->len[sym] = (uint8_t)L;
-            cb->code[sym] = code;
+            sh_bad = bad;
+            sh_end = p;
         }
-        bad = __builtin_amdgcn_readfirstlane(bad);
-        if (bad) break;
+    }
+    __syncthreads();
+    if (sh_bad) {
+        if (tid == 0) atomicOr(err, 2u);
+        return;
+    }
+    uint32_t mx = 0, mn = 255;
+    for (uint32_t i = tid; i < U; i += nt) {
+        const uint64_t p = ws[i];
+        const uint32_t head = (uint32_t)file_bits(f, len, p, 24);
+        const uint32_t sym = head >> 8, L = head & 0xffu;
+        if (atomicOr(&seen[sym >> 5], 1u << (sym & 31)) & (1u << (sym & 31))) atomicOr(&sh_bad, 1u);  // duplicate
+        cb->order[i] = (uint16_t)sym;
+        cb->len[sym] = (uint8_t)L;
+        cb->code[sym] = file_bits(f, len, p + 24, L);
         mx = L > mx ? L : mx;
         mn = L < mn ? L : mn;
-        p += 24 + L;
-        if ((p + 64 + 7) / 8 > len) { bad = 1; break; }     // truncated (N must follow)
     }
-    if (!bad) {
-        if (p - win.base > 2048 - 128) load(p);
-        uint64_t n = 0;
-        for (int b = 0; b < 8; ++b) n |= (uint64_t)(hdr_bits32(win, p + 8 * b) >> 24) << (8 * b);
+    atomicMax(&sh_max, mx);
+    atomicMin(&sh_min, mn);
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t p = sh_end;
+        const uint64_t n = file_bits(f, len, p, 32) << 32 | file_bits(f, len, p + 32, 32);  // N, stream order
+        uint64_t nn = 0;  // 8 LE bytes, each MSB first
+        for (int b = 0; b < 8; ++b) nn |= ((n >> (56 - 8 * b)) & 0xffu) << (8 * b);
         p += 64;
-        if (n / 2 > 0 && U == 0) bad = 1;
-        if (lane == 0 && !bad) {
+        if ((p + 7) / 8 > len || (nn / 2 > 0 && U == 0) || sh_bad) {
+            atomicOr(err, 2u);
+        } else {
             cb->nsym = U;
-            cb->max_len = U ? mx : 0;
-            cb->min_len = U ? mn : 0;
+            cb->max_len = U ? sh_max : 0;
+            cb->min_len = U ? sh_min : 0;
             cb->reserved = 0;
-            info[0] = n;
+            info[0] = nn;
             info[1] = p >> 3;
             info[2] = p & 7;
             info[3] = odd;
@@ -413,7 +445,6 @@ __global__ __launch_bounds__(64) void k_header_parse(const uint8_t* __restrict__
             info[5] = U;
         }
     }
-    if (bad && lane == 0) atomicOr(err, 2u);
 }
 
 hipError_t launch_header_write(const hz_codebook* d_cb, uint64_t n, uint32_t last_byte, uint8_t* d_out, uint64_t cap,
@@ -423,8 +454,9 @@ hipError_t launch_header_write(const hz_codebook* d_cb, uint64_t n, uint32_t las
 }
 
 hipError_t launch_header_parse(const uint8_t* d_file, uint64_t len, hz_codebook* d_cb, unsigned long long* d_info,
-                               uint32_t* d_err, hipStream_t s) {
-    hipLaunchKernelGGL(k_header_parse, dim3(1), dim3(64), 0, s, d_file, len, d_cb, d_info, d_err);
+                               unsigned long long* d_ws, uint32_t* d_err, hipStream_t s) {
+    hipLaunchKernelGGL(k_header_parse, dim3(1), dim3(kParseThreads), 0, s, d_file, len, d_cb, d_info,
+                       reinterpret_cast<uint32_t*>(d_ws), d_err);
     return hipGetLastError();
 }
 

@@ -221,7 +221,9 @@ extern "C" int hz_header_parse_device(hz_ctx* c, const uint8_t* d_file, uint64_t
                                       uint64_t* d_info) {
     if (!c || !d_file || !d_cb || !d_info) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
-    HZ_TRY(launch_header_parse(d_file, len, d_cb, reinterpret_cast<unsigned long long*>(d_info), c->d_err, c->stream));
+    if (!c->d_cbws) HZ_TRY(hipMalloc(&c->d_cbws, codebook_ws_words() * sizeof(unsigned long long)));
+    HZ_TRY(launch_header_parse(d_file, len, d_cb, reinterpret_cast<unsigned long long*>(d_info), c->d_cbws, c->d_err,
+                               c->stream));
     return arm_err_check(c);
 }
 
