@@ -328,7 +328,7 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
     x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
-    x.bstart = a.blk_start ? a.blk_start[blk] : 0;  // one-pass pack: from the look-back
+    x.bstart = a.blk_start[blk];
 }
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
@@ -708,218 +708,6 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
-// ---- one-pass pack: decoupled look-back over chunks -------------------------
-// A chunk is one block per wave of a workgroup (8 blocks, 32 KiB of input).
-// Chunks are taken by ticket, in order, so every chunk's predecessors are
-// held by running workgroups (no co-residency assumption). Per chunk the
-// workgroup looks up and counts its blocks and publishes the chunk's
-// aggregate (status AGG). One iteration later, while the next chunk is
-// counted, it resolves the chunk's exclusive prefix from a window of the
-// previous 64 x waves chunk statuses -- each wave loads 64 of them, one per
-// lane, issued before its count and summarised after it -- publishes INCL,
-// and the waves emit the chunk's blocks at their now known start bits.
-// Every thread combines the waves' summaries after the one barrier per
-// chunk, so no wave waits on another's look-back; a window without an INCL
-// or with an unpublished status takes wave 0's slow loop (rare). The emit of
-// chunk i overlaps the look-back of chunk i + 1. Replaces k_pack_count and the
-// scan kernels for HOT and DENSE tables: pack reads its input once.
-constexpr int kLbPer = 8;                              // slow loop: statuses per lane (512-chunk window)
-constexpr uint64_t kStIncl = 1ull << 63, kStAgg = 1ull << 62, kStVal = kStAgg - 1;
-constexpr uint32_t kLbMaxTries = 1u << 22;             // then flag HZ_ETIMEOUT and go on (no hang)
-
-HZ_DEV uint64_t status_load(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-HZ_DEV void status_store(unsigned long long* p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Slow loop: statuses of chunks top, top - 1, ..., top - 511 (lane l holds
-// top - 8 l - k); a fixed count of loads (indices below 0 read as INCL 0).
-HZ_DEV void lb_issue(const unsigned long long* status, int64_t top, int lane, uint64_t (&st)[kLbPer]) {
-#pragma unroll
-    for (int k = 0; k < kLbPer; ++k) {
-        const int64_t j = top - (int64_t)(lane * kLbPer + k);
-        st[k] = status_load(status + (j >= 0 ? j : 0));
-    }
-#pragma unroll
-    for (int k = 0; k < kLbPer; ++k) {
-        const int64_t j = top - (int64_t)(lane * kLbPer + k);
-        st[k] = j >= 0 ? st[k] : kStIncl;
-    }
-}
-
-// 0: resolved (acc += the window up to and including its first INCL), 1: no
-// INCL in the window (acc += all of it), 2: a status before the first INCL
-// is not published yet (acc unchanged).
-HZ_DEV int lb_resolve(const uint64_t (&st)[kLbPer], int lane, uint64_t& acc) {
-    int ki = kLbPer, kn = kLbPer;
-#pragma unroll
-    for (int k = kLbPer - 1; k >= 0; --k) {
-        ki = (st[k] & kStIncl) ? k : ki;
-        kn = st[k] == 0 ? k : kn;
-    }
-    const uint64_t bi = __ballot(ki < kLbPer), bn = __ballot(kn < kLbPer);
-    const int li = bi ? __builtin_ctzll(bi) : 64, ln = bn ? __builtin_ctzll(bn) : 64;
-    const int ji = li < 64 ? li * kLbPer + (int)readlane((uint32_t)ki, li) : 64 * kLbPer;
-    const int jn = ln < 64 ? ln * kLbPer + (int)readlane((uint32_t)kn, ln) : 64 * kLbPer;
-    if (jn < ji) return 2;
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < kLbPer; ++k) v += lane * kLbPer + k <= ji ? (st[k] & kStVal) : 0;
-    acc += wave_sum_u64(v);
-    return ji < 64 * kLbPer ? 0 : 1;
-}
-
-HZ_DEV uint64_t lb_slow(const unsigned long long* status, uint64_t chunk, int lane, uint32_t* err) {
-    uint64_t acc = 0, st[kLbPer];
-    int64_t top = (int64_t)chunk - 1;
-    lb_issue(status, top, lane, st);
-    for (uint32_t tries = 0;;) {
-        const int r = lb_resolve(st, lane, acc);
-        if (r == 0) break;
-        if (r == 1) {
-            top -= 64 * kLbPer;
-        } else {
-            if (++tries > kLbMaxTries) {
-                if (lane == 0) atomicOr(err, 8u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        lb_issue(status, top, lane, st);
-    }
-    return acc;
-}
-
-struct OneArgs {
-    unsigned long long* status;  // per chunk, zeroed: AGG | bits, or INCL | end bit
-    unsigned long long* ticket;  // zeroed chunk counter
-    uint64_t nchunks;
-    uint64_t start_bit;
-};
-
-template <int MODE>
-__global__ __launch_bounds__(kPackWriteThreads) void k_pack_one(PackArgs a, OneArgs o) {
-    constexpr int kMaxW = kPackWriteThreads / 64;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t sh_bits[3][kMaxW];            // per-wave block bits, by iteration mod 3
-    __shared__ unsigned long long sh_lbs[2][kMaxW];   // per-wave window sums, by iteration parity
-    __shared__ uint32_t sh_lbf[2][kMaxW];             // per-wave first INCL | first unpublished << 8
-    __shared__ unsigned long long sh_tk[2];           // tickets, by iteration parity
-    __shared__ unsigned long long sh_slow;            // slow-loop result
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    if (threadIdx.x == 0) {
-        sh_tk[0] = atomicAdd(o.ticket, 1ull);
-        sh_tk[1] = atomicAdd(o.ticket, 1ull);
-    }
-    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);  // ends in a barrier
-    uint32_t* slot = a.slot_words ? lds + a.lds_words + wv * a.slot_words : nullptr;
-    uint64_t c = sh_tk[0], cn = sh_tk[1];
-    uint64_t c_pend = ~0ull, agg_pend = 0, max_bits = 0;
-    // every prefetch is issued (clamped to the last block): static load counts
-    auto pf_blk = [&](uint64_t ch) {
-        const uint64_t b = ch < o.nchunks ? ch * nw + wv : a.nblocks - 1;
-        return b < a.nblocks ? b : a.nblocks - 1;
-    };
-    PackIn nx;
-    pack_prefetch(a, pf_blk(c), lane, nx);
-    PackBlk<MODE> pb;
-    uint64_t st = 0;  // this wave's slice of the pending chunk's look-back window
-    for (uint32_t it = 0;; ++it) {
-        const bool have = c < o.nchunks, pend = c_pend != ~0ull;
-        if (!have && !pend) break;
-        unsigned long long tk = ~0ull;
-        if (have && threadIdx.x == 0) tk = atomicAdd(o.ticket, 1ull);  // the chunk after next
-        PackBlk<MODE> b;
-        const uint64_t blk = c * nw + wv;
-        const bool mine = have && blk < a.nblocks;
-        if (mine) {
-            PackIn cur = nx;
-            pack_block_lookup<MODE>(a, lds, blk, lane, cur, b);
-        }
-        {
-            // this wave's 64 statuses of the pending chunk's window, in flight during the count
-            const int64_t j = (int64_t)c_pend - 1 - (int64_t)(wv * 64 + lane);
-            st = status_load(o.status + (pend && j >= 0 ? j : 0));
-        }
-        pack_prefetch(a, pf_blk(cn), lane, nx);
-        if (mine) pack_block_count<MODE>(lane, b);
-        if (lane == 0) sh_bits[it % 3][wv] = mine ? b.bits : 0u;
-        if (pend) {
-            const int64_t j = (int64_t)c_pend - 1 - (int64_t)(wv * 64 + lane);
-            st = j >= 0 ? st : kStIncl;  // before chunk 0: INCL 0
-            const uint64_t bi = __ballot((st & kStIncl) != 0), bn = __ballot(st == 0);
-            const uint32_t fi = bi ? __builtin_ctzll(bi) : 64, fn = bn ? __builtin_ctzll(bn) : 64;
-            const uint64_t sum = wave_sum_u64((uint32_t)lane <= fi ? (st & kStVal) : 0);
-            if (lane == 0) {
-                sh_lbs[it & 1][wv] = sum;
-                sh_lbf[it & 1][wv] = fi | fn << 8;
-            }
-        }
-        if (threadIdx.x == 0) sh_tk[it & 1] = tk;
-        __syncthreads();
-        // lane w < nw reads wave w's entries: one LDS round trip, then lane reads
-        const int lw = lane & (kMaxW - 1);
-        const uint32_t b_cur = lane < nw ? sh_bits[it % 3][lw] : 0u;
-        const uint32_t b_prev = lane < nw ? sh_bits[(it + 2) % 3][lw] : 0u;  // counted in iteration it - 1
-        const uint64_t l_sum = lane < nw ? sh_lbs[it & 1][lw] : 0ull;
-        const uint32_t l_f = lane < nw ? sh_lbf[it & 1][lw] : (64u | 64u << 8);
-        uint32_t agg = 0, pre = 0;
-        const int wu = __builtin_amdgcn_readfirstlane(wv);
-#pragma unroll
-        for (int w = 0; w < kMaxW; ++w) {
-            agg += readlane(b_cur, w);
-            pre += w < wu ? readlane(b_prev, w) : 0u;
-        }
-        if (have && threadIdx.x == 0)  // chunk 0 knows its start: INCL at once
-            status_store(o.status + c, c == 0 ? kStIncl | (o.start_bit + agg) : kStAgg | agg);
-        if (pend) {
-            uint64_t excl = o.start_bit;
-            if (c_pend > 0) {
-                // the waves' window summaries in order: the first wave whose slice holds
-                // an INCL (or an unpublished status before one) ends the window
-                const uint32_t fi = l_f & 0xffu, fn = l_f >> 8;
-                const uint64_t stop = __ballot(fn < fi || fi < 64);
-                const int L = stop ? __builtin_ctzll(stop) : 64;
-                bool ok = false;
-                uint64_t acc = 0;
-                if (L < 64) {
-                    const uint32_t f = readlane(l_f, L);
-                    ok = (f >> 8) >= (f & 0xffu);
-#pragma unroll
-                    for (int w = 0; w < kMaxW; ++w) {
-                        const uint64_t v = ((uint64_t)readlane((uint32_t)(l_sum >> 32), w) << 32) |
-                                           readlane((uint32_t)l_sum, w);
-                        acc += w <= L ? v : 0ull;
-                    }
-                }
-                if (!ok) {  // workgroup-uniform
-                    if (wv == 0) {
-                        const uint64_t r = lb_slow(o.status, c_pend, lane, a.err);
-                        if (lane == 0) sh_slow = r;
-                    }
-                    __syncthreads();
-                    acc = sh_slow;
-                }
-                excl = acc;
-                if (threadIdx.x == 0) status_store(o.status + c_pend, kStIncl | (excl + agg_pend));
-            }
-            const uint64_t pblk = c_pend * nw + wv;
-            if (pblk < a.nblocks) {
-                const uint64_t bstart = excl + pre;
-                pack_block_emit<MODE>(a, slot, pblk, lane, pb, bstart, max_bits);
-            }
-        }
-        pb = b;
-        agg_pend = agg;
-        c_pend = have ? c : ~0ull;
-        c = cn;
-        cn = sh_tk[it & 1];
-    }
-    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
-}
-
 // ---- every code 16 bits (U = 65 536, min_len = max_len = 16) ---------------
 // Symbol i starts at bit start_bit + 16 i: no count pass and no scan. Lane j
 // packs symbols [32 j, 32 j + 32) into the 16 words whose last bit lies in its
@@ -1094,8 +882,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long
     }
 }
 
-constexpr uint32_t kOneLdsReserveWords = 128;  // k_pack_one's static LDS (look-back summaries, tickets)
-
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
@@ -1136,7 +922,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     // (Kraft estimate from the code lengths, +12 %) as fit beside the table.
     const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
     a.lds_words = table_words;
-    const uint32_t free_words = kLdsBytes / 4 - table_words - kOneLdsReserveWords;
+    const uint32_t free_words = kLdsBytes / 4 - table_words;
     const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * 1.12 / 32.0) + 4;
     constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
     uint32_t waves = free_words / est_words;
@@ -1151,29 +937,12 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t lds = 4 * (table_words + waves * a.slot_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
-    if (t.enc_mode != ENC_WIDE) {
-        // one pass: status[nchunks] + ticket in the scratch, zeroed
-        OneArgs o;
-        o.nchunks = (nblocks + waves - 1) / waves;
-        o.status = d_scratch;
-        o.ticket = d_scratch + o.nchunks;
-        o.start_bit = start_bit;
-        a.blk_start = nullptr;
-        hipError_t e = hipMemsetAsync(d_scratch, 0, (o.nchunks + 1) * sizeof(unsigned long long), s);
-        if (e != hipSuccess) return e;
-        const void* fn = t.enc_mode == ENC_HOT ? (const void*)k_pack_one<ENC_HOT> : (const void*)k_pack_one<ENC_DENSE>;
-        if ((e = ensure_lds_limit(fn, (int)lds)) != hipSuccess) return e;
-        const uint64_t g = o.nchunks < wgs ? o.nchunks : wgs;
-        if (t.enc_mode == ENC_HOT)
-            hipLaunchKernelGGL(k_pack_one<ENC_HOT>, dim3(g), dim3(threads), lds, s, a, o);
-        else
-            hipLaunchKernelGGL(k_pack_one<ENC_DENSE>, dim3(g), dim3(threads), lds, s, a, o);
-        return hipGetLastError();
-    }
     {
         hipError_t e = ensure_lds_limit((const void*)k_pack_count, kLen8LdsBytes);
         if (e != hipSuccess) return e;
-        if ((e = ensure_lds_limit((const void*)k_pack_write<ENC_WIDE>, kLdsBytes)) != hipSuccess) return e;
+        const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE>, (const void*)k_pack_write<ENC_HOT>,
+                             (const void*)k_pack_write<ENC_WIDE>};
+        if ((e = ensure_lds_limit(fw[t.enc_mode], kLdsBytes)) != hipSuccess) return e;
     }
     {
         const uint64_t cw = kCountThreads / 64;
@@ -1186,7 +955,11 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, start_bit);
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
                        nblocks, (const unsigned long long*)tiles, blk_start);
-    hipLaunchKernelGGL(k_pack_write<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a);
+    switch (t.enc_mode) {
+        case ENC_DENSE: hipLaunchKernelGGL(k_pack_write<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL(k_pack_write<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a); break;
+        default: hipLaunchKernelGGL(k_pack_write<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+    }
     return hipGetLastError();
 }
 
