@@ -55,6 +55,16 @@ _U64 = ctypes.c_uint64
 _U32 = ctypes.c_uint32
 _I = ctypes.c_int
 
+class StreamTiming(ctypes.Structure):
+    """hz_stream_timing: stage split of the thread's last streamed archive / extract."""
+    _fields_ = [("total_ms", ctypes.c_double), ("fread_ms", ctypes.c_double), ("fwrite_ms", ctypes.c_double),
+                ("alloc_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # (name, restype, argtypes): exactly the entry points include/huffman_amd.h declares.
 PROTOTYPES = [
     ("hz_strerror", ctypes.c_char_p, [_I]),
@@ -88,6 +98,7 @@ PROTOTYPES = [
     ("hz_archive_stream", _I, [ctypes.c_char_p, ctypes.c_char_p, _U64, _I]),
     ("hz_extract_stream", _I, [ctypes.c_char_p, ctypes.c_char_p, _U64, _I]),
     ("hz_extract_file", _I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, _I]),
+    ("hz_stream_last_timing", _I, [ctypes.POINTER(StreamTiming)]),
     ("hz_encode_host", _I, [_P, _U64, _P, _U64, ctypes.POINTER(_U64)]),
     ("hz_encoded_size", _I, [_P, _U64, ctypes.POINTER(_U64)]),
     ("hz_decode_host", _I, [_P, _U64, _P, _U64, ctypes.POINTER(_U64)]),

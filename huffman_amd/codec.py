@@ -73,6 +73,14 @@ def extract_stream(path, out_path, chunk_bytes=1 << 30, verbose=False):
     return str(out_path)
 
 
+def stream_timing():
+    """Stage split (dict) of this thread's last archive_stream / extract_stream call."""
+    from ._lib import StreamTiming
+    t = StreamTiming()
+    check(load().hz_stream_last_timing(ctypes.byref(t)), "hz_stream_last_timing")
+    return t.as_dict()
+
+
 def extract(path, verbose=True):
     """`extract <path>`: writes ./DECOMPRESSED_FILE (or (k)); returns its name."""
     name = ctypes.create_string_buffer(256)

@@ -2,6 +2,9 @@
 // (Compressor.cu:315-632) on the gfx950 kernels of libhuffman_amd.
 // Exit codes follow the reference: 0 on usage error and on a missing file
 // (Compressor.cu:317-330); 2 when the codec or any other I/O fails.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <iostream>
 
 #include "huffman_amd.h"
@@ -12,6 +15,17 @@ int main(int argc, char* argv[]) {
         return 0;
     }
     const int rc = hz_archive_file(argv[1], 1);
+    if (getenv("HZ_TIMING")) {  // stage split of the run, one JSON line on stderr
+        hz_stream_timing t;
+        if (hz_stream_last_timing(&t) == HZ_OK)
+            fprintf(stderr,
+                    "{\"total_ms\": %.3f, \"fread_ms\": %.3f, \"fwrite_ms\": %.3f, \"alloc_ms\": %.3f, "
+                    "\"host_ms\": %.3f, "
+                    "\"h2d_ms\": %.3f, \"kernel_ms\": %.3f, \"d2h_ms\": %.3f, \"bytes_in\": %llu, "
+                    "\"bytes_out\": %llu}\n",
+                    t.total_ms, t.fread_ms, t.fwrite_ms, t.alloc_ms, t.host_ms, t.h2d_ms, t.kernel_ms, t.d2h_ms,
+                    (unsigned long long)t.bytes_in, (unsigned long long)t.bytes_out);
+    }
     if (rc == HZ_ENOENT || rc == HZ_OK) return 0;
     return 2;
 }

@@ -9,6 +9,7 @@
 #include <string.h>
 #include <sys/stat.h>
 
+#include <chrono>
 #include <iostream>
 #include <memory>
 #include <mutex>
@@ -458,7 +459,8 @@ extern "C" int hz_generate(hz_ctx* c, uint8_t* d_out, uint64_t n, uint64_t offse
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr uint64_t kArchiveChunk = 1ull << 30;  // 1 GiB per streamed chunk
+constexpr uint64_t kArchiveChunk = 256ull << 20;  // archive: 256 MiB per streamed chunk (~1.2 GB pinned)
+constexpr uint64_t kExtractWindow = 512ull << 20; // extract: 512 MiB payload windows
 
 std::mutex g_mu;
 hz_ctx* g_ctx = nullptr;
@@ -608,8 +610,10 @@ std::string output_name() {
 // Pass 1 reads the file in chunks and accumulates the histogram on the device;
 // pass 2 packs chunk by chunk at the running bit offset. Each chunk's last,
 // partial word is carried into the next chunk as its `lead` bits, so the file
-// is byte-identical to the whole-buffer encoder's. Two pinned host buffers let
-// the next chunk's fread overlap the device work on the current one.
+// is byte-identical to the whole-buffer encoder's. Double-buffered pinned and
+// device buffers keep the host's fread of chunk k + 1 and fwrite of chunk
+// k - 1 beside the device's upload and pack of chunk k, and the copy-out of
+// chunk k runs on a second stream beside the upload and pack of chunk k + 1.
 namespace {
 
 struct PinnedBuf {
@@ -618,11 +622,104 @@ struct PinnedBuf {
     int alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault) == hipSuccess ? HZ_OK : HZ_ENOMEM; }
 };
 
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
+thread_local hz_stream_timing g_timing;  // the calling thread's last streamed call
+
+// Device busy time per stage: an event pair around each copy or kernel
+// launch (events are never shared between spans), folded into its stage once
+// the end event has completed.
+class Spans {
+  public:
+    ~Spans() {
+        for (auto& s : open_) {
+            (void)hipEventDestroy(s.a);
+            (void)hipEventDestroy(s.b);
+        }
+        for (auto e : free_) (void)hipEventDestroy(e);
+    }
+    hipEvent_t mark(hipStream_t st) {
+        hipEvent_t e = nullptr;
+        if (!free_.empty()) {
+            e = free_.back();
+            free_.pop_back();
+        } else if (hipEventCreate(&e) != hipSuccess) {
+            return nullptr;
+        }
+        if (hipEventRecord(e, st) != hipSuccess) {
+            free_.push_back(e);
+            return nullptr;
+        }
+        return e;
+    }
+    void add(hipEvent_t a, hipEvent_t b, double* acc) {
+        if (a && b) open_.push_back({a, b, acc});
+        else {
+            if (a) free_.push_back(a);
+            if (b) free_.push_back(b);
+        }
+    }
+    void fold() {
+        for (size_t i = 0; i < open_.size();) {
+            if (hipEventQuery(open_[i].b) != hipSuccess) { ++i; continue; }
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, open_[i].a, open_[i].b) == hipSuccess) *open_[i].acc += ms;
+            free_.push_back(open_[i].a);
+            free_.push_back(open_[i].b);
+            open_[i] = open_.back();
+            open_.pop_back();
+        }
+    }
+  private:
+    struct Span { hipEvent_t a, b; double* acc; };
+    std::vector<Span> open_;
+    std::vector<hipEvent_t> free_;
+};
+
 int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
-    return (n == 0 || fread(p, 1, n, fp) == n) ? HZ_OK : HZ_EIO;
+    if (n == 0) return HZ_OK;
+    const auto t0 = Clock::now();
+    const bool ok = fread(p, 1, n, fp) == n;
+    g_timing.fread_ms += ms_since(t0);
+    g_timing.bytes_in += ok ? n : 0;
+    return ok ? HZ_OK : HZ_EIO;
 }
 
+int write_exact(FILE* fp, const uint8_t* p, uint64_t n) {
+    if (n == 0) return HZ_OK;
+    const auto t0 = Clock::now();
+    const bool ok = fwrite(p, 1, n, fp) == n;
+    g_timing.fwrite_ms += ms_since(t0);
+    g_timing.bytes_out += ok ? n : 0;
+    return ok ? HZ_OK : HZ_EIO;
+}
+
+struct StreamGuard {
+    hipStream_t s = nullptr;
+    ~StreamGuard() { if (s) (void)hipStreamDestroy(s); }
+};
+
+struct EventPair {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EventPair() {
+        for (auto x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+    int create() {
+        for (auto& x : e)
+            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return HZ_EHIP;
+        return HZ_OK;
+    }
+};
+
 }  // namespace
+
+extern "C" int hz_stream_last_timing(hz_stream_timing* t) {
+    if (!t) return HZ_EINVAL;
+    *t = g_timing;
+    return HZ_OK;
+}
 
 static int hz_archive_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     if (!in_path || !out_path || chunk_bytes < 64) return HZ_EINVAL;
@@ -631,43 +728,53 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     if (stat(in_path, &st) != 0) return HZ_ENOENT;
     const uint64_t n = (uint64_t)st.st_size;
     hz_ctx* c;
+    const auto tc = Clock::now();
     int rc = default_ctx(&c);
+    g_timing.alloc_ms += ms_since(tc);
     if (rc) return rc;
     HZ_TRY(hipSetDevice(c->device));
+    Spans spans;
     const uint64_t chunk = std::min<uint64_t>(chunk_bytes, std::max<uint64_t>(n, 16));
     PinnedBuf hin[2];
     DevBuf din[2], dhist;
+    const auto ta = Clock::now();
     for (int i = 0; i < 2; ++i) {
         if ((rc = hin[i].alloc(chunk))) return rc;
         if ((rc = din[i].alloc(chunk + 16))) return rc;
     }
     if ((rc = dhist.alloc(HZ_NSYM * 8))) return rc;
+    g_timing.alloc_ms += ms_since(ta);
     uint8_t last_byte = 0;
     FILE* fp = fopen(in_path, "rb");
     if (!fp) return HZ_EIO;
     std::unique_ptr<FILE, int (*)(FILE*)> fin(fp, fclose);
     // ---- pass 1: histogram
     HZ_TRY(hipMemsetAsync(dhist.p, 0, HZ_NSYM * 8, c->stream));
-    hipEvent_t done[2];
-    HZ_TRY(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
-    HZ_TRY(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
-    std::unique_ptr<hipEvent_t, void (*)(hipEvent_t*)> ev_guard(done, [](hipEvent_t* e) {
-        (void)hipEventDestroy(e[0]);
-        (void)hipEventDestroy(e[1]);
-    });
+    EventPair done;
+    if ((rc = done.create())) return rc;
     for (uint64_t off = 0, k = 0; off < n; off += chunk, ++k) {
         const uint64_t len = std::min(chunk, n - off);
         const int b = (int)(k & 1);
-        if (k >= 2) HZ_TRY(hipEventSynchronize(done[b]));  // buffer b's previous chunk is consumed
+        if (k >= 2) HZ_TRY(hipEventSynchronize(done.e[b]));  // buffer b's previous chunk is consumed
+        spans.fold();
         if ((rc = read_exact(fp, hin[b].p, len))) return rc;
         if (off + len == n && (n & 1)) last_byte = hin[b].p[len - 1];
+        hipEvent_t t0 = spans.mark(c->stream);
         HZ_TRY(hipMemcpyAsync(din[b].p, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
+        spans.add(t0, spans.mark(c->stream), &g_timing.h2d_ms);
+        hipEvent_t t1 = spans.mark(c->stream);
         if ((rc = hz_hist16(c, (const uint8_t*)din[b].p, len, (uint64_t*)dhist.p, 1))) return rc;
-        HZ_TRY(hipEventRecord(done[b], c->stream));
+        spans.add(t1, spans.mark(c->stream), &g_timing.kernel_ms);
+        HZ_TRY(hipEventRecord(done.e[b], c->stream));
     }
     std::vector<uint64_t> hist(HZ_NSYM);
-    HZ_TRY(hipMemcpyAsync(hist.data(), dhist.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
+    {
+        hipEvent_t t0 = spans.mark(c->stream);
+        HZ_TRY(hipMemcpyAsync(hist.data(), dhist.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
+        spans.add(t0, spans.mark(c->stream), &g_timing.d2h_ms);
+    }
     if ((rc = hz_ctx_sync(c))) return rc;
+    const auto th = Clock::now();
     std::unique_ptr<hz_codebook> cb(new hz_codebook());
     if ((rc = hz_codebook_build(hist.data(), cb.get()))) return rc;
     uint64_t hbits = 0, pbits = 0;
@@ -683,56 +790,96 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     uint32_t pend_bits;
     uint8_t pend;
     if ((rc = hz_header_write(cb.get(), n, last_byte, head.data(), head.size(), &hb, &pend_bits, &pend))) return rc;
+    g_timing.host_ms += ms_since(th);
     FILE* fo = fopen(out_path, "wb");
     if (!fo) return HZ_EIO;
     std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
-    if (hb && fwrite(head.data(), 1, hb, fo) != hb) return HZ_EIO;
+    if ((rc = write_exact(fo, head.data(), hb))) return rc;
     uint64_t written = hb;
     const uint64_t nsym_total = n / 2;
     if (nsym_total == 0) {
-        if (pend_bits && fwrite(&pend, 1, 1, fo) != 1) return HZ_EIO;
+        if (pend_bits && (rc = write_exact(fo, &pend, 1))) return rc;
         written += pend_bits ? 1 : 0;
     } else {
         // ---- pass 2: pack chunk by chunk at the running bit offset
+        const auto tu = Clock::now();
         if ((rc = hz_codebook_upload_encode(c, cb.get()))) return rc;
+        g_timing.host_ms += ms_since(tu);
         const uint64_t csym = chunk / 2;
         const uint64_t out_cap = ((32 + csym * (uint64_t)cb->max_len + 31) / 32 + 1) * 4;
-        DevBuf dout, didx;
-        PinnedBuf hout;
-        if ((rc = dout.alloc(out_cap))) return rc;
-        if ((rc = hout.alloc(out_cap))) return rc;
+        DevBuf dout[2], didx;
+        PinnedBuf hout[2];
+        const auto tb = Clock::now();
+        for (int i = 0; i < 2; ++i) {
+            if ((rc = dout[i].alloc(out_cap))) return rc;
+            if ((rc = hout[i].alloc(out_cap))) return rc;
+        }
         if ((rc = didx.alloc(hz_index_bytes(csym)))) return rc;
+        g_timing.alloc_ms += ms_since(tb);
+        StreamGuard cs;  // copy-out stream
+        HZ_TRY(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
+        EventPair packed, copied;
+        if ((rc = packed.create()) || (rc = copied.create())) return rc;
         if (fseek(fp, 0, SEEK_SET) != 0) return HZ_EIO;
         uint32_t sbit = pend_bits;                       // bit of the chunk's first code in its first word
         uint32_t lead = pend_bits ? (uint32_t)(pend >> (8 - pend_bits)) : 0u;
         const uint64_t body = 2 * nsym_total;             // the odd last byte travels in the header
         if ((rc = read_exact(fp, hin[0].p, std::min(chunk, body)))) return rc;
+        int wbuf = -1;          // chunk waiting for its fwrite: buffer, bytes
+        uint64_t wbytes = 0;
         for (uint64_t off = 0, k = 0; off < body; off += chunk, ++k) {
             const int b = (int)(k & 1);
             const uint64_t len = std::min(chunk, body - off);
+            hipEvent_t t0 = spans.mark(c->stream);
             HZ_TRY(hipMemcpyAsync(din[b].p, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
-            if ((rc = hz_pack(c, (const uint8_t*)din[b].p, len, sbit, lead, (uint8_t*)dout.p, out_cap, (uint64_t*)didx.p)))
+            spans.add(t0, spans.mark(c->stream), &g_timing.h2d_ms);
+            if (k >= 2) HZ_TRY(hipStreamWaitEvent(c->stream, copied.e[b], 0));  // dout[b] copied out
+            hipEvent_t t1 = spans.mark(c->stream);
+            if ((rc = hz_pack(c, (const uint8_t*)din[b].p, len, sbit, lead, (uint8_t*)dout[b].p, out_cap,
+                              (uint64_t*)didx.p)))
                 return rc;
+            spans.add(t1, spans.mark(c->stream), &g_timing.kernel_ms);
+            HZ_TRY(hipEventRecord(packed.e[b], c->stream));
             const uint64_t nb = (len / 2 + 2047) / 2048;
             uint64_t end_bit = 0;
             HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
-            // the next chunk's fread overlaps this chunk's upload and pack
+            // host work beside the upload and pack: the previous chunk's fwrite, the next chunk's fread
+            if (wbuf >= 0) {
+                HZ_TRY(hipEventSynchronize(copied.e[wbuf]));
+                if ((rc = write_exact(fo, hout[wbuf].p, wbytes))) return rc;
+                written += wbytes;
+                wbuf = -1;
+            }
             const uint64_t next = off + len;
             if (next < body && (rc = read_exact(fp, hin[1 - b].p, std::min(chunk, body - next)))) return rc;
             if ((rc = hz_ctx_sync(c))) return rc;
+            spans.fold();
             const bool last = next >= body;
             const uint64_t bytes = last ? (end_bit + 7) / 8 : end_bit / 32 * 4;  // complete words until the end
-            const uint64_t copy = last ? bytes : (end_bit + 31) / 32 * 4;        // plus the partial word to carry
-            HZ_TRY(hipMemcpyAsync(hout.p, dout.p, copy, hipMemcpyDeviceToHost, c->stream));
-            if ((rc = hz_ctx_sync(c))) return rc;
-            if (bytes && fwrite(hout.p, 1, bytes, fo) != bytes) return HZ_EIO;
-            written += bytes;
             sbit = (uint32_t)(end_bit % 32);
-            uint32_t w = 0;
-            if (sbit && !last) memcpy(&w, hout.p + bytes, 4);
-            lead = sbit ? (__builtin_bswap32(w) >> (32 - sbit)) : 0u;
+            lead = 0;
+            if (sbit && !last) {  // the partial word, carried into the next chunk as its lead bits
+                uint32_t w = 0;
+                HZ_TRY(hipMemcpyAsync(&w, (const uint8_t*)dout[b].p + bytes, 4, hipMemcpyDeviceToHost, c->stream));
+                if ((rc = hz_ctx_sync(c))) return rc;
+                lead = __builtin_bswap32(w) >> (32 - sbit);
+            }
+            HZ_TRY(hipStreamWaitEvent(cs.s, packed.e[b], 0));
+            hipEvent_t t2 = spans.mark(cs.s);
+            if (bytes) HZ_TRY(hipMemcpyAsync(hout[b].p, dout[b].p, bytes, hipMemcpyDeviceToHost, cs.s));
+            spans.add(t2, spans.mark(cs.s), &g_timing.d2h_ms);
+            HZ_TRY(hipEventRecord(copied.e[b], cs.s));
+            wbuf = b;
+            wbytes = bytes;
         }
+        if (wbuf >= 0) {
+            HZ_TRY(hipEventSynchronize(copied.e[wbuf]));
+            if ((rc = write_exact(fo, hout[wbuf].p, wbytes))) return rc;
+            written += wbytes;
+        }
+        HZ_TRY(hipStreamSynchronize(cs.s));
     }
+    spans.fold();
     if (written != (hbits + pbits + 7) / 8) return HZ_EFORMAT;
     if (verbose) {
         std::cout << "The size of the COMPRESSED file is: " << written << " bytes" << std::endl;
@@ -746,14 +893,20 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
 }
 
 extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
-    return guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+    g_timing = hz_stream_timing();
+    const auto t0 = Clock::now();
+    const int rc = guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+    g_timing.total_ms = ms_since(t0);
+    return rc;
 }
 
 // Streaming extract: the payload passes through a device window of chunk_bytes.
 // Each round decodes as many symbols as the window surely holds (the file's
 // mean code length with a margin; a round whose codes overrun the window is
-// redone at the max_len bound), writes them out, and moves the unconsumed
-// tail of the window to the front of the other buffer before refilling it.
+// redone at the max_len bound), and moves the unconsumed tail of the window to
+// the front of the other buffer before refilling it. The host's fread of the
+// next window overlaps the decode, and its fwrite of a round's output overlaps
+// the next round's upload and index build.
 static int hz_extract_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     if (!in_path || !out_path || chunk_bytes < 4096) return HZ_EINVAL;
     chunk_bytes &= ~(uint64_t)15;
@@ -767,18 +920,26 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
     std::vector<uint8_t> head(std::min<uint64_t>(fsize, 1u << 20));
     int rc = read_exact(fp, head.data(), head.size());
     if (rc) return rc;
+    const auto th = Clock::now();
     std::unique_ptr<hz_codebook> cb(new hz_codebook());
     hz_header_info info;
     if ((rc = hz_header_parse(head.data(), head.size(), cb.get(), &info))) return rc;
+    g_timing.host_ms += ms_since(th);
     FILE* fo = fopen(out_path, "wb");
     if (!fo) return HZ_EIO;
     std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
     const uint64_t nsym = info.n / 2;
     if (nsym > 0) {
         hz_ctx* c;
-        if ((rc = default_ctx(&c))) return rc;
+        const auto tc = Clock::now();
+        rc = default_ctx(&c);
+        g_timing.alloc_ms += ms_since(tc);
+        if (rc) return rc;
         HZ_TRY(hipSetDevice(c->device));
+        Spans spans;
+        const auto tu = Clock::now();
         if ((rc = hz_codebook_upload_decode(c, cb.get()))) return rc;
+        g_timing.host_ms += ms_since(tu);
         const uint64_t W = chunk_bytes;               // window bytes
         const uint64_t pay_total = fsize > info.payload_byte ? fsize - info.payload_byte : 0;
         const uint64_t max_len = std::max<uint32_t>(cb->max_len, 1);
@@ -787,84 +948,114 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
         const uint64_t sym_cap = std::max<uint64_t>(W / 2, kBlockSyms);  // output per round <= W bytes
         DevBuf dwin[2], didx, dout;
         PinnedBuf hin, hout;
+        const auto ta = Clock::now();
         for (int i = 0; i < 2; ++i)
             if ((rc = dwin[i].alloc(W + 16))) return rc;
         if ((rc = didx.alloc(hz_index_bytes(sym_cap)))) return rc;
         if ((rc = dout.alloc(2 * sym_cap + 16))) return rc;
         if ((rc = hin.alloc(W))) return rc;
         if ((rc = hout.alloc(2 * sym_cap))) return rc;
+        g_timing.alloc_ms += ms_since(ta);
         if (fseek(fp, (long)info.payload_byte, SEEK_SET) != 0) return HZ_EIO;
         uint64_t file_left = pay_total, have = 0, done = 0;
         uint64_t bit = info.payload_bit;
         int cur = 0;
+        // symbols this round decodes from the window: what it surely holds
+        auto round_syms = [&]() {
+            const uint64_t left = nsym - done, avail = have * 8 - bit;
+            if (file_left == 0) return std::min(left, sym_cap);
+            uint64_t k = (uint64_t)((double)avail / (mean * 1.03));
+            k = std::min(std::min(left, sym_cap), k);
+            // whole blocks when the window holds at least one; a smaller window keeps k
+            if (k < left && k >= (uint64_t)kBlockSyms) k = k / kBlockSyms * kBlockSyms;
+            return std::max<uint64_t>(k, 1);
+        };
+        uint64_t end_bit = 0;
+        auto launch_index = [&](uint64_t kk) -> int {
+            hipEvent_t t0 = spans.mark(c->stream);
+            int r2 = hz_index_build(c, (const uint8_t*)dwin[cur].p, have, bit, kk, (uint64_t*)didx.p);
+            if (r2) return r2;
+            spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
+            HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(kk), 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+            return HZ_OK;
+        };
         // first fill
         uint64_t r = std::min(W, file_left);
         if ((rc = read_exact(fp, hin.p, r))) return rc;
         HZ_TRY(hipMemsetAsync(dwin[cur].p, 0, W + 16, c->stream));
-        HZ_TRY(hipMemcpyAsync(dwin[cur].p, hin.p, r, hipMemcpyHostToDevice, c->stream));
+        {
+            hipEvent_t t0 = spans.mark(c->stream);
+            HZ_TRY(hipMemcpyAsync(dwin[cur].p, hin.p, r, hipMemcpyHostToDevice, c->stream));
+            spans.add(t0, spans.mark(c->stream), &g_timing.h2d_ms);
+        }
         have = r;
         file_left -= r;
+        uint64_t k = round_syms();
+        if ((rc = launch_index(k))) return rc;
         while (done < nsym) {
-            const uint64_t left = nsym - done;
-            const uint64_t avail = have * 8 - bit;
-            uint64_t k;
-            if (file_left == 0) {
-                k = std::min(left, sym_cap);
-            } else {
-                k = (uint64_t)((double)avail / (mean * 1.03));
-                k = std::min(std::min(left, sym_cap), k);
-                // whole blocks when the window holds at least one; a smaller window keeps k
-                if (k < left && k >= (uint64_t)kBlockSyms) k = k / kBlockSyms * kBlockSyms;
-                k = std::max<uint64_t>(k, 1);
-            }
-            uint64_t end_bit = 0;
-            for (int attempt = 0;; ++attempt) {
-                if ((rc = hz_index_build(c, (const uint8_t*)dwin[cur].p, have, bit, k, (uint64_t*)didx.p))) return rc;
-                HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(k), 8, hipMemcpyDeviceToHost,
-                                      c->stream));
-                if ((rc = hz_ctx_sync(c))) return rc;
-                if (end_bit <= have * 8 || file_left == 0) break;
-                if (attempt) return HZ_EFORMAT;
-                k = std::max<uint64_t>(avail / max_len, 1);  // codes surely inside the window
+            if ((rc = hz_ctx_sync(c))) return rc;
+            if (end_bit > have * 8 && file_left > 0) {  // the round's codes overran the window: redo at the bound
+                k = std::max<uint64_t>((have * 8 - bit) / max_len, 1);
+                if ((rc = launch_index(k)) || (rc = hz_ctx_sync(c))) return rc;
             }
             if (end_bit > have * 8) return HZ_EFORMAT;    // truncated file
+            hipEvent_t t0 = spans.mark(c->stream);
             if ((rc = hz_decode(c, (const uint8_t*)dwin[cur].p, have, k, (const uint64_t*)didx.p, (uint8_t*)dout.p)))
                 return rc;
+            spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
+            hipEvent_t t1 = spans.mark(c->stream);
             HZ_TRY(hipMemcpyAsync(hout.p, dout.p, 2 * k, hipMemcpyDeviceToHost, c->stream));
-            // move the unconsumed tail to the other window and refill it behind
+            spans.add(t1, spans.mark(c->stream), &g_timing.d2h_ms);
+            // move the unconsumed tail to the other window and read the refill behind the decode
             const uint64_t used = end_bit / 8, tail = have - used;
             const int nxt = cur ^ 1;
-            if (done + k < nsym) {
+            const bool more = done + k < nsym;
+            r = 0;
+            if (more) {
                 if (tail) HZ_TRY(hipMemcpyAsync(dwin[nxt].p, (const uint8_t*)dwin[cur].p + used, tail,
                                                 hipMemcpyDeviceToDevice, c->stream));
                 r = std::min(W - tail, file_left);
-                if ((rc = read_exact(fp, hin.p, r))) return rc;  // overlaps the decode
-            } else {
-                r = 0;
+                if ((rc = read_exact(fp, hin.p, r))) return rc;
             }
             if ((rc = hz_ctx_sync(c))) return rc;    // decode, output copy and tail move done
-            if (fwrite(hout.p, 1, 2 * k, fo) != 2 * k) return HZ_EIO;
-            done += k;
-            if (done < nsym) {
+            spans.fold();
+            const uint64_t kdone = k;
+            if (more) {  // next window and its index build, beside this round's fwrite
                 if (r < W - tail) HZ_TRY(hipMemsetAsync((uint8_t*)dwin[nxt].p + tail + r, 0, W + 16 - tail - r, c->stream));
-                if (r) HZ_TRY(hipMemcpyAsync((uint8_t*)dwin[nxt].p + tail, hin.p, r, hipMemcpyHostToDevice, c->stream));
+                if (r) {
+                    hipEvent_t t2 = spans.mark(c->stream);
+                    HZ_TRY(hipMemcpyAsync((uint8_t*)dwin[nxt].p + tail, hin.p, r, hipMemcpyHostToDevice, c->stream));
+                    spans.add(t2, spans.mark(c->stream), &g_timing.h2d_ms);
+                }
                 have = tail + r;
                 file_left -= r;
                 bit = end_bit % 8;
                 cur = nxt;
+                done += kdone;
+                k = round_syms();
+                if ((rc = launch_index(k))) return rc;
+            } else {
+                done += kdone;
             }
+            if ((rc = write_exact(fo, hout.p, 2 * kdone))) return rc;
         }
+        spans.fold();
     }
     if (info.is_odd) {
         const uint8_t b = (uint8_t)info.last_byte;
-        if (fwrite(&b, 1, 1, fo) != 1) return HZ_EIO;
+        if ((rc = write_exact(fo, &b, 1))) return rc;
     }
     if (verbose) std::cout << "Decompression is complete" << std::endl;
     return HZ_OK;
 }
 
 extern "C" int hz_extract_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
-    return guarded([&] { return hz_extract_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+    g_timing = hz_stream_timing();
+    const auto t0 = Clock::now();
+    const int rc = guarded([&] { return hz_extract_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+    g_timing.total_ms = ms_since(t0);
+    return rc;
 }
 
 static int hz_encode_host_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
@@ -942,7 +1133,7 @@ extern "C" int hz_extract_file(const char* path, char* out_name, size_t out_name
         return HZ_ENOENT;
     }
     std::string name = output_name();
-    int rc = hz_extract_stream(path, name.c_str(), kArchiveChunk, 0);
+    int rc = hz_extract_stream(path, name.c_str(), kExtractWindow, 0);
     if (rc) {
         remove(name.c_str());
         if (verbose) std::cerr << "extract: " << hz_strerror(rc) << std::endl;

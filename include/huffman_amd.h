@@ -191,13 +191,30 @@ int hz_archive_file(const char *path, int verbose);
  * over the file in chunk_bytes pieces (histogram, then pack at the running bit
  * offset with the previous chunk's partial word carried as `lead`). Output is
  * byte-identical to the whole-buffer encoder. hz_archive_file uses it with
- * 1 GiB chunks. Replaces the whole-file buffers of Compressor.cu:343-367,585-601. */
+ * 256 MiB chunks. Replaces the whole-file buffers of Compressor.cu:343-367,585-601. */
 int hz_archive_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* Streaming extract of in_path into out_path through a device window of
  * chunk_bytes of payload (index-less: hz_index_build per window), bounded
- * host and device memory. hz_extract_file uses it with 1 GiB windows.
+ * host and device memory. hz_extract_file uses it with 512 MiB windows.
  * Replaces the whole-file buffers of Decompressor.cu:65-114,259-291. */
 int hz_extract_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
+/* Stage split of the calling thread's last hz_archive_stream /
+ * hz_extract_stream call (hz_archive_file / hz_extract_file included). Stage
+ * times are busy times: host file reads and writes overlap the device's
+ * copies and kernels, so they do not add up to total_ms. */
+typedef struct hz_stream_timing {
+    double total_ms;   /* wall clock of the call */
+    double fread_ms;   /* host: file reads */
+    double fwrite_ms;  /* host: file writes */
+    double alloc_ms;   /* host: device context, device buffers, pinned host buffers */
+    double host_ms;    /* host: codebook build, header write / parse, table uploads */
+    double h2d_ms;     /* device: host-to-device copies */
+    double kernel_ms;  /* device: histogram, pack, index build, decode */
+    double d2h_ms;     /* device: device-to-host copies */
+    uint64_t bytes_in;   /* bytes read from in_path */
+    uint64_t bytes_out;  /* bytes written to out_path */
+} hz_stream_timing;
+int hz_stream_last_timing(hz_stream_timing *t);
 /* `extract <path>`: writes ./DECOMPRESSED_FILE or DECOMPRESSED_FILE(k)
  * (Decompressor.cu:47-114,185-219). out_name may be NULL. */
 int hz_extract_file(const char *path, char *out_name, size_t out_name_cap, int verbose);

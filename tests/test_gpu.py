@@ -184,9 +184,13 @@ def test_archive_stream_matches_whole_buffer(hz, tmp_path, n, chunk):
     src = tmp_path / "in.bin"
     src.write_bytes(data)
     out = hz.archive_stream(src, tmp_path / "in.bin.compressed", chunk_bytes=chunk)
+    t = hz.stream_timing()
     blob = open(out, "rb").read()
     assert blob == oracle_lib.encode(data)
     assert hz.decode(blob) == data
+    # stage split: two passes over the input (the second without the odd last byte), the archive written once
+    assert t["bytes_in"] == n + (n - n % 2) and t["bytes_out"] == len(blob)
+    assert t["total_ms"] > 0 and min(t[k] for k in ("fread_ms", "fwrite_ms", "h2d_ms", "kernel_ms", "d2h_ms")) >= 0
 
 
 @pytest.mark.parametrize("kind", ["fib28", "uniform"])
@@ -226,7 +230,10 @@ def test_extract_stream_roundtrip(hz, tmp_path, kind, n, window):
     blob = oracle_lib.encode(data)
     (tmp_path / "in.compressed").write_bytes(blob)
     out = hz.extract_stream(tmp_path / "in.compressed", tmp_path / "out", chunk_bytes=window)
+    t = hz.stream_timing()
     assert open(out, "rb").read() == data
+    assert t["bytes_out"] == len(data) and t["total_ms"] > 0
+    assert min(t[k] for k in ("fread_ms", "fwrite_ms", "h2d_ms", "kernel_ms", "d2h_ms")) >= 0
 
 
 @pytest.mark.parametrize("name", INPUTS)
