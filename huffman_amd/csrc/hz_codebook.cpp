@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <queue>
 #include <vector>
 
@@ -22,24 +23,35 @@
 
 namespace {
 
-// LSD radix sort of u64 keys with 16-bit digits over the bits in use.
-// LSD radix sort, 16-bit digits from bit `lo` (digits below lo are already in order).
-void radix_sort_u64(std::vector<uint64_t>& k, int lo = 0) {
-    if (k.size() < 2) return;
+// LSD radix sort of u64 keys, 11-bit digits (a 2048-entry count table stays
+// in L1) over bits [lo, highest set bit]; a digit every key shares is skipped.
+// `tmp` is scratch of k's size. Stable.
+void radix_sort_u64(uint64_t* k, uint64_t* tmp, uint32_t n, int lo) {
+    if (n < 2) return;
     uint64_t mx = 0;
-    for (uint64_t v : k) mx |= v;
-    int bits = 64 - __builtin_clzll(mx | 1);
-    std::vector<uint64_t> tmp(k.size());
-    std::vector<uint32_t> cnt(65536);
-    for (int sh = lo; sh < bits; sh += 16) {
-        std::fill(cnt.begin(), cnt.end(), 0u);
-        for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
+    for (uint32_t i = 0; i < n; ++i) mx |= k[i];
+    const int bits = 64 - __builtin_clzll(mx | 1);
+    uint32_t cnt[2048];
+    uint64_t* const out = k;
+    for (int sh = lo; sh < bits; sh += 11) {
+        memset(cnt, 0, sizeof(cnt));
+        for (uint32_t i = 0; i < n; ++i) cnt[(k[i] >> sh) & 2047]++;
+        if (cnt[(k[0] >> sh) & 2047] == n) continue;  // one digit value: already in order
         uint32_t sum = 0;
-        for (auto& c : cnt) { uint32_t t = c; c = sum; sum += t; }
-        for (uint64_t v : k) tmp[cnt[(v >> sh) & 0xffff]++] = v;
-        k.swap(tmp);
+        for (auto& c : cnt) { const uint32_t t = c; c = sum; sum += t; }
+        for (uint32_t i = 0; i < n; ++i) tmp[cnt[(k[i] >> sh) & 2047]++] = k[i];
+        std::swap(k, tmp);
     }
+    if (k != out) memcpy(out, k, (size_t)n * sizeof(uint64_t));  // the result is in the scratch
 }
+
+// Per-thread scratch of the codebook builder (no zero-fill per call).
+struct CbScratch {
+    std::unique_ptr<uint64_t[]> keys{new uint64_t[HZ_NSYM]}, tmp{new uint64_t[HZ_NSYM]};
+    std::unique_ptr<uint64_t[]> f{new uint64_t[2 * HZ_NSYM]}, cw{new uint64_t[2 * HZ_NSYM]};
+    std::unique_ptr<uint32_t[]> lc{new uint32_t[2 * HZ_NSYM]}, rc{new uint32_t[2 * HZ_NSYM]};
+    std::unique_ptr<uint8_t[]> dep{new uint8_t[2 * HZ_NSYM]};
+};
 
 struct BitWriter {
     uint8_t* p;
@@ -86,18 +98,19 @@ extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
     memset(cb->len, 0, sizeof(cb->len));
     memset(cb->code, 0, sizeof(cb->code));
     cb->nsym = cb->max_len = cb->min_len = 0;
-    std::vector<uint64_t> keys;
-    keys.reserve(HZ_NSYM);
+    thread_local CbScratch sc;
+    uint64_t* keys = sc.keys.get();
+    uint32_t U = 0;
     for (uint32_t s = 0; s < HZ_NSYM; ++s) {
         if (hist[s]) {
             if (hist[s] >> 47) return HZ_EINVAL;  // > 2^47 symbols: out of range
-            keys.push_back((hist[s] << 16) | s);
+            keys[U++] = (hist[s] << 16) | s;
         }
     }
-    const uint32_t U = (uint32_t)keys.size();
     cb->nsym = U;
     if (U == 0) return HZ_OK;
-    radix_sort_u64(keys, 16);  // keys were built in symbol order: a stable sort by count == (count, symbol) order (thrust's)
+    // keys were built in symbol order: a stable sort by count == (count, symbol) order (thrust's)
+    radix_sort_u64(keys, sc.tmp.get(), U, 16);
     for (uint32_t i = 0; i < U; ++i) cb->order[i] = (uint16_t)(keys[i] & 0xffff);
     if (U == 1) {  // reference defect B4: its code would be empty; use "0"
         cb->len[cb->order[0]] = 1;
@@ -106,8 +119,8 @@ extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
         return HZ_OK;
     }
     const uint32_t nn = 2 * U - 1;
-    std::vector<uint64_t> f(nn);
-    std::vector<uint32_t> lc(nn), rc(nn);
+    uint64_t* f = sc.f.get();
+    uint32_t *lc = sc.lc.get(), *rc = sc.rc.get();
     for (uint32_t i = 0; i < U; ++i) f[i] = keys[i] >> 16;
     uint32_t li = 0, qi = U;
     for (uint32_t nx = U; nx < nn; ++nx) {
@@ -120,23 +133,23 @@ extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
         lc[nx] = pick[0];
         rc[nx] = pick[1];
     }
-    std::vector<uint32_t> dep(nn);
-    std::vector<uint64_t> cw(nn);
+    uint8_t* dep = sc.dep.get();
+    uint64_t* cw = sc.cw.get();
     dep[nn - 1] = 0;
     cw[nn - 1] = 0;
     for (uint32_t v = nn - 1; v >= U; --v) {
-        dep[lc[v]] = dep[v] + 1; cw[lc[v]] = (cw[v] << 1) | 1u;  // first child '1'
-        dep[rc[v]] = dep[v] + 1; cw[rc[v]] = cw[v] << 1;         // second child '0'
-        if (dep[lc[v]] > HZ_MAXLEN) return HZ_ETOOLONG;
+        const uint32_t d = dep[v] + 1u;
+        if (d > HZ_MAXLEN) return HZ_ETOOLONG;
+        dep[lc[v]] = (uint8_t)d; cw[lc[v]] = (cw[v] << 1) | 1u;  // first child '1'
+        dep[rc[v]] = (uint8_t)d; cw[rc[v]] = cw[v] << 1;         // second child '0'
     }
     uint32_t mx = 0, mn = 255;
     for (uint32_t i = 0; i < U; ++i) {
-        const uint32_t s = cb->order[i];
-        if (dep[i] > HZ_MAXLEN) return HZ_ETOOLONG;
-        cb->len[s] = (uint8_t)dep[i];
+        const uint32_t s = cb->order[i], d = dep[i];
+        cb->len[s] = (uint8_t)d;
         cb->code[s] = cw[i];
-        mx = std::max(mx, dep[i]);
-        mn = std::min(mn, dep[i]);
+        mx = std::max(mx, d);
+        mn = std::min(mn, d);
     }
     cb->max_len = mx;
     cb->min_len = mn;
@@ -271,20 +284,30 @@ std::vector<uint32_t> build_enc_dense(const hz_codebook* cb) {
 uint32_t choose_hot_mask(const hz_codebook* cb) {
     static const uint32_t cand[] = {0x8000, 0xffff, 0x8080, 0xc0c0, 0x80ff, 0xff80, 0xa0a0, 0xf0f0,
                                     0x8888, 0xcccc, 0xaaaa, 0x8001, 0xff00, 0x80c0, 0xe0e0, 0x9999};
-    // weight 2^-L in fixed point (2^-56 units); ineligible (absent or > 25 bits)
-    // symbols escape whatever the pairing, so they do not rank the masks
-    static thread_local std::vector<uint64_t> w(HZ_NSYM);
+    // weight 2^-L in fixed point (2^-25 units, fits u32); ineligible (absent or > 25
+    // bits) symbols escape whatever the pairing, so they do not rank the masks
+    static_assert(kHotMaxLen <= 25, "u32 weights");
+    thread_local std::unique_ptr<uint32_t[]> wbuf(new uint32_t[HZ_NSYM]);
+    uint32_t* w = wbuf.get();
     for (uint32_t s = 0; s < HZ_NSYM; ++s) {
         const uint32_t L = cb->len[s];
-        w[s] = (L && L <= (uint32_t)kHotMaxLen) ? (1ull << (HZ_MAXLEN - L)) : 0ull;
+        w[s] = (L && L <= (uint32_t)kHotMaxLen) ? (1u << (kHotMaxLen - L)) : 0u;
     }
     uint32_t best = 0x8000;
     uint64_t best_miss = ~0ull;
     for (uint32_t m : cand) {
+        // s ^ m for s in an 8-aligned run is an 8-aligned run permuted by m & 7
+        const uint32_t hi = m & ~7u, lo = m & 7u;
         uint64_t miss = 0;
-        for (uint32_t s = 0; s < 32768; ++s) {
-            const uint64_t wa = w[s], wb = w[s ^ m];  // s ^ m: the partner with bit 15 set
-            miss += wa < wb ? wa : wb;                // the slot keeps the heavier one
+        for (uint32_t s0 = 0; s0 < 32768; s0 += 8) {
+            const uint32_t* a = w + s0;
+            const uint32_t* b = w + (s0 ^ hi);
+            uint32_t part = 0;  // <= 8 * 2^24
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t wa = a[j], wb = b[j ^ lo];  // the partner with bit 15 set
+                part += wa < wb ? wa : wb;                 // the slot keeps the heavier one
+            }
+            miss += part;
         }
         if (miss < best_miss) { best_miss = miss; best = m; }
     }

@@ -281,9 +281,11 @@ static int hz_codebook_upload_encode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.min_len = (int)cb->min_len;
     const int mode = select_enc_mode(cb);
     {
+        // expected bits per symbol under the code's own distribution (Kraft weights 2^-L)
+        uint64_t nl[HZ_MAXLEN + 1] = {0};
+        for (uint32_t s = 0; s < HZ_NSYM; ++s) nl[cb->len[s]]++;
         double avg = 0.0;
-        for (uint32_t s = 0; s < HZ_NSYM; ++s)
-            if (cb->len[s]) avg += ldexp(1.0, -(int)cb->len[s]) * cb->len[s];
+        for (int L = 1; L <= HZ_MAXLEN; ++L) avg += ldexp((double)nl[L], -L) * L;
         t.enc_avg_bits = avg > 0.0 ? avg : 1.0;
     }
     if (mode == ENC_FIXED16) {
