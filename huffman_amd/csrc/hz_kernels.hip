@@ -1914,8 +1914,8 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k0 < y.nseg; k0 += 2 * stride) {
         BitReader r[2];
-        uint64_t s0[2], pos[2], n[2];
-        uint32_t cw[2], cur[2];
+        uint64_t s0[2];
+        uint32_t d[2], n[2], cw[2], cur[2];  // 32-bit: bits and codewords relative to the segment
         uint4 q[2];
         bool act[2];
         uint4* bm[2];
@@ -1924,8 +1924,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
             const uint64_t k = k0 + c * stride;
             act[c] = k < y.nseg;
             s0[c] = y.start + (act[c] ? k : k0) * kSegBits;
-            pos[c] = s0[c];
-            n[c] = 0;
+            d[c] = n[c] = 0;
             cw[c] = cur[c] = 0;
             q[c] = make_uint4(0, 0, 0, 0);
             bm[c] = reinterpret_cast<uint4*>(y.bmp + (act[c] ? k : k0) * kBmpWords);
@@ -1944,10 +1943,10 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
         while (act[0] || act[1]) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                if (act[c] && cw[c] < kBmpWords) {
-                    const uint32_t d = (uint32_t)(pos[c] - s0[c]);
-                    while ((d >> 5) != cw[c] && cw[c] < kBmpWords) put(c);
-                    cur[c] |= 1u << (d & 31);
+                // codes <= 32 bits: the boundary's bitmap word advances by at most one per step
+                if (act[c] && d[c] < kBmpBits) {
+                    if ((d[c] >> 5) != cw[c]) put(c);
+                    cur[c] |= 1u << (d[c] & 31);
                 }
                 br_refill(r[c], a);
             }
@@ -1959,9 +1958,9 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
                 if (L[c] == 0) { atomicOr(a.err, 2u); act[c] = false; continue; }
                 r[c].buf <<= L[c];
                 r[c].nb -= L[c];
-                pos[c] += L[c];
+                d[c] += L[c];
                 ++n[c];
-                act[c] = pos[c] < s0[c] + kSegBits;
+                act[c] = d[c] < kSegBits;
             }
         }
 #pragma unroll
@@ -1969,7 +1968,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
             const uint64_t k = k0 + c * stride;
             if (k >= y.nseg) continue;
             while (cw[c] < kBmpWords) put(c);
-            y.exit0[k] = pos[c];
+            y.exit0[k] = s0[c] + d[c];
             y.cnt0[k] = n[c];
         }
     }
