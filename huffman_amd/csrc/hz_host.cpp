@@ -699,7 +699,20 @@ int write_exact(FILE* fp, const uint8_t* p, uint64_t n) {
 
 struct StreamGuard {
     hipStream_t s = nullptr;
-    ~StreamGuard() { if (s) (void)hipStreamDestroy(s); }
+    ~StreamGuard() {
+        if (s) {
+            (void)hipStreamSynchronize(s);  // no copy may outlive the buffers it targets
+            (void)hipStreamDestroy(s);
+        }
+    }
+};
+
+// Declared after a function's pinned and device buffers, so it runs before
+// they are freed: an early return (I/O error) waits for the copies in flight.
+struct DrainGuard {
+    hipStream_t s;
+    explicit DrainGuard(hipStream_t st) : s(st) {}
+    ~DrainGuard() { (void)hipStreamSynchronize(s); }
 };
 
 struct EventPair {
@@ -746,6 +759,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     }
     if ((rc = dhist.alloc(HZ_NSYM * 8))) return rc;
     g_timing.alloc_ms += ms_since(ta);
+    DrainGuard drain_in(c->stream);
     uint8_t last_byte = 0;
     FILE* fp = fopen(in_path, "rb");
     if (!fp) return HZ_EIO;
@@ -818,6 +832,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         }
         if ((rc = didx.alloc(hz_index_bytes(csym)))) return rc;
         g_timing.alloc_ms += ms_since(tb);
+        DrainGuard drain_out(c->stream);
         StreamGuard cs;  // copy-out stream
         HZ_TRY(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
         EventPair packed, copied;
@@ -958,6 +973,7 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
         if ((rc = hin.alloc(W))) return rc;
         if ((rc = hout.alloc(2 * sym_cap))) return rc;
         g_timing.alloc_ms += ms_since(ta);
+        DrainGuard drain(c->stream);
         if (fseek(fp, (long)info.payload_byte, SEEK_SET) != 0) return HZ_EIO;
         uint64_t file_left = pay_total, have = 0, done = 0;
         uint64_t bit = info.payload_bit;
