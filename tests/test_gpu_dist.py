@@ -102,3 +102,22 @@ def test_sharded_rehearsal_equals_single_stream(tmp_path, world, n_total, kind):
                        start_method="spawn")
     got = [open(tmp_path / f"rank{r}.txt").read() for r in range(world)]
     assert got == ["ok"] * world, got
+
+
+def test_bench_rehearsal_three_ranks(tmp_path):
+    """bench.py's own N > 1 step (pipelined: histogram all-gather, offsets from the
+    gathered local histograms) under torch.distributed.run, every rank on cuda:0:
+    each rank's round trip and the reassembled whole stream must be bit-exact."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "3", "--rehearse", "--size", str(96 << 20), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 3 and line["roundtrip_bit_exact"]
+    assert line["reassembly_outside_step"]["whole_stream_decoded_bit_exact"]
