@@ -532,7 +532,7 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
 }
 
 constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
-constexpr int kPackCopyIters = 16;       // slot copy-out: 16 x 64 words covers a 1024-word slot
+constexpr int kPackCopyIters = 16;       // slot copy-out covers 16 x 64 words: a 1024-word slot
 
 // One block of a wave between its lookup and its emit: the lane's 32 entries,
 // the entry of one of the previous block's last 32 symbols, the lane's bits,
@@ -608,34 +608,54 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     const bool last = blk + 1 == a.nblocks;
     const uint64_t wfirst = bstart >> 5;
     const uint32_t nwords = (uint32_t)((bend >> 5) - wfirst);  // words completed inside the block
-    if (slot && !last && nwords <= a.slot_words) {
+    const uint32_t sh4 = (uint32_t)(wfirst & 3);  // slot word i holds output word (wfirst & ~3) + i
+    if (slot && !last && nwords + sh4 <= a.slot_words) {
         // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
         // own: emit with the leading bits zero, then OR in the previous
-        // lane's tail once all lanes are done.
+        // lane's tail once all lanes are done. The slot is laid out like the
+        // output modulo 16 bytes, so the copy-out moves aligned 16-byte chunks.
+        uint32_t* sl = slot + sh4;  // sl[w] = output word wfirst + w
         uint64_t acc = 0;
         if constexpr (MODE == ENC_WIDE) {  // codes may exceed 32 bits
             uint32_t na = (uint32_t)(o & 31);
-            pack_emit<MODE, true>(b.e, acc, na, slot + (uint32_t)((o >> 5) - wfirst), true);
+            pack_emit<MODE, true>(b.e, acc, na, sl + (uint32_t)((o >> 5) - wfirst), true);
         } else {
-            pack_emit_lds<MODE>(b.e, acc, (uint32_t)(o - (wfirst << 5)), slot);
+            pack_emit_lds<MODE>(b.e, acc, (uint32_t)(o - (wfirst << 5)), sl);
         }
         const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)ptail, (int)(uint32_t)acc, kDppWaveShr1,
                                                                     0xf, 0xf, false);  // lane 0: ptail
         const uint32_t h = (uint32_t)(o & 31);
-        if (h) slot[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
+        if (h) sl[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
         __builtin_amdgcn_wave_barrier();
         if (fits) {
             if constexpr (MODE != ENC_WIDE) {  // host: slot_words <= kPackCopyIters * kWave
-                // a fixed count of full-wave stores (lanes past the block rewrite its last
-                // word with the same value), so later load waits count them statically
+                // Output words [wfirst, wfirst + nwords): a partial first 16-byte chunk
+                // (its words before wfirst are the previous block's), whole chunks,
+                // a partial last chunk. A fixed count of stores (1 + 4 + 1; lanes with
+                // nothing to write rewrite the block's first word with its own value),
+                // so later load waits count them statically. nwords >= 64.
+                const uint64_t base4 = wfirst & ~3ull;
+                const uint32_t wend = sh4 + nwords;                 // slot index past the block
+                const uint32_t cf = sh4 ? 1u : 0u, cl = wend >> 2;  // whole chunks [cf, cl)
+                const uint32_t nhead = sh4 ? 4u - sh4 : 0u, ntail = wend & 3u;
+                {
+                    const uint32_t i = (uint32_t)lane < nhead ? sh4 + (uint32_t)lane : sh4;
+                    a.out[base4 + i] = bswap32(slot[i]);
+                }
 #pragma unroll
-                for (int it = 0; it < kPackCopyIters; ++it) {
-                    uint32_t w = (uint32_t)lane + (uint32_t)it * kWave;
-                    w = w < nwords ? w : nwords - 1;
-                    a.out[wfirst + w] = bswap32(slot[w]);
+                for (int it = 0; it < kPackCopyIters / 4; ++it) {
+                    uint32_t c = cf + (uint32_t)lane + (uint32_t)it * kWave;
+                    c = c < cl ? c : cl - 1;
+                    const uint4 v = reinterpret_cast<const uint4*>(slot)[c];
+                    reinterpret_cast<uint4*>(a.out + base4)[c] =
+                        make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+                }
+                {
+                    const uint32_t i = (uint32_t)lane < ntail ? 4u * cl + (uint32_t)lane : sh4;
+                    a.out[base4 + i] = bswap32(slot[i]);
                 }
             } else {
-                for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(slot[w]);
+                for (uint32_t w = lane; w < nwords; w += kWave) a.out[wfirst + w] = bswap32(sl[w]);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -928,7 +948,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     uint32_t waves = free_words / est_words;
     waves = waves > kMaxWaves ? kMaxWaves : waves;
     a.slot_words = 0;
-    if (waves >= 6) a.slot_words = free_words / waves;
+    if (waves >= 6) a.slot_words = free_words / waves & ~3u;  // 16-byte aligned slots
     else waves = kMaxWaves;  // no room for slots: lanes store directly
     if (t.enc_mode != ENC_WIDE && a.slot_words > (uint32_t)(kPackCopyIters * kWave))
         a.slot_words = kPackCopyIters * kWave;  // larger blocks take the direct path
