@@ -1733,30 +1733,28 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
 // Block index of an index-less stream (a .compressed file from the reference
 // encoder; Decompressor.cu:259-291 decodes it serially). Huffman codes
 // resynchronise: a decoder started at an arbitrary bit falls onto the true
-// codeword boundaries after some codewords (measured on Zipf(1.1): median 81
-// bits, p99 600). The stream is cut into 4096-bit segments, one lane each:
-//   k_sync_scan : decode segment k from its first bit to the first boundary
-//                 past its end -> exit0[k], cnt0[k] and a bitmap of every
-//                 boundary of that path in the segment
-//   k_sync_iter : the true path enters k at exit[k-1]; follow it until it
-//                 lands on a bitmap boundary (from there both paths agree:
-//                 count = cnt0 - boundaries before + codewords walked, exit =
-//                 exit0) or leaves the segment (count and exit from the walk).
-//                 Repeated (host loop) for segments whose entry changed,
-//                 until no exit changes: chains of unsynchronised segments
-//                 are rare and short.
-//   k_scan_*    : exclusive scan of counts -> first symbol number per segment
-//   k_sync_emit : decode every segment again from its true entry and write
-//                 block starts and raw chain positions
-//   k_sync_subs : chain positions relative to their block, max block bits
+// codeword boundaries after some codewords (measured on Zipf(1.1): median 83
+// bits, p99 590). The stream is cut into 4096-bit segments, one lane each, and
+// every segment keeps a BOUNDARY BITMAP (bit d of its row = a codeword starts
+// at segment bit d), one bit per payload bit:
+//   k_sync_scan   : decode segment k from its first bit to the first boundary
+//                   past its end -> exit[k], count[k] and the bitmap of every
+//                   boundary of that path in the segment
+//   k_sync_iter   : the true path enters k at exit[k-1]; follow it until it
+//                   lands on a bitmap boundary (from there both paths agree)
+//                   or leaves the segment, rewriting the bitmap up to there
+//                   with the true boundaries (count and exit follow). Repeated
+//                   (host loop) for segments whose entry changed, until no
+//                   exit changes: chains of unsynchronised segments are rare.
+//   k_scan_*      : exclusive scan of counts -> first codeword number per segment
+//   k_sync_select : the bitmap now holds exactly the true boundaries; every
+//                   8th one (a chain start) and every 2048th (a block start)
+//                   is picked by popcounts -- no second walk of the stream
+//   k_sync_subs   : chain positions relative to their block, max block bits
 // ===========================================================================
 constexpr uint32_t kSegBits = 4096;
 constexpr int kSyncThreads = 1024;
-// The scan keeps the boundary bitmap of a segment's first kBmpBits only: the
-// true path lands on a scan-path boundary after a median 81 bits (p99 600,
-// Zipf); one that has not within the prefix walks on to the segment's end.
-constexpr uint32_t kBmpBits = 1024;
-constexpr uint32_t kBmpWords = kBmpBits / 32;
+constexpr uint32_t kBmpWords = kSegBits / 32;  // bitmap row of a segment
 
 // Per-lane bit reader over the payload. Words come from 16-byte chunks with
 // the next chunk always in flight (128 bits of lookahead, a quarter of the
@@ -1835,11 +1833,9 @@ HZ_DEV uint32_t br_next(BitReader& r, const DecArgs& a, const uint32_t* lds, uin
 struct SyncArgs {
     uint64_t start;                 // stream bit of the first symbol (payload view: + bit_adj)
     uint64_t nseg;
-    unsigned long long* exit0;      // scan path: first boundary >= segment end
-    unsigned long long* cnt0;       // scan path: codewords inside the segment
-    uint32_t* bmp;                  // scan path: boundaries in the first kBmpBits, kBmpWords per segment
-    unsigned long long* ex[2];      // true exits, ping-pong between iterations
-    unsigned long long* cnt;        // true counts
+    uint32_t* bmp;                  // boundary bitmap, kBmpWords per segment
+    unsigned long long* ex[2];      // exits (scan: ex[0]), ping-pong between iterations
+    unsigned long long* cnt;        // boundaries in the segment's bitmap row
     uint32_t* dirty[2];             // entry changed in the previous iteration
     uint32_t* changed;              // exits changed in this iteration
 };
@@ -1871,10 +1867,8 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
         };
         while (pos < s1) {
             const uint32_t d = (uint32_t)(pos - s0);
-            if (cw < kBmpWords) {
-                while ((d >> 5) != cw && cw < kBmpWords) put();
-                cur |= 1u << (d & 31);  // past the prefix: never stored
-            }
+            while ((d >> 5) != cw) put();
+            cur |= 1u << (d & 31);
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
@@ -1882,15 +1876,15 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
             ++n;
         }
         while (cw < kBmpWords) put();
-        y.exit0[k] = pos;
-        y.cnt0[k] = n;
+        y.ex[0][k] = pos;
+        y.cnt[k] = n;
     }
 }
 
 // Two segments per lane in lockstep (codebooks the pipelined decoder takes:
 // codes <= 32 bits, every global lookup a leaf): both streams' LUT walks and
 // gathers are in flight together, so one stream's lookup latency hides the
-// other's. Same outputs as the one-segment kernels.
+// other's. Same outputs as the one-segment kernel.
 template <typename A>
 HZ_DEV void br_refill(BitReader& r, const A& a) {
     if (r.nb <= 32) {
@@ -1964,7 +1958,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 // codes <= 32 bits: the boundary's bitmap word advances by at most one per step
-                if (act[c] && d[c] < kBmpBits) {
+                if (act[c]) {
                     if ((d[c] >> 5) != cw[c]) put(c);
                     cur[c] |= 1u << (d[c] & 31);
                 }
@@ -1988,85 +1982,18 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
             const uint64_t k = k0 + c * stride;
             if (k >= y.nseg) continue;
             while (cw[c] < kBmpWords) put(c);
-            y.exit0[k] = s0[c] + d[c];
-            y.cnt0[k] = n[c];
+            y.ex[0][k] = s0[c] + d[c];
+            y.cnt[k] = n[c];
         }
     }
 }
 
-__global__ __launch_bounds__(kSyncThreads) void k_sync_emit2(DecArgs a, SyncArgs y, const unsigned long long* exits,
-                                                  const unsigned long long* first, unsigned long long* starts,
-                                                  uint16_t* subs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, a.lds_img, a.lds_words);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k0 < y.nseg; k0 += 2 * stride) {
-        BitReader r[2];
-        uint64_t i[2], pos[2], s1[2], acc[2], g[2];
-        uint32_t have[2];
-        bool act[2], live[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const uint64_t k = k0 + c * stride;
-            const uint64_t kk = k < y.nseg ? k : k0;
-            i[c] = first[kk];
-            act[c] = live[c] = k < y.nseg && i[c] < a.nsym;
-            s1[c] = y.start + (kk + 1) * kSegBits;
-            pos[c] = kk ? exits[kk - 1] : y.start;
-            acc[c] = 0;
-            g[c] = ~0ull;
-            have[c] = 0;
-            br_init(r[c], a, pos[c] + a.bit_adj);
-        }
-        auto flush = [&](int c) {
-            for (uint32_t t = 0; t < 4; ++t)
-                if (have[c] & (1u << t)) subs[4 * g[c] + t] = (uint16_t)(acc[c] >> (16 * t));
-            have[c] = 0;
-        };
-        while (act[0] || act[1]) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (act[c]) {
-                    if (i[c] % kBlockSyms == 0) starts[i[c] / kBlockSyms] = pos[c];
-                    if (i[c] % kChainSyms == 0) {
-                        const uint64_t ch = i[c] / kChainSyms;
-                        if ((ch >> 2) != g[c]) {
-                            flush(c);
-                            g[c] = ch >> 2;
-                            acc[c] = 0;
-                        }
-                        acc[c] |= (uint64_t)(uint16_t)pos[c] << (16 * (ch & 3));
-                        have[c] |= 1u << (ch & 3);
-                        if (have[c] == 15u) {
-                            reinterpret_cast<uint64_t*>(subs)[g[c]] = acc[c];
-                            have[c] = 0;
-                        }
-                    }
-                }
-                br_refill(r[c], a);
-            }
-            uint32_t L[2];
-            lut_len2(a, lds, r, L);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (!act[c]) continue;
-                if (L[c] == 0) { atomicOr(a.err, 2u); act[c] = false; continue; }
-                r[c].buf <<= L[c];
-                r[c].nb -= L[c];
-                pos[c] += L[c];
-                ++i[c];
-                act[c] = pos[c] < s1[c] && i[c] < a.nsym;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (!live[c]) continue;
-            flush(c);
-            if (i[c] == a.nsym) starts[a.nblocks] = pos[c];
-        }
-    }
-}
-
+// Fix-up of segment k from its true entry exit[k-1]: walk until the path
+// lands on a boundary of the segment's bitmap (the paths agree from there)
+// or leaves the segment. The bitmap words the walk passes are rewritten with
+// the walked boundaries (the landing word keeps its bits from the landing
+// point on), so the row keeps holding one consistent path; its count and,
+// when the walk left the segment, its exit follow.
 template <int MODE>
 __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -2077,94 +2004,94 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs 
     uint32_t* dw = y.dirty[(it + 1) & 1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
-        if (k == 0) { if (it == 0) { exw[0] = y.exit0[0]; y.cnt[0] = y.cnt0[0]; } else exw[0] = exr[0]; continue; }
-        if (it > 0 && !dr[k]) { exw[k] = exr[k]; continue; }
+        if (k == 0 || (it > 0 && !dr[k])) { exw[k] = exr[k]; continue; }
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
-        const uint32_t* bm = y.bmp + k * kBmpWords;
-        uint64_t p = it == 0 ? y.exit0[k - 1] : exr[k - 1];
-        uint64_t walked = 0, ex = 0, n = 0;
+        uint32_t* bm = y.bmp + k * kBmpWords;
+        uint64_t p = exr[k - 1];
+        uint32_t walked = 0, below = 0, acc = 0, cw = 0;
+        uint32_t old = bm[0];  // the row's word cw before the rewrite
         bool landed = false;
         BitReader r;
         br_init(r, a, p + a.bit_adj);
         while (p < s1) {
             const uint32_t d = (uint32_t)(p - s0);
-            if (d < kBmpBits && ((bm[d >> 5] >> (d & 31)) & 1u)) { landed = true; break; }
+            while ((d >> 5) != cw) {  // words the walk has passed: the walked boundaries replace them
+                below += __popc(old);
+                bm[cw] = acc;
+                acc = 0;
+                old = bm[++cw];
+            }
+            if ((old >> (d & 31)) & 1u) { landed = true; break; }
+            acc |= 1u << (d & 31);
             uint32_t sym;
             const uint32_t L = br_next<MODE>(r, a, lds, sym);
             if (L == 0) { atomicOr(a.err, 2u); break; }
             p += L;
             ++walked;
         }
+        uint64_t n, ex;
         if (landed) {
-            const uint32_t d = (uint32_t)(p - s0);
-            uint32_t below = 0;
-            for (uint32_t i = 0; i < (d >> 5); ++i) below += __popc(bm[i]);
-            if (d & 31) below += __popc(bm[d >> 5] & ((1u << (d & 31)) - 1u));
-            n = y.cnt0[k] - below + walked;
-            ex = y.exit0[k];
+            const uint32_t lowm = (1u << ((uint32_t)(p - s0) & 31)) - 1u;
+            below += __popc(old & lowm);
+            bm[cw] = acc | (old & ~lowm);
+            n = y.cnt[k] - below + walked;
+            ex = exr[k];
         } else {
+            for (; cw < kBmpWords; ++cw) { bm[cw] = acc; acc = 0; }
             n = walked;
             ex = p;
         }
         y.cnt[k] = n;
-        const uint64_t prev = it == 0 ? y.exit0[k] : exr[k];
         exw[k] = ex;
-        if (ex != prev) {
+        if (ex != exr[k]) {
             if (k + 1 < y.nseg) dw[k + 1] = 1;
             atomicAdd(y.changed, 1u);
         }
     }
 }
 
-// Decode each segment from its true entry; symbol i (global) lands at pos.
-template <int MODE>
-__global__ __launch_bounds__(kSyncThreads) void k_sync_emit(DecArgs a, SyncArgs y, const unsigned long long* exits,
-                                                  const unsigned long long* first, unsigned long long* starts,
-                                                  uint16_t* subs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, a.lds_img, a.lds_words);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
-        uint64_t i = first[k];
-        if (i >= a.nsym) continue;
-        const uint64_t s1 = y.start + (k + 1) * kSegBits;
-        uint64_t pos = k ? exits[k - 1] : y.start;
-        BitReader r;
-        br_init(r, a, pos + a.bit_adj);
-        // chain positions leave four at a time (8-byte stores) when this lane
-        // wrote the whole group of four; a group split with a neighbouring
-        // segment is flushed slot by slot
-        uint64_t acc = 0, g = ~0ull;
-        uint32_t have = 0;
-        auto flush = [&]() {
-            for (uint32_t t = 0; t < 4; ++t)
-                if (have & (1u << t)) subs[4 * g + t] = (uint16_t)(acc >> (16 * t));
-            have = 0;
-        };
-        while (pos < s1 && i < a.nsym) {
-            if (i % kBlockSyms == 0) starts[i / kBlockSyms] = pos;
-            if (i % kChainSyms == 0) {
-                const uint64_t c = i / kChainSyms;
-                if ((c >> 2) != g) {
-                    flush();
-                    g = c >> 2;
-                    acc = 0;
-                }
-                acc |= (uint64_t)(uint16_t)pos << (16 * (c & 3));
-                have |= 1u << (c & 3);
-                if (have == 15u) {
-                    reinterpret_cast<uint64_t*>(subs)[g] = acc;
-                    have = 0;
-                }
+// Position (0..31) of the r-th (0-based) set bit of m; r < popc(m).
+HZ_DEV uint32_t select_bit(uint32_t m, uint32_t r) {
+    uint32_t pos = 0, c;
+    c = __popc(m & 0xffffu); if (r >= c) { r -= c; pos += 16; m >>= 16; }
+    c = __popc(m & 0xffu);   if (r >= c) { r -= c; pos += 8;  m >>= 8; }
+    c = __popc(m & 0xfu);    if (r >= c) { r -= c; pos += 4;  m >>= 4; }
+    c = __popc(m & 0x3u);    if (r >= c) { r -= c; pos += 2;  m >>= 2; }
+    return pos + ((r >= (m & 1u)) ? 1u : 0u);
+}
+
+// One wave per bitmap row: lane l holds the row's bits [64 l, 64 l + 64);
+// a wave scan of popcounts numbers every boundary. Boundary i < nsym with
+// i % 8 == 0 is a chain start (raw position, low 16 bits; k_sync_subs makes it
+// block-relative), i % 2048 == 0 also a block start; boundary nsym is the end
+// of the stream (or, when the rows hold exactly nsym, the last exit).
+constexpr int kSelectThreads = 256;
+__global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint64_t nsym, uint64_t nblocks,
+                                                                const unsigned long long* exits,
+                                                                const unsigned long long* first,
+                                                                unsigned long long* starts, uint16_t* subs) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwave = (uint64_t)gridDim.x * (kSelectThreads / 64);
+    for (uint64_t k = (uint64_t)blockIdx.x * (kSelectThreads / 64) + (threadIdx.x >> 6); k < y.nseg; k += nwave) {
+        const uint64_t f = first[k];
+        if (f > nsym) continue;  // wave-uniform
+        if (k + 1 == y.nseg && lane == 0 && f + y.cnt[k] == nsym) starts[nblocks] = exits[k];
+        const uint2 w = reinterpret_cast<const uint2*>(y.bmp + k * kBmpWords)[lane];
+        const uint32_t c0 = __popc(w.x), c1 = __popc(w.y);
+        uint64_t i = f + wave_incl_sum(c0 + c1) - (c0 + c1);  // number of the lane's first boundary
+        uint64_t base = y.start + k * kSegBits + 64u * (uint32_t)lane;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t m = h ? w.y : w.x, c = h ? c1 : c0;
+            if (i <= nsym && nsym < i + c) starts[nblocks] = base + select_bit(m, (uint32_t)(nsym - i));
+            for (uint32_t r = (uint32_t)(-i) & 7u; r < c && i + r < nsym; r += 8) {
+                const uint64_t idx = i + r, pos = base + select_bit(m, r);
+                subs[idx / kChainSyms] = (uint16_t)pos;
+                if (idx % kBlockSyms == 0) starts[idx / kBlockSyms] = pos;
             }
-            uint32_t sym;
-            const uint32_t L = br_next<MODE>(r, a, lds, sym);
-            if (L == 0) { atomicOr(a.err, 2u); break; }
-            pos += L;
-            ++i;
+            i += c;
+            base += 32;
         }
-        flush();
-        if (i == a.nsym) starts[a.nblocks] = pos;
     }
 }
 
@@ -2197,14 +2124,14 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // exit0, cnt0, ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
-    return nseg * (6 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
+    // ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
+    return nseg * (4 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
 }
 
 template <int MODE>
 static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* first, unsigned long long* tiles,
                             unsigned long long* d_index, uint32_t* h_changed, uint32_t lds, int ncu, hipStream_t s) {
-    for (const void* f : {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>, (const void*)k_sync_emit<MODE>}) {
+    for (const void* f : {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>}) {
         hipError_t e = ensure_lds_limit(f, kLdsBytes);
         if (e != hipSuccess) return e;
     }
@@ -2215,15 +2142,12 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     // two segments per lane where the pipelined decoder's table shape holds
     const bool two = MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + kDecLevelBits;
     if (two) {
-        for (const void* f : {(const void*)k_sync_scan2, (const void*)k_sync_emit2}) {
-            hipError_t e = ensure_lds_limit(f, kLdsBytes);
-            if (e != hipSuccess) return e;
-        }
-    }
-    if (two)
+        hipError_t e = ensure_lds_limit((const void*)k_sync_scan2, kLdsBytes);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_sync_scan2, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
-    else
+    } else {
         hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
+    }
     // resolve entries until no exit changes (host loop; typically 1-3 passes)
     int it = 0;
     for (;; ++it) {
@@ -2243,17 +2167,16 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
                        (const unsigned long long*)tiles, first);
     uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
-    // end bit = all ones unless the payload holds nsym codewords (k_sync_emit writes it then)
+    // end bit = all ones unless the payload holds nsym codewords (k_sync_select writes it then)
     hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
     if (e != hipSuccess) return e;
-    if (two)
-        hipLaunchKernelGGL(k_sync_emit2, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits,
+    if ((e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s)) != hipSuccess) return e;
+    {
+        uint64_t sg = (y.nseg + kSelectThreads / 64 - 1) / (kSelectThreads / 64);
+        sg = sg < (uint64_t)ncu * 8 ? sg : (uint64_t)ncu * 8;
+        hipLaunchKernelGGL(k_sync_select, dim3(sg), dim3(kSelectThreads), 0, s, y, a.nsym, a.nblocks, exits,
                            (const unsigned long long*)first, d_index, subs);
-    else
-        hipLaunchKernelGGL(k_sync_emit<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, exits,
-                           (const unsigned long long*)first, d_index, subs);
-    e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s);
-    if (e != hipSuccess) return e;
+    }
     uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
     sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
     hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index, subs);
@@ -2299,8 +2222,6 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.nseg = (bits + kSegBits - 1) / kSegBits;
     if (y.nseg == 0) return hipErrorInvalidValue;
     unsigned long long* p = d_scratch;
-    y.exit0 = p; p += y.nseg;
-    y.cnt0 = p; p += y.nseg;
     y.ex[0] = p; p += y.nseg;
     y.ex[1] = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
