@@ -461,21 +461,14 @@ static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t 
     return HZ_OK;
 }
 
-// Hot second level in the LDS image. The LDS left after level 1 and the
-// decoder's staging slots (16 waves, slots sized from the Kraft-weighted mean
-// code length) holds c-bit heads of the most used global subtables: entry j
+// Hot second level in the LDS image. `budget` LDS words (what the kernel's
+// staging leaves beside level 1) hold c-bit heads of the most used global subtables: entry j
 // of a head is the leaf its range resolves to, or a link to the rest of the
 // global subtable. Choice: greedy by decoded-mass per LDS word; the Kraft
 // weight 2^-L of a code stands in for its frequency, so each global entry of
 // an nb-bit subtable under level 1 carries mass 2^-(K1+nb).
-static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, const std::vector<uint32_t>& l2, int K1) {
-    double kbits = 0.0;
-    for (uint32_t s = 0; s < HZ_NSYM; ++s)
-        if (cb->len[s]) kbits += ldexp((double)cb->len[s], -(int)cb->len[s]);
-    const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
-    const long room = (long)(kLdsBytes / 4) - (long)img.size() -
-                      (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64;
-    long budget = room;
+static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, const std::vector<uint32_t>& l2, int K1,
+                          long budget) {
     if (budget < 64) return;
     struct Head { uint32_t q, nb, off, c; };
     std::vector<Head> heads;
@@ -535,8 +528,12 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
     while (img.size() & 3) img.push_back(leaf(1, 0));
 }
 
-// LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global memory.
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
+// LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global
+// memory. `walk` receives the index walker's image (hz_kernels.hip
+// k_idx_walk): the same level 1 with hot heads sized to the LDS its rings
+// leave, over the same global levels.
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1,
+                  std::vector<uint32_t>* walk) {
     K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
     img.assign(1u << K1, 0u);
@@ -553,7 +550,18 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     for (auto& e : img) if (!e) e = leaf(1, 0);
     for (auto& e : l2) if (!e) e = leaf(1, 0);
     if (l2.empty()) l2.push_back(leaf(1, 0));
-    add_lds_level(cb, img, l2, K1);
+    if (walk) {
+        *walk = img;
+        add_lds_level(cb, *walk, l2, K1, (long)(kLdsBytes / 4) - (long)walk->size() - (long)(kWalkLdsRingBytes / 4) - 64);
+    }
+    // heads fill what the decoder's staging slots (16 waves, sized from the
+    // Kraft-weighted mean code length) leave
+    double kbits = 0.0;
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) kbits += ldexp((double)cb->len[s], -(int)cb->len[s]);
+    const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
+    add_lds_level(cb, img, l2, K1,
+                  (long)(kLdsBytes / 4) - (long)img.size() - (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64);
     return HZ_OK;
 }
 

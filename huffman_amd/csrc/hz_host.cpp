@@ -31,7 +31,8 @@ std::vector<uint32_t> build_len8(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1,
+                  std::vector<uint32_t>* walk);
 }  // namespace hz
 
 using namespace hz;
@@ -74,7 +75,8 @@ struct hz_ctx {
     hipEvent_t ev[4][2] = {};
     bool ev_used[4] = {false, false, false, false};
     Staging stage_enc, stage_dec;
-    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0;
+    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0,
+           cap_walk_lds = 0;
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -103,6 +105,7 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_len8);
     (void)hipFree(t.d_dec_lds);
     (void)hipFree(t.d_dec_l2);
+    (void)hipFree(t.d_walk_lds);
     t = Tables();
 }
 
@@ -329,10 +332,13 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.dec_max_len = (int)cb->max_len;
     t.dec_min_len = (int)cb->min_len;
     const int mode = select_dec_mode(cb);
-    std::vector<uint32_t> dimg, l2;
+    std::vector<uint32_t> dimg, l2, wimg;
+    // the index walker takes the pipelined decoder's codebooks: codes <= 32 bits, one global level
+    const bool walk = mode == DEC_LUT && cb->max_len <= 32 &&
+                      (int)cb->max_len <= std::min((int)cb->max_len, kDecLutMaxK1) + kDecLevelBits;
     if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
     else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
-    else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, walk ? &wimg : nullptr);
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
@@ -342,6 +348,14 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
+    t.walk_lds_bytes = 0;
+    if (!wimg.empty()) {
+        while (wimg.size() % 4) wimg.push_back(0);
+        if (wimg.size() * 4 + kWalkLdsRingBytes <= kLdsBytes) {
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
+            t.walk_lds_bytes = (uint32_t)(wimg.size() * 4);
+        }
+    }
     HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
     t.dec_mode = mode;
     return HZ_OK;

@@ -60,6 +60,14 @@ constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-b
 constexpr int kDecLevelBits = HZ_DEC_LEVEL_BITS;  // bits per global subtable level
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
+// Index walker (k_idx_walk): per chain an LDS ring of 4 payload chunks (16 B)
+// plus a copy of chunk 0 and 4 mark chunks; kWalkChains chains per lane,
+// kWalkWaves waves per CU. Its LUT image's hot heads get the rest of the LDS.
+constexpr int kWalkChains = 2;
+constexpr int kWalkWaves = 4;  // 2..8 measured: 4 fastest (more waves: more L2 misses on the per-chain streams)
+constexpr uint32_t kRingWords = 36;
+constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
+constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
 
 // Per-wave LDS slot for one block's payload (u32 words), from the largest
@@ -95,6 +103,8 @@ struct Tables {
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
     uint64_t dec_l2_entries = 0;
+    uint32_t* d_walk_lds = nullptr; // LDS image of the index walker (level 1 + smaller hot heads)
+    uint32_t walk_lds_bytes = 0;    // 0 = no walker image (the segment walkers build the index)
 };
 
 // Count-pass length table layout: the high byte is XORed into the bank bits

@@ -1834,10 +1834,10 @@ struct SyncArgs {
     uint64_t start;                 // stream bit of the first symbol (payload view: + bit_adj)
     uint64_t nseg;
     uint32_t* bmp;                  // boundary bitmap, kBmpWords per segment
-    unsigned long long* ex[2];      // exits (scan: ex[0]), ping-pong between iterations
+    unsigned long long* ent;        // entry of a dirty segment: the previous segment's exit
     unsigned long long* cnt;        // boundaries in the segment's bitmap row
-    uint32_t* dirty[2];             // entry changed in the previous iteration
-    uint32_t* changed;              // exits changed in this iteration
+    uint32_t* dirty[2];             // segments to check against their entry, ping-pong between iterations
+    uint32_t* changed;              // segments whose walk left them in this iteration
 };
 
 template <int MODE>
@@ -1876,7 +1876,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan(DecArgs a, SyncArgs 
             ++n;
         }
         while (cw < kBmpWords) put();
-        y.ex[0][k] = pos;
+        if (k + 1 < y.nseg) { y.ent[k + 1] = pos; y.dirty[0][k + 1] = 1u; }
         y.cnt[k] = n;
     }
 }
@@ -1982,32 +1982,263 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
             const uint64_t k = k0 + c * stride;
             if (k >= y.nseg) continue;
             while (cw[c] < kBmpWords) put(c);
-            y.ex[0][k] = s0[c] + d[c];
+            if (k + 1 < y.nseg) { y.ent[k + 1] = s0[c] + d[c]; y.dirty[0][k + 1] = 1u; }
             y.cnt[k] = n[c];
         }
     }
 }
 
-// Fix-up of segment k from its true entry exit[k-1]: walk until the path
-// lands on a boundary of the segment's bitmap (the paths agree from there)
-// or leaves the segment. The bitmap words the walk passes are rewritten with
-// the walked boundaries (the landing word keeps its bits from the landing
-// point on), so the row keeps holding one consistent path; its count and,
-// when the walk left the segment, its exit follow.
+// ---------------------------------------------------------------------------
+// Index walker for the pipelined decoder's codebooks (codes <= 32 bits, one
+// global LUT level): LONG chains -- each lane walks two stretches of spc whole
+// segments, each starting kWalkLead bits early so the walk has resynchronised
+// (P(not) ~ 4e-4 on Zipf) when it reaches its first segment: one start per
+// ~10^5 codewords instead of one per segment. Each chain streams its payload
+// through a 4-chunk LDS ring (16-byte chunks, one refill load per round,
+// issued a round ahead) and marks boundaries into a 4-chunk LDS mark ring
+// (ds_or), flushed one chunk per round as a 16-byte store into the bitmap;
+// per-segment counts come from popcounts of the flushed chunks.
+// Lookups use the decoder's level 1 with hot heads sized to the LDS the rings
+// leave; a chain whose code needs the global level PARKS for the rest of the
+// round, and the round ends with one gather for all parked chains: every wait
+// is the round's single vmcnt(0) (refill + gathers), never a gather queued
+// behind a refill in mid-walk.
+// A chain's exit becomes the entry of the next chain's first segment
+// (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
+// when the lead-in resynchronised.
+// ---------------------------------------------------------------------------
+constexpr int kWalkSteps = 8;  // steps per round: ~92 bits consumed on Zipf, 128 refilled (6 and 12 measured slower)
+constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
+
+struct WalkArgs {
+    const uint32_t* words;    // payload view, 64-byte aligned
+    uint64_t nwords;          // >= 4 (host check)
+    uint32_t bit_adj;         // payload bit 0 = bit bit_adj of words
+    uint64_t start;           // stream bit of the first symbol
+    uint64_t nseg, spc, nchains;
+    const uint32_t* lds_img;  // walker LUT image (level 1 + hot heads)
+    uint32_t lds_words;
+    int k;
+    const uint32_t* l2;       // global level (every entry a leaf)
+    uint32_t* bmp;
+    unsigned long long* cnt;
+    unsigned long long* ent;
+    uint32_t* dirty;
+};
+
+// 16 payload bytes at word w (4-aligned): zeros before word 0 / past the end.
+HZ_DEV uint4 walk_load(const WalkArgs& a, uint64_t w) {
+    const bool in = w < a.nwords;  // false for a window that wrapped below word 0
+    const uint64_t wl = !in ? 0 : (w + 4 <= a.nwords ? w : a.nwords - 4);
+    return *reinterpret_cast<const uint4*>(a.words + wl);
+}
+HZ_DEV uint4 walk_fix(const WalkArgs& a, uint64_t w, uint4 x) {
+    if (w < a.nwords && w + 4 <= a.nwords) return x;
+    const uint64_t base = a.nwords - 4;
+    uint32_t q[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint64_t wt = w + t;
+        q[t] = wt < a.nwords && w < a.nwords ? pick4(x, (uint32_t)(wt - base)) : 0u;
+    }
+    return make_uint4(q[0], q[1], q[2], q[3]);
+}
+
+// Chunk slot q (0..3) of a transposed payload ring, byte-swapped; slot 0 also
+// fills the copy rows 16..19 that a window at the ring's last word reads.
+template <uint32_t ROW>
+HZ_DEV void ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
+    const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ring[(4 * q + i) * ROW] = v[i];
+    if (q == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ring[(16 + i) * ROW] = v[i];
+    }
+}
+
+__global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    constexpr int C = kWalkChains;
+    constexpr uint32_t kRow = 1;  // ring word stride
+    const uint32_t k = (uint32_t)a.k;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t* ring[C];
+    uint32_t off[C], off0[C], ms[C], end[C], f[C], mcount[C], nmc[C], rc[C], pgi[C];
+    uint64_t bch[C], x0[C], seg0[C], seg1[C];
+    bool live[C], pk[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        ring[c] = lds + a.lds_words + ((wid * C + c) * 64 + lane) * kRingWords;
+        const uint64_t ch = tid + c * T;
+        live[c] = ch < a.nchains;
+        const uint64_t chc = live[c] ? ch : 0;
+        seg0[c] = chc * a.spc;
+        seg1[c] = seg0[c] + a.spc < a.nseg ? seg0[c] + a.spc : a.nseg;
+        const uint64_t cs = seg0[c] * kSegBits, ce = seg1[c] * kSegBits;
+        x0[c] = cs - (cs < kWalkLead ? cs : kWalkLead);
+        const uint64_t P0 = a.start + a.bit_adj + x0[c];
+        bch[c] = (P0 >> 7) - 1;  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
+        off0[c] = off[c] = (uint32_t)(P0 - 128 * bch[c]);
+        ms[c] = off[c] + (uint32_t)(cs - x0[c]);
+        end[c] = live[c] ? off[c] + (uint32_t)(ce - x0[c]) : off[c];
+        nmc[c] = live[c] ? (uint32_t)((ce - cs) / 128) : 0u;
+        mcount[c] = rc[c] = pgi[c] = 0;
+        pk[c] = false;
+#pragma unroll
+        for (int i = 20; i < 36; ++i) ring[c][i * kRow] = 0u;
+    }
+    // prologue: chunks 0..2 of every chain
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        uint4 v[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch[c] + g));
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            ring_put<kRow>(ring[c], (uint32_t)g, walk_fix(a, 4 * (bch[c] + g), v[g]));
+        }
+        f[c] = 3;
+    }
+    uint32_t pW[C], pe[C], pD[C];  // a parked chain's window, entry and consumed bits
+    // refill of chunk f when it fits the ring (the chain no longer needs chunk f - 4);
+    // issued at the end of the round before (here: the prologue) and written at the
+    // end of this one, ahead of the round's bitmap stores in the vmcnt queue
+    bool rf[C];
+    uint4 v[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        rf[c] = f[c] <= ((off[c] - 1) >> 7) + 3;
+        if (rf[c]) v[c] = walk_load(a, 4 * (bch[c] + f[c]));
+    }
+    for (;;) {
+        bool alive = false;
+#pragma unroll
+        for (int c = 0; c < C; ++c) alive |= off[c] < end[c] || mcount[c] < nmc[c];
+        if (!__any(alive)) break;
+        uint32_t lim[C];  // the round's steps stay below: chain end, filled data, free mark slots
+#pragma unroll
+        for (int c = 0; c < C; ++c) lim[c] = min(end[c], min(128 * f[c] - 31, ms[c] + 128 * (mcount[c] + 4)));
+        // branch-free steps: every chain's window, level-1 and hot-head reads are
+        // in flight together; a chain that cannot step only leaves off unchanged
+#pragma unroll
+        for (int t = 0; t < kWalkSteps; ++t) {
+            uint32_t W[C], e[C], x[C], D[C], wa[C], wb[C];
+            bool ok[C], h[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                ok[c] = !pk[c] & (off[c] < lim[c]);
+                const uint32_t* r = ring[c] + (((off[c] - 1) >> 5) & 15) * kRow;
+                wa[c] = r[0];
+                wb[c] = r[kRow];
+            }
+            HZ_WALK_FENCE();
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                W[c] = __builtin_amdgcn_alignbit(wa[c], wb[c], (0u - off[c]) & 31);
+                e[c] = lds[W[c] >> (32 - k)];
+            }
+            HZ_WALK_FENCE();
+#pragma unroll
+            for (int c = 0; c < C; ++c) {  // LDS second level (hot heads); other lanes read word 0
+                h[c] = (e[c] >> 30) == 1u;
+                const uint32_t nb = (e[c] >> 26) & 15u;
+                D[c] = h[c] ? k + nb : k;
+                x[c] = lds[h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u];
+            }
+            HZ_WALK_FENCE();
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t ee = h[c] ? x[c] : e[c];
+                const bool leaf = (int32_t)ee < 0;
+                const bool adv = ok[c] & leaf, park = ok[c] & !leaf;
+                const uint32_t rel = off[c] - ms[c];
+                const uint32_t bit = (adv & (off[c] >= ms[c])) ? (1u << (rel & 31)) : 0u;
+                atomicOr(ring[c] + (20 + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
+                off[c] += adv ? (ee >> 16) & 63u : 0u;
+                pk[c] |= park;
+                pW[c] = park ? W[c] : pW[c];
+                pe[c] = park ? ee : pe[c];
+                pD[c] = park ? D[c] : pD[c];
+            }
+        }
+        uint32_t g[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (pk[c]) g[c] = a.l2[(pe[c] & 0x3ffffffu) + ((pW[c] << pD[c]) >> (32 - ((pe[c] >> 26) & 15u)))];
+        bool fl[C];
+        uint4 m[C];
+        uint64_t j[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (pk[c]) {
+                if (off[c] >= ms[c]) {
+                    const uint32_t rel = off[c] - ms[c];
+                    atomicOr(ring[c] + (20 + ((rel >> 5) & 15)) * kRow, 1u << (rel & 31));
+                }
+                off[c] += (g[c] >> 16) & 63u;
+                pk[c] = false;
+            }
+            if (rf[c]) {
+                ring_put<kRow>(ring[c], f[c] & 3, walk_fix(a, 4 * (bch[c] + f[c]), v[c]));
+                ++f[c];
+            }
+            // mark chunk mcount leaves once the walk is past it
+            fl[c] = mcount[c] < nmc[c] && off[c] >= ms[c] && off[c] - ms[c] >= 128 * (mcount[c] + 1);
+            if (fl[c]) {
+                uint32_t* slot = ring[c] + (20 + 4 * (mcount[c] & 3)) * kRow;
+                m[c] = make_uint4(slot[0], slot[kRow], slot[2 * kRow], slot[3 * kRow]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) slot[i * kRow] = 0u;
+                j[c] = seg0[c] * (kSegBits / 128) + mcount[c];
+                rc[c] = ((mcount[c] & 31) ? rc[c] : 0u) + __popc(m[c].x) + __popc(m[c].y) + __popc(m[c].z) +
+                        __popc(m[c].w);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {  // the next round's refill, then this round's bitmap stores
+            rf[c] = f[c] <= ((off[c] - 1) >> 7) + 3;
+            if (rf[c]) v[c] = walk_load(a, 4 * (bch[c] + f[c]));
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (!fl[c]) continue;
+            reinterpret_cast<uint4*>(a.bmp)[j[c]] = m[c];
+            if ((mcount[c] & 31) == 31) a.cnt[j[c] >> 5] = rc[c];
+            ++mcount[c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        if (!live[c] || seg1[c] >= a.nseg) continue;
+        a.ent[seg1[c]] = a.start + x0[c] + (off[c] - off0[c]);
+        a.dirty[seg1[c]] = 1u;
+    }
+}
+
+// Fix-up of a dirty segment k from its true entry ent[k] (the previous
+// segment's exit): walk until the path lands on a boundary of the segment's
+// bitmap (the paths agree from there) or leaves the segment. The bitmap words
+// the walk passes are rewritten with the walked boundaries (the landing word
+// keeps its bits from the landing point on), so the row keeps holding one
+// consistent path, and its count follows. A walk that leaves the segment
+// hands its end to segment k + 1 for the next iteration.
 template <int MODE>
 __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs y, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
-    const unsigned long long* exr = y.ex[it & 1];
-    unsigned long long* exw = y.ex[(it + 1) & 1];
     const uint32_t* dr = y.dirty[it & 1];
     uint32_t* dw = y.dirty[(it + 1) & 1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < y.nseg; k += stride) {
-        if (k == 0 || (it > 0 && !dr[k])) { exw[k] = exr[k]; continue; }
+        if (!dr[k]) continue;
         const uint64_t s0 = y.start + k * kSegBits, s1 = s0 + kSegBits;
         uint32_t* bm = y.bmp + k * kBmpWords;
-        uint64_t p = exr[k - 1];
+        uint64_t p = y.ent[k];
         uint32_t walked = 0, below = 0, acc = 0, cw = 0;
         uint32_t old = bm[0];  // the row's word cw before the rewrite
         bool landed = false;
@@ -2029,22 +2260,15 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_iter(DecArgs a, SyncArgs 
             p += L;
             ++walked;
         }
-        uint64_t n, ex;
         if (landed) {
             const uint32_t lowm = (1u << ((uint32_t)(p - s0) & 31)) - 1u;
             below += __popc(old & lowm);
             bm[cw] = acc | (old & ~lowm);
-            n = y.cnt[k] - below + walked;
-            ex = exr[k];
+            y.cnt[k] = y.cnt[k] - below + walked;
         } else {
             for (; cw < kBmpWords; ++cw) { bm[cw] = acc; acc = 0; }
-            n = walked;
-            ex = p;
-        }
-        y.cnt[k] = n;
-        exw[k] = ex;
-        if (ex != exr[k]) {
-            if (k + 1 < y.nseg) dw[k + 1] = 1;
+            y.cnt[k] = walked;
+            if (k + 1 < y.nseg) { y.ent[k + 1] = p; dw[k + 1] = 1u; }
             atomicAdd(y.changed, 1u);
         }
     }
@@ -2064,10 +2288,9 @@ HZ_DEV uint32_t select_bit(uint32_t m, uint32_t r) {
 // a wave scan of popcounts numbers every boundary. Boundary i < nsym with
 // i % 8 == 0 is a chain start (raw position, low 16 bits; k_sync_subs makes it
 // block-relative), i % 2048 == 0 also a block start; boundary nsym is the end
-// of the stream (or, when the rows hold exactly nsym, the last exit).
+// of the stream.
 constexpr int kSelectThreads = 256;
 __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint64_t nsym, uint64_t nblocks,
-                                                                const unsigned long long* exits,
                                                                 const unsigned long long* first,
                                                                 unsigned long long* starts, uint16_t* subs) {
     const int lane = threadIdx.x & 63;
@@ -2075,7 +2298,8 @@ __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint
     for (uint64_t k = (uint64_t)blockIdx.x * (kSelectThreads / 64) + (threadIdx.x >> 6); k < y.nseg; k += nwave) {
         const uint64_t f = first[k];
         if (f > nsym) continue;  // wave-uniform
-        if (k + 1 == y.nseg && lane == 0 && f + y.cnt[k] == nsym) starts[nblocks] = exits[k];
+        // the rows hold exactly nsym boundaries: the last codeword ends at the bitmap's end
+        if (k + 1 == y.nseg && lane == 0 && f + y.cnt[k] == nsym) starts[nblocks] = y.start + y.nseg * kSegBits;
         const uint2 w = reinterpret_cast<const uint2*>(y.bmp + k * kBmpWords)[lane];
         const uint32_t c0 = __popc(w.x), c1 = __popc(w.y);
         uint64_t i = f + wave_incl_sum(c0 + c1) - (c0 + c1);  // number of the lane's first boundary
@@ -2124,15 +2348,61 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // ex[2], cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
-    return nseg * (4 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
+    // ent, cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
+    return nseg * (3 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
 }
 
+// Common tail of the index build, after the boundary bitmap and the dirty
+// entries exist: fix-ups to a fixed point, count scan, select, subs.
 template <int MODE>
-static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* first, unsigned long long* tiles,
-                            unsigned long long* d_index, uint32_t* h_changed, uint32_t lds, int ncu, hipStream_t s) {
-    for (const void* f : {(const void*)k_sync_scan<MODE>, (const void*)k_sync_iter<MODE>}) {
-        hipError_t e = ensure_lds_limit(f, kLdsBytes);
+static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long* first, unsigned long long* tiles,
+                               unsigned long long* d_index, uint32_t* h_changed, uint32_t lds, int ncu,
+                               hipStream_t s) {
+    {
+        hipError_t e = ensure_lds_limit((const void*)k_sync_iter<MODE>, kLdsBytes);
+        if (e != hipSuccess) return e;
+    }
+    uint64_t wgs = (y.nseg + kSyncThreads - 1) / kSyncThreads;
+    const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 2 ? 1 : 2) : 2);
+    wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
+    // resolve entries until no walk leaves its segment (host loop; typically 1-2 passes)
+    for (int it = 0;; ++it) {
+        hipError_t e = hipMemsetAsync(y.changed, 0, 4, s);
+        if (e != hipSuccess) return e;
+        if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nseg, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sync_iter<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, it);
+        if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (*h_changed == 0 || it > (int)y.nseg) break;
+    }
+    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
+    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       (const unsigned long long*)tiles, first);
+    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
+    // end bit = all ones unless the payload holds nsym codewords (k_sync_select writes it then)
+    hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s)) != hipSuccess) return e;
+    {
+        uint64_t sg = (y.nseg + kSelectThreads / 64 - 1) / (kSelectThreads / 64);
+        sg = sg < (uint64_t)ncu * 8 ? sg : (uint64_t)ncu * 8;
+        hipLaunchKernelGGL(k_sync_select, dim3(sg), dim3(kSelectThreads), 0, s, y, a.nsym, a.nblocks,
+                           (const unsigned long long*)first, d_index, subs);
+    }
+    uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
+    sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
+    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index, subs);
+    return hipGetLastError();
+}
+
+// Boundary bitmap by the LUT walkers (one or two 4096-bit segments per lane).
+template <int MODE>
+static hipError_t scan_lut(const DecArgs& a, SyncArgs y, uint32_t lds, int ncu, hipStream_t s) {
+    {
+        hipError_t e = ensure_lds_limit((const void*)k_sync_scan<MODE>, kLdsBytes);
         if (e != hipSuccess) return e;
     }
     // 16-wave workgroups: one table copy per workgroup, as many waves as a CU holds
@@ -2148,38 +2418,28 @@ static hipError_t run_index(const DecArgs& a, SyncArgs y, unsigned long long* fi
     } else {
         hipLaunchKernelGGL(k_sync_scan<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y);
     }
-    // resolve entries until no exit changes (host loop; typically 1-3 passes)
-    int it = 0;
-    for (;; ++it) {
-        hipError_t e = hipMemsetAsync(y.changed, 0, 4, s);
-        if (e != hipSuccess) return e;
-        if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nseg, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sync_iter<MODE>, dim3(wgs), dim3(kSyncThreads), lds, s, a, y, it);
-        if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (*h_changed == 0 || it > (int)y.nseg) break;
-    }
-    const unsigned long long* exits = y.ex[(it + 1) & 1];
-    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       tiles);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
-    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       (const unsigned long long*)tiles, first);
-    uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
-    // end bit = all ones unless the payload holds nsym codewords (k_sync_select writes it then)
-    hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
+    return hipGetLastError();
+}
+
+// Boundary bitmap by the long-chain walker.
+static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int ncu, hipStream_t s) {
+    hipError_t e = ensure_lds_limit((const void*)k_idx_walk, kLdsBytes);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s)) != hipSuccess) return e;
-    {
-        uint64_t sg = (y.nseg + kSelectThreads / 64 - 1) / (kSelectThreads / 64);
-        sg = sg < (uint64_t)ncu * 8 ? sg : (uint64_t)ncu * 8;
-        hipLaunchKernelGGL(k_sync_select, dim3(sg), dim3(kSelectThreads), 0, s, y, a.nsym, a.nblocks, exits,
-                           (const unsigned long long*)first, d_index, subs);
-    }
-    uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
-    sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
-    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index, subs);
+    WalkArgs w;
+    w.words = a.words; w.nwords = a.nwords; w.bit_adj = a.bit_adj;
+    w.start = y.start; w.nseg = y.nseg;
+    const uint64_t per_wg = (uint64_t)kWalkWaves * 64 * kWalkChains;
+    const uint64_t target = per_wg * (uint64_t)ncu;
+    w.spc = (y.nseg + target - 1) / target;
+    w.nchains = (y.nseg + w.spc - 1) / w.spc;
+    w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
+    w.k = t.dec_k; w.l2 = t.d_dec_l2;
+    w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0];
+    // chains tid and tid + T of every thread
+    const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
+    uint64_t wgs = (threads_needed + kWalkWaves * 64 - 1) / (kWalkWaves * 64);
+    wgs = wgs ? wgs : 1;
+    hipLaunchKernelGGL(k_idx_walk, dim3(wgs), dim3(kWalkWaves * 64), t.walk_lds_bytes + kWalkLdsRingBytes, s, w);
     return hipGetLastError();
 }
 
@@ -2222,8 +2482,7 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.nseg = (bits + kSegBits - 1) / kSegBits;
     if (y.nseg == 0) return hipErrorInvalidValue;
     unsigned long long* p = d_scratch;
-    y.ex[0] = p; p += y.nseg;
-    y.ex[1] = p; p += y.nseg;
+    y.ent = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     unsigned long long* first = p; p += y.nseg;
     p += (reinterpret_cast<uintptr_t>(p) >> 3) & 1;  // 16-byte aligned bitmap rows (uint4 stores)
@@ -2240,9 +2499,15 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
         return hipGetLastError();
     }
     const uint32_t lds = t.dec_lds_bytes;
-    if (t.dec_mode == DEC_DENSE) return run_index<DEC_DENSE>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
-    if (t.dec_mode == DEC_FIXED16) return run_index<DEC_FIXED16>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
-    return run_index<DEC_LUT>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
+    hipError_t e = hipMemsetAsync(y.dirty[0], 0, 4 * y.nseg, s);  // the scan marks the segments to check
+    if (e != hipSuccess) return e;
+    const bool walk = t.walk_lds_bytes > 0 && a.nwords >= 4;
+    if (walk) e = scan_walk(t, a, y, ncu, s);
+    else if (t.dec_mode == DEC_DENSE) e = scan_lut<DEC_DENSE>(a, y, lds, ncu, s);
+    else e = scan_lut<DEC_LUT>(a, y, lds, ncu, s);
+    if (e != hipSuccess) return e;
+    if (t.dec_mode == DEC_DENSE) return finish_index<DEC_DENSE>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
+    return finish_index<DEC_LUT>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
 }
 
 }  // namespace hz
