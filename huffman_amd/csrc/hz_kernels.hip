@@ -2284,54 +2284,127 @@ HZ_DEV uint32_t select_bit(uint32_t m, uint32_t r) {
     return pos + ((r >= (m & 1u)) ? 1u : 0u);
 }
 
-// One wave per bitmap row: lane l holds the row's bits [64 l, 64 l + 64);
-// a wave scan of popcounts numbers every boundary. Boundary i < nsym with
-// i % 8 == 0 is a chain start (raw position, low 16 bits; k_sync_subs makes it
-// block-relative), i % 2048 == 0 also a block start; boundary nsym is the end
-// of the stream.
+// One workgroup per tile of kSelTileSegs bitmap rows (64 Kbit); thread t
+// holds words [8 t, 8 t + 8). A workgroup scan of popcounts numbers every
+// boundary from the tile's first (first[] of its first row). Boundary i < nsym
+// with i % 8 == 0 is a chain start (raw position, low 16 bits, staged in LDS
+// and stored as one contiguous run; k_sync_subs makes it block-relative),
+// i % 2048 == 0 also a block start; boundary nsym is the end of the stream.
 constexpr int kSelectThreads = 256;
+constexpr uint32_t kSelTileSegs = 16;
+constexpr uint32_t kSelTileWords = kSelTileSegs * kBmpWords;  // 2048 = 8 words per thread
+constexpr uint32_t kSelMaxChains = kSelTileWords * 32 / kChainSyms + 2;
 __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint64_t nsym, uint64_t nblocks,
                                                                 const unsigned long long* first,
                                                                 unsigned long long* starts, uint16_t* subs) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t nwave = (uint64_t)gridDim.x * (kSelectThreads / 64);
-    for (uint64_t k = (uint64_t)blockIdx.x * (kSelectThreads / 64) + (threadIdx.x >> 6); k < y.nseg; k += nwave) {
-        const uint64_t f = first[k];
-        if (f > nsym) continue;  // wave-uniform
-        // the rows hold exactly nsym boundaries: the last codeword ends at the bitmap's end
-        if (k + 1 == y.nseg && lane == 0 && f + y.cnt[k] == nsym) starts[nblocks] = y.start + y.nseg * kSegBits;
-        const uint2 w = reinterpret_cast<const uint2*>(y.bmp + k * kBmpWords)[lane];
-        const uint32_t c0 = __popc(w.x), c1 = __popc(w.y);
-        uint64_t i = f + wave_incl_sum(c0 + c1) - (c0 + c1);  // number of the lane's first boundary
-        uint64_t base = y.start + k * kSegBits + 64u * (uint32_t)lane;
+    __shared__ uint16_t ch[kSelMaxChains];
+    __shared__ uint32_t wsum[kSelectThreads / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t ntile = (y.nseg + kSelTileSegs - 1) / kSelTileSegs;
+    const uint64_t nch_all = (nsym + kChainSyms - 1) / kChainSyms;  // chains with a start inside the stream
+    const uint64_t nw = y.nseg * kBmpWords;
+    // the next tile's first[] and bitmap words are loaded while this one is processed
+    auto load = [&](uint64_t tile, uint64_t& f, uint32_t (&mm)[8]) {
+        const uint64_t w0 = tile * kSelTileWords + 8u * threadIdx.x;
+        f = first[tile * kSelTileSegs];
+        if (w0 + 8 <= nw) {
+            const uint4* q = reinterpret_cast<const uint4*>(y.bmp + w0);
+            const uint4 a = q[0], b = q[1];
+            mm[0] = a.x; mm[1] = a.y; mm[2] = a.z; mm[3] = a.w; mm[4] = b.x; mm[5] = b.y; mm[6] = b.z; mm[7] = b.w;
+        } else {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t m = h ? w.y : w.x, c = h ? c1 : c0;
-            if (i <= nsym && nsym < i + c) starts[nblocks] = base + select_bit(m, (uint32_t)(nsym - i));
-            for (uint32_t r = (uint32_t)(-i) & 7u; r < c && i + r < nsym; r += 8) {
-                const uint64_t idx = i + r, pos = base + select_bit(m, r);
-                subs[idx / kChainSyms] = (uint16_t)pos;
-                if (idx % kBlockSyms == 0) starts[idx / kBlockSyms] = pos;
-            }
-            i += c;
-            base += 32;
+            for (int i = 0; i < 8; ++i) mm[i] = w0 + i < nw ? y.bmp[w0 + i] : 0u;
         }
+    };
+    uint64_t fn = 0;
+    uint32_t mn[8];
+    if (blockIdx.x < ntile) load(blockIdx.x, fn, mn);
+    for (uint64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const uint64_t seg0 = tile * kSelTileSegs;
+        const uint64_t f0 = fn;
+        uint32_t m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = mn[i];
+        if (tile + gridDim.x < ntile) load(tile + gridDim.x, fn, mn);
+        if (f0 > nsym) break;  // workgroup-uniform; later tiles start later still
+        const uint64_t w0 = seg0 * kBmpWords + 8u * threadIdx.x;
+        uint32_t c[8], tot = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { c[i] = __popc(m[i]); tot += c[i]; }
+        const uint32_t incl = wave_incl_sum(tot);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        uint32_t wpre = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < kSelectThreads / 64; ++w) {
+            const uint32_t v = wsum[w];
+            wpre += w < wid ? v : 0u;
+            all += v;
+        }
+        // 32-bit arithmetic relative to the tile's first boundary f0
+        const uint32_t d0 = wpre + incl - tot;  // the thread's first boundary: number f0 + d0
+        const uint64_t left = nsym - f0;
+        const uint32_t dn = left < 0xffffffffull ? (uint32_t)left : 0xffffffffu;  // boundaries before nsym
+        const uint32_t q = (uint32_t)(f0 & 7), qb = (uint32_t)(f0 & (kBlockSyms - 1));
+        const uint64_t base = y.start + w0 * 32;
+        const uint64_t cb = (f0 + kChainSyms - 1) / kChainSyms;  // first chain starting in the tile
+        uint32_t cum[8];
+        cum[0] = 0;
+#pragma unroll
+        for (int h = 1; h < 8; ++h) cum[h] = cum[h - 1] + c[h - 1];
+        // the thread's boundary of rank r (0-based): word h = #(cum[1..7] <= r), bit = select in m[h]
+        auto pos_of = [&](uint32_t r) -> uint64_t {
+            uint32_t mh = m[0], ch0 = 0, sh = 0;
+#pragma unroll
+            for (int h = 1; h < 8; ++h) {
+                const bool in = r >= cum[h];
+                mh = in ? m[h] : mh;
+                ch0 = in ? cum[h] : ch0;
+                sh = in ? 32u * h : sh;
+            }
+            return base + sh + select_bit(mh, r - ch0);
+        };
+        if (d0 <= dn && dn < d0 + tot) starts[nblocks] = pos_of(dn - d0);
+        // chain starts: boundaries whose number is a multiple of 8
+        for (uint32_t r = (8u - ((q + d0) & 7)) & 7; r < tot && d0 + r < dn; r += 8) {
+            const uint32_t d = d0 + r;
+            const uint64_t pos = pos_of(r);
+            ch[((q + d) >> 3) - (q ? 1u : 0u)] = (uint16_t)pos;
+            if (((qb + d) & (kBlockSyms - 1)) == 0) starts[(f0 + d) / kBlockSyms] = pos;
+        }
+        // the rows hold exactly nsym boundaries: the last codeword ends at the bitmap's end
+        if (threadIdx.x == 0 && seg0 + kSelTileSegs >= y.nseg && f0 + all == nsym)
+            starts[nblocks] = y.start + y.nseg * kSegBits;
+        __syncthreads();
+        uint64_t ce = (f0 + all + kChainSyms - 1) / kChainSyms;
+        ce = ce < nch_all ? ce : nch_all;
+        for (uint64_t t = cb + threadIdx.x; t < ce; t += kSelectThreads) subs[t] = ch[t - cb];
+        __syncthreads();
     }
 }
 
 // Chain positions relative to their block start (mod 2^16), chains past the
-// stream's end at the end, and the largest block.
+// stream's end at the end, and the largest block. One thread per lane word
+// (four chains, one u64) of the index.
 __global__ __launch_bounds__(256) void k_sync_subs(uint64_t nsym, uint64_t nblocks, unsigned long long* starts,
-                                                   uint16_t* subs) {
-    const uint64_t nch = nblocks * kChainsPerBlock;
+                                                   unsigned long long* sub64) {
+    const uint64_t nq = nblocks * kWave;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t end = starts[nblocks];
     unsigned long long mx = 0;
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += stride) {
-        const uint64_t b = c / kChainsPerBlock;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+        const uint64_t b = q / kWave;
         const uint64_t bs = starts[b];
-        const uint64_t raw = c * kChainSyms < nsym ? (uint64_t)subs[c] : starts[nblocks];
-        subs[c] = (uint16_t)((raw - bs) & 0xffffu);
-        if (c % kChainsPerBlock == 0) {
+        const uint64_t raw = sub64[q];
+        uint64_t out = 0;
+#pragma unroll
+        for (int t = 0; t < kChainsPerLane; ++t) {
+            const uint64_t c = q * kChainsPerLane + t;
+            const uint64_t p = c * kChainSyms < nsym ? (raw >> (16 * t)) & 0xffffu : end;
+            out |= ((p - bs) & 0xffffu) << (16 * t);
+        }
+        sub64[q] = out;
+        if (q % kWave == 0) {
             const unsigned long long bits = starts[b + 1] - bs;
             mx = bits > mx ? bits : mx;
         }
@@ -2387,14 +2460,16 @@ static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long*
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(d_index + a.nblocks + 1, 0, 8, s)) != hipSuccess) return e;
     {
-        uint64_t sg = (y.nseg + kSelectThreads / 64 - 1) / (kSelectThreads / 64);
+        // tiles in order over a grid-stride loop: a workgroup stops at the first tile past the stream
+        uint64_t sg = (y.nseg + kSelTileSegs - 1) / kSelTileSegs;
         sg = sg < (uint64_t)ncu * 8 ? sg : (uint64_t)ncu * 8;
         hipLaunchKernelGGL(k_sync_select, dim3(sg), dim3(kSelectThreads), 0, s, y, a.nsym, a.nblocks,
                            (const unsigned long long*)first, d_index, subs);
     }
-    uint64_t sw = (a.nblocks * kChainsPerBlock + 255) / 256;
+    uint64_t sw = (a.nblocks * kWave + 255) / 256;
     sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
-    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index, subs);
+    hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index,
+                       d_index + index_sub_offset(a.nblocks));
     return hipGetLastError();
 }
 
