@@ -63,8 +63,17 @@ constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): per chain an LDS ring of 4 payload chunks (16 B)
 // plus a copy of chunk 0 and 4 mark chunks; kWalkChains chains per lane,
 // kWalkWaves waves per CU. Its LUT image's hot heads get the rest of the LDS.
-constexpr int kWalkChains = 2;
-constexpr int kWalkWaves = 4;  // 2..8 measured: 4 fastest (more waves: more L2 misses on the per-chain streams)
+// Measured at 16 GiB Zipf (index build): 1 chain x 8 waves 38.4 ms; 1 x 6/10/12/13
+// waves 43.8/39.6/41.1/44.7; 2 chains x 4 waves 53.7; 3 x 3 78; 4 x 2 105 (more
+// chains per lane compile to worse code than more waves).
+#ifndef HZ_WALK_CHAINS
+#define HZ_WALK_CHAINS 1
+#endif
+#ifndef HZ_WALK_WAVES
+#define HZ_WALK_WAVES 8
+#endif
+constexpr int kWalkChains = HZ_WALK_CHAINS;
+constexpr int kWalkWaves = HZ_WALK_WAVES;
 constexpr uint32_t kRingWords = 36;
 constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
 constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;

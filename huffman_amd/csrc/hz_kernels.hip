@@ -1990,7 +1990,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 
 // ---------------------------------------------------------------------------
 // Index walker for the pipelined decoder's codebooks (codes <= 32 bits, one
-// global LUT level): LONG chains -- each lane walks two stretches of spc whole
+// global LUT level): LONG chains -- each lane walks kWalkChains stretches of spc whole
 // segments, each starting kWalkLead bits early so the walk has resynchronised
 // (P(not) ~ 4e-4 on Zipf) when it reaches its first segment: one start per
 // ~10^5 codewords instead of one per segment. Each chain streams its payload
@@ -2007,7 +2007,10 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
 // when the lead-in resynchronised.
 // ---------------------------------------------------------------------------
-constexpr int kWalkSteps = 8;  // steps per round: ~92 bits consumed on Zipf, 128 refilled (6 and 12 measured slower)
+#ifndef HZ_WALK_STEPS
+#define HZ_WALK_STEPS 8
+#endif
+constexpr int kWalkSteps = HZ_WALK_STEPS;  // steps per round: ~92 bits consumed on Zipf, 128 refilled
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
