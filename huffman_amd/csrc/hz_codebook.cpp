@@ -529,11 +529,8 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
 }
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global
-// memory. `walk` receives the index walker's image (hz_kernels.hip
-// k_idx_walk): the same level 1 with hot heads sized to the LDS its rings
-// leave, over the same global levels.
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1,
-                  std::vector<uint32_t>* walk) {
+// memory.
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
     K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
     img.assign(1u << K1, 0u);
@@ -550,10 +547,6 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     for (auto& e : img) if (!e) e = leaf(1, 0);
     for (auto& e : l2) if (!e) e = leaf(1, 0);
     if (l2.empty()) l2.push_back(leaf(1, 0));
-    if (walk) {
-        *walk = img;
-        add_lds_level(cb, *walk, l2, K1, (long)(kLdsBytes / 4) - (long)walk->size() - (long)(kWalkLdsRingBytes / 4) - 64);
-    }
     // heads fill what the decoder's staging slots (16 waves, sized from the
     // Kraft-weighted mean code length) leave
     double kbits = 0.0;
@@ -563,6 +556,34 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     add_lds_level(cb, img, l2, K1,
                   (long)(kLdsBytes / 4) - (long)img.size() - (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64);
     return HZ_OK;
+}
+
+// Index walker tables (hz_kernels.hip k_idx_walk): a walk needs code LENGTHS
+// only. img: one byte per K-bit window, K = min(max_len, kWalkK): the length
+// of the code the window starts with, 0 when that code is longer than K.
+// esc (max_len > K): one byte per max_len-bit window, filled under the escape
+// prefixes. Windows no code starts (incomplete code spaces) read length 1, so
+// a walk past the stream's end keeps moving. Byte i of a table is byte i of
+// its u32 vector (little-endian).
+void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M) {
+    M = (int)cb->max_len;
+    K = std::min(M, kWalkK);
+    img.assign(std::max<size_t>((size_t)1 << K, 16) / 4, 0x01010101u);
+    uint8_t* t1 = reinterpret_cast<uint8_t*>(img.data());
+    esc.clear();
+    if (M > K) esc.assign(((size_t)1 << M) / 4, 0x01010101u);
+    uint8_t* t2 = reinterpret_cast<uint8_t*>(esc.data());
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const int L = cb->len[s];
+        if (!L) continue;
+        const uint64_t c = cb->code[s];
+        if (L <= K) {
+            memset(t1 + (c << (K - L)), L, (size_t)1 << (K - L));
+        } else {
+            t1[c >> (L - K)] = 0;
+            memset(t2 + (c << (M - L)), L, (size_t)1 << (M - L));
+        }
+    }
 }
 
 }  // namespace hz

@@ -31,8 +31,8 @@ std::vector<uint32_t> build_len8(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1,
-                  std::vector<uint32_t>* walk);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
+void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M);
 }  // namespace hz
 
 using namespace hz;
@@ -76,7 +76,7 @@ struct hz_ctx {
     bool ev_used[4] = {false, false, false, false};
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0,
-           cap_walk_lds = 0;
+           cap_walk_lds = 0, cap_walk_esc = 0;
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -106,6 +106,7 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_dec_lds);
     (void)hipFree(t.d_dec_l2);
     (void)hipFree(t.d_walk_lds);
+    (void)hipFree(t.d_walk_esc);
     t = Tables();
 }
 
@@ -332,13 +333,10 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.dec_max_len = (int)cb->max_len;
     t.dec_min_len = (int)cb->min_len;
     const int mode = select_dec_mode(cb);
-    std::vector<uint32_t> dimg, l2, wimg;
-    // the index walker takes the pipelined decoder's codebooks: codes <= 32 bits, one global level
-    const bool walk = mode == DEC_LUT && cb->max_len <= 32 &&
-                      (int)cb->max_len <= std::min((int)cb->max_len, kDecLutMaxK1) + kDecLevelBits;
+    std::vector<uint32_t> dimg, l2, wimg, wesc;
     if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
     else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
-    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, walk ? &wimg : nullptr);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
@@ -348,11 +346,14 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (l2.empty()) l2.push_back(0x80010000u);
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
+    // the index walker's length tables (FIXED16 streams have an arithmetic index)
     t.walk_lds_bytes = 0;
-    if (!wimg.empty()) {
-        while (wimg.size() % 4) wimg.push_back(0);
+    if (mode != DEC_FIXED16 && cb->max_len >= 1 && cb->max_len <= kWalkMaxLen) {
+        build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m);
         if (wimg.size() * 4 + kWalkLdsRingBytes <= kLdsBytes) {
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
+            if (wesc.empty()) wesc.push_back(0x01010101u);
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;
             t.walk_lds_bytes = (uint32_t)(wimg.size() * 4);
         }
     }

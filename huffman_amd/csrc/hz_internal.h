@@ -61,8 +61,8 @@ constexpr int kDecLevelBits = HZ_DEC_LEVEL_BITS;  // bits per global subtable le
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): per chain an LDS ring of 4 payload chunks (16 B)
-// plus a copy of chunk 0 and 4 mark chunks; kWalkChains chains per lane,
-// kWalkWaves waves per CU. Its LUT image's hot heads get the rest of the LDS.
+// and 4 mark chunks; kWalkChains chains per lane, kWalkWaves waves per CU,
+// beside a u8 code-length table of the top min(max_len, kWalkK) window bits.
 // Measured at 16 GiB Zipf (index build): 1 chain x 8 waves 38.4 ms; 1 x 6/10/12/13
 // waves 43.8/39.6/41.1/44.7; 2 chains x 4 waves 53.7; 3 x 3 78; 4 x 2 105 (more
 // chains per lane compile to worse code than more waves).
@@ -70,11 +70,16 @@ constexpr int kDecMaxWaves = 16;
 #define HZ_WALK_CHAINS 1
 #endif
 #ifndef HZ_WALK_WAVES
-#define HZ_WALK_WAVES 8
+#define HZ_WALK_WAVES 10
 #endif
+#ifndef HZ_WALK_K
+#define HZ_WALK_K 16
+#endif
+constexpr int kWalkK = HZ_WALK_K;           // walker length table: 2^16 u8 in LDS
+constexpr int kWalkMaxLen = 22;             // escape table: 2^max_len u8 in global memory (<= 4 MiB)
 constexpr int kWalkChains = HZ_WALK_CHAINS;
 constexpr int kWalkWaves = HZ_WALK_WAVES;
-constexpr uint32_t kRingWords = 36;
+constexpr uint32_t kRingWords = 33;  // odd stride: the lanes' rings start in distinct banks
 constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
 constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
@@ -112,8 +117,10 @@ struct Tables {
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
     uint64_t dec_l2_entries = 0;
-    uint32_t* d_walk_lds = nullptr; // LDS image of the index walker (level 1 + smaller hot heads)
-    uint32_t walk_lds_bytes = 0;    // 0 = no walker image (the segment walkers build the index)
+    uint32_t* d_walk_lds = nullptr; // index walker: u8 code length per walk_k-bit window (0 = longer code)
+    uint32_t walk_lds_bytes = 0;    // 0 = no walker tables (the segment walkers build the index)
+    uint32_t* d_walk_esc = nullptr; // index walker: u8 code length per walk_m-bit window (walk_m > walk_k)
+    int walk_k = 0, walk_m = 0;
 };
 
 // Count-pass length table layout: the high byte is XORed into the bank bits

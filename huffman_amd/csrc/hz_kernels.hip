@@ -2019,10 +2019,11 @@ struct WalkArgs {
     uint32_t bit_adj;         // payload bit 0 = bit bit_adj of words
     uint64_t start;           // stream bit of the first symbol
     uint64_t nseg, spc, nchains;
-    const uint32_t* lds_img;  // walker LUT image (level 1 + hot heads)
+    const uint32_t* lds_img;  // u8 code length per k-bit window (0: longer than k bits)
     uint32_t lds_words;
     int k;
-    const uint32_t* l2;       // global level (every entry a leaf)
+    const uint8_t* esc;       // u8 code length per m-bit window (escapes only)
+    int m;
     uint32_t* bmp;
     unsigned long long* cnt;
     unsigned long long* ent;
@@ -2047,33 +2048,70 @@ HZ_DEV uint4 walk_fix(const WalkArgs& a, uint64_t w, uint4 x) {
     return make_uint4(q[0], q[1], q[2], q[3]);
 }
 
-// Chunk slot q (0..3) of a transposed payload ring, byte-swapped; slot 0 also
-// fills the copy rows 16..19 that a window at the ring's last word reads.
+// Chunk slot q (0..3) of a payload ring, byte-swapped.
 template <uint32_t ROW>
 HZ_DEV void ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
 #pragma unroll
     for (int i = 0; i < 4; ++i) ring[(4 * q + i) * ROW] = v[i];
-    if (q == 0) {
+}
+
+// Payload chunks reach a chain's ring from a register group of kWalkGroup
+// chunks loaded together (one 64/128-byte run per lane, issued as soon as the
+// previous group is in the ring), and finished mark chunks leave as a run of
+// kWalkMarkGroup chunks: every lane touches a different stretch of the stream,
+// so 16-byte accesses spread over many rounds let L2 evict a line between them
+// (fetches ~10x the payload, writes ~3.5x the bitmap with single chunks).
+#ifndef HZ_WALK_GROUP
+#define HZ_WALK_GROUP 4
+#endif
+#ifndef HZ_WALK_MGROUP
+#define HZ_WALK_MGROUP 4
+#endif
+constexpr uint32_t kWalkGroup = HZ_WALK_GROUP;
+constexpr uint32_t kWalkMarkGroup = HZ_WALK_MGROUP;
+static_assert((kWalkGroup & (kWalkGroup - 1)) == 0 && kWalkGroup >= 1 && kWalkGroup <= 8, "walk group");
+static_assert((kWalkMarkGroup & (kWalkMarkGroup - 1)) == 0 && kWalkMarkGroup >= 1 && kWalkMarkGroup <= 8,
+              "mark group");
+
+template <uint32_t G>
+HZ_DEV uint4 pick_group(const uint4 (&g)[G], uint32_t i) {
+    uint4 x = g[0];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ring[(16 + i) * ROW] = v[i];
+    for (uint32_t t = 1; t < G; ++t) {
+        const bool s = i == t;
+        x.x = s ? g[t].x : x.x;
+        x.y = s ? g[t].y : x.y;
+        x.z = s ? g[t].z : x.z;
+        x.w = s ? g[t].w : x.w;
     }
+    return x;
 }
 
 __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(lds);
     constexpr int C = kWalkChains;
     constexpr uint32_t kRow = 1;  // ring word stride
+    constexpr uint32_t G = kWalkGroup, GM = kWalkMarkGroup;
+    constexpr uint32_t kMarkRow = 16;  // ring words 0..15 payload, 16..31 marks, 32 pad
     const uint32_t k = (uint32_t)a.k;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = threadIdx.x >> 6;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t* ring[C];
-    uint32_t off[C], off0[C], ms[C], end[C], f[C], mcount[C], nmc[C], rc[C], pgi[C];
+    uint32_t off[C], off0[C], ms[C], end[C], f[C], mcount[C], nmc[C], rc[C];
     uint64_t bch[C], x0[C], seg0[C], seg1[C];
     bool live[C], pk[C];
+    uint4 pre[C][G];   // payload group holding chunk f
+    uint4 mk[C][GM];   // finished mark chunks of the current run
+    // bit buffer: bits [off, off + nbits) MSB-aligned in buf; nxt = ring word wn,
+    // the word after them ((off + nbits) % 32 == 0). The window comes from
+    // registers, so a step's dependent LDS chain is level 1 -> hot head only.
+    uint64_t buf[C];
+    uint32_t nbits[C], wn[C], nxt[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         ring[c] = lds + a.lds_words + ((wid * C + c) * 64 + lane) * kRingWords;
@@ -2090,128 +2128,142 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         ms[c] = off[c] + (uint32_t)(cs - x0[c]);
         end[c] = live[c] ? off[c] + (uint32_t)(ce - x0[c]) : off[c];
         nmc[c] = live[c] ? (uint32_t)((ce - cs) / 128) : 0u;
-        mcount[c] = rc[c] = pgi[c] = 0;
+        mcount[c] = rc[c] = 0;
         pk[c] = false;
 #pragma unroll
-        for (int i = 20; i < 36; ++i) ring[c][i * kRow] = 0u;
+        for (uint32_t i = kMarkRow; i < kRingWords; ++i) ring[c][i * kRow] = 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < GM; ++i) mk[c][i] = make_uint4(0, 0, 0, 0);
     }
-    // prologue: chunks 0..2 of every chain
+    // prologue: chunks 0..2 of every chain, and the group holding chunk 3
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         uint4 v[3];
 #pragma unroll
         for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch[c] + g));
+        const uint64_t gb = (bch[c] + 3) & ~(uint64_t)(G - 1);
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) pre[c][g] = walk_load(a, 4 * (gb + g));
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
             ring_put<kRow>(ring[c], (uint32_t)g, walk_fix(a, 4 * (bch[c] + g), v[g]));
         }
         f[c] = 3;
+        const uint32_t w0 = off[c] >> 5, sh = off[c] & 31;
+        buf[c] = (((uint64_t)ring[c][w0 * kRow] << 32) | ring[c][(w0 + 1) * kRow]) << sh;
+        nbits[c] = 64 - sh;
+        wn[c] = w0 + 2;
     }
-    uint32_t pW[C], pe[C], pD[C];  // a parked chain's window, entry and consumed bits
-    // refill of chunk f when it fits the ring (the chain no longer needs chunk f - 4);
-    // issued at the end of the round before (here: the prologue) and written at the
-    // end of this one, ahead of the round's bitmap stores in the vmcnt queue
-    bool rf[C];
-    uint4 v[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        rf[c] = f[c] <= ((off[c] - 1) >> 7) + 3;
-        if (rf[c]) v[c] = walk_load(a, 4 * (bch[c] + f[c]));
-    }
+    uint32_t pW[C];  // a parked chain's window
+    // chunk f goes into the ring at a round's end when it fits (the chain no
+    // longer needs chunk f - 4), ahead of the round's bitmap stores
     for (;;) {
         bool alive = false;
 #pragma unroll
         for (int c = 0; c < C; ++c) alive |= off[c] < end[c] || mcount[c] < nmc[c];
         if (!__any(alive)) break;
-        uint32_t lim[C];  // the round's steps stay below: chain end, filled data, free mark slots
+        // the round's steps stay below: chain end, filled data (the buffer and the
+        // word after it, after a 32-bit step: off + 96 bits), free mark slots
+        uint32_t lim[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) lim[c] = min(end[c], min(128 * f[c] - 31, ms[c] + 128 * (mcount[c] + 4)));
-        // branch-free steps: every chain's window, level-1 and hot-head reads are
-        // in flight together; a chain that cannot step only leaves off unchanged
+        for (int c = 0; c < C; ++c) {
+            lim[c] = min(end[c], min(128 * f[c] - 96, ms[c] + 128 * (mcount[c] + 4)));
+            nxt[c] = ring[c][(wn[c] & 15) * kRow];  // (re)read after the ring's refill
+        }
+        // branch-free steps: one LDS length lookup per chain and step; a chain that
+        // cannot step only leaves off unchanged, a code longer than k bits parks the
+        // chain for the rest of the round
 #pragma unroll
         for (int t = 0; t < kWalkSteps; ++t) {
-            uint32_t W[C], e[C], x[C], D[C], wa[C], wb[C];
-            bool ok[C], h[C];
+            uint32_t W[C], e[C];
+            bool ok[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 ok[c] = !pk[c] & (off[c] < lim[c]);
-                const uint32_t* r = ring[c] + (((off[c] - 1) >> 5) & 15) * kRow;
-                wa[c] = r[0];
-                wb[c] = r[kRow];
+                W[c] = (uint32_t)(buf[c] >> 32);
+                e[c] = lds8[W[c] >> (32 - k)];
             }
             HZ_WALK_FENCE();
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                W[c] = __builtin_amdgcn_alignbit(wa[c], wb[c], (0u - off[c]) & 31);
-                e[c] = lds[W[c] >> (32 - k)];
-            }
-            HZ_WALK_FENCE();
-#pragma unroll
-            for (int c = 0; c < C; ++c) {  // LDS second level (hot heads); other lanes read word 0
-                h[c] = (e[c] >> 30) == 1u;
-                const uint32_t nb = (e[c] >> 26) & 15u;
-                D[c] = h[c] ? k + nb : k;
-                x[c] = lds[h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u];
-            }
-            HZ_WALK_FENCE();
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const uint32_t ee = h[c] ? x[c] : e[c];
-                const bool leaf = (int32_t)ee < 0;
+                const bool leaf = e[c] != 0u;
                 const bool adv = ok[c] & leaf, park = ok[c] & !leaf;
                 const uint32_t rel = off[c] - ms[c];
                 const uint32_t bit = (adv & (off[c] >= ms[c])) ? (1u << (rel & 31)) : 0u;
-                atomicOr(ring[c] + (20 + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
-                off[c] += adv ? (ee >> 16) & 63u : 0u;
+                atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
+                const uint32_t L = adv ? e[c] : 0u;
+                off[c] += L;
+                buf[c] <<= L;
+                nbits[c] -= L;
+                const bool rfl = nbits[c] <= 32;  // >= 1 (codes <= 32 bits)
+                buf[c] |= rfl ? (uint64_t)nxt[c] << ((32u - nbits[c]) & 31u) : 0ull;
+                nbits[c] += rfl ? 32u : 0u;
+                wn[c] += rfl ? 1u : 0u;
+                nxt[c] = ring[c][(wn[c] & 15) * kRow];
                 pk[c] |= park;
                 pW[c] = park ? W[c] : pW[c];
-                pe[c] = park ? ee : pe[c];
-                pD[c] = park ? D[c] : pD[c];
             }
         }
         uint32_t g[C];
 #pragma unroll
         for (int c = 0; c < C; ++c)
-            if (pk[c]) g[c] = a.l2[(pe[c] & 0x3ffffffu) + ((pW[c] << pD[c]) >> (32 - ((pe[c] >> 26) & 15u)))];
-        bool fl[C];
-        uint4 m[C];
-        uint64_t j[C];
+            if (pk[c]) g[c] = a.esc[pW[c] >> (32 - a.m)];
+        bool fl[C], ld[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             if (pk[c]) {
                 if (off[c] >= ms[c]) {
                     const uint32_t rel = off[c] - ms[c];
-                    atomicOr(ring[c] + (20 + ((rel >> 5) & 15)) * kRow, 1u << (rel & 31));
+                    atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, 1u << (rel & 31));
                 }
-                off[c] += (g[c] >> 16) & 63u;
+                const uint32_t L = g[c];
+                off[c] += L;
+                buf[c] <<= L;
+                nbits[c] -= L;
+                if (nbits[c] <= 32) {
+                    buf[c] |= (uint64_t)nxt[c] << ((32u - nbits[c]) & 31u);
+                    nbits[c] += 32;
+                    ++wn[c];
+                }
                 pk[c] = false;
             }
-            if (rf[c]) {
-                ring_put<kRow>(ring[c], f[c] & 3, walk_fix(a, 4 * (bch[c] + f[c]), v[c]));
+            ld[c] = false;
+            if (f[c] <= ((off[c] - 1) >> 7) + 3) {
+                const uint64_t q = bch[c] + f[c];
+                ring_put<kRow>(ring[c], f[c] & 3, walk_fix(a, 4 * q, pick_group<G>(pre[c], (uint32_t)q & (G - 1))));
                 ++f[c];
+                ld[c] = ((q + 1) & (G - 1)) == 0;  // the group is in the ring: load the next one
             }
-            // mark chunk mcount leaves once the walk is past it
+            // mark chunk mcount is done once the walk is past it
             fl[c] = mcount[c] < nmc[c] && off[c] >= ms[c] && off[c] - ms[c] >= 128 * (mcount[c] + 1);
             if (fl[c]) {
-                uint32_t* slot = ring[c] + (20 + 4 * (mcount[c] & 3)) * kRow;
-                m[c] = make_uint4(slot[0], slot[kRow], slot[2 * kRow], slot[3 * kRow]);
+                uint32_t* slot = ring[c] + (kMarkRow + 4 * (mcount[c] & 3)) * kRow;
+                const uint4 m = make_uint4(slot[0], slot[kRow], slot[2 * kRow], slot[3 * kRow]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) slot[i * kRow] = 0u;
-                j[c] = seg0[c] * (kSegBits / 128) + mcount[c];
-                rc[c] = ((mcount[c] & 31) ? rc[c] : 0u) + __popc(m[c].x) + __popc(m[c].y) + __popc(m[c].z) +
-                        __popc(m[c].w);
+                rc[c] = ((mcount[c] & 31) ? rc[c] : 0u) + __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+#pragma unroll
+                for (uint32_t i = 0; i + 1 < GM; ++i) mk[c][i] = mk[c][i + 1];  // shift in (constant indices)
+                mk[c][GM - 1] = m;
             }
         }
 #pragma unroll
-        for (int c = 0; c < C; ++c) {  // the next round's refill, then this round's bitmap stores
-            rf[c] = f[c] <= ((off[c] - 1) >> 7) + 3;
-            if (rf[c]) v[c] = walk_load(a, 4 * (bch[c] + f[c]));
+        for (int c = 0; c < C; ++c) {  // the next group's loads, then this round's bitmap stores
+            if (!ld[c]) continue;
+            const uint64_t q = bch[c] + f[c];
+#pragma unroll
+            for (uint32_t i = 0; i < G; ++i) pre[c][i] = walk_load(a, 4 * (q + i));
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             if (!fl[c]) continue;
-            reinterpret_cast<uint4*>(a.bmp)[j[c]] = m[c];
-            if ((mcount[c] & 31) == 31) a.cnt[j[c] >> 5] = rc[c];
+            const uint64_t j = seg0[c] * (kSegBits / 128) + mcount[c];
+            if ((mcount[c] & (GM - 1)) == GM - 1) {
+                uint4* dst = reinterpret_cast<uint4*>(a.bmp) + (j - (GM - 1));
+#pragma unroll
+                for (uint32_t i = 0; i < GM; ++i) dst[i] = mk[c][i];
+            }
+            if ((mcount[c] & 31) == 31) a.cnt[j >> 5] = rc[c];
             ++mcount[c];
         }
     }
@@ -2425,7 +2477,7 @@ uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
     // ent, cnt, first (u64), bitmap (kBmpWords u32), dirty[2] (u32), counter, tiles
-    return nseg * (3 + kBmpWords / 2 + 1) + 1 + ntiles + 8;
+    return nseg * (3 + kBmpWords / 2 + 1) + 1 + ntiles + 24;
 }
 
 // Common tail of the index build, after the boundary bitmap and the dirty
@@ -2511,7 +2563,7 @@ static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int n
     w.spc = (y.nseg + target - 1) / target;
     w.nchains = (y.nseg + w.spc - 1) / w.spc;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
-    w.k = t.dec_k; w.l2 = t.d_dec_l2;
+    w.k = t.walk_k; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
     w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0];
     // chains tid and tid + T of every thread
     const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
@@ -2563,7 +2615,7 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     y.ent = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     unsigned long long* first = p; p += y.nseg;
-    p += (reinterpret_cast<uintptr_t>(p) >> 3) & 1;  // 16-byte aligned bitmap rows (uint4 stores)
+    p += ((128 - (reinterpret_cast<uintptr_t>(p) & 127)) & 127) / 8;  // 128-byte aligned bitmap (run stores)
     y.bmp = reinterpret_cast<uint32_t*>(p); p += y.nseg * (kBmpWords / 2);
     y.dirty[0] = reinterpret_cast<uint32_t*>(p);
     y.dirty[1] = y.dirty[0] + y.nseg;

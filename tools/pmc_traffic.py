@@ -29,9 +29,9 @@ STAGES = {
     "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16"),
              ("k_pack_write", "k_pack_fixed16")),
     "decode": (("k_decode", "k_decode_fixed16"), ("k_decode", "k_decode_fixed16")),
-    "index": (("k_idx_scan", "k_idx_iter", "k_idx_emit", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2",
-               "k_sync_iter", "k_sync_emit", "k_sync_emit2", "k_sync_subs"),
-              ("k_idx_emit", "k_idx_fixed16", "k_sync_emit", "k_sync_emit2")),
+    "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
+               "k_sync_subs"),
+              ("k_sync_subs", "k_idx_fixed16")),
 }
 
 
