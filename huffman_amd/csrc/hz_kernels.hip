@@ -2107,11 +2107,10 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     bool live[C], pk[C];
     uint4 pre[C][G];   // payload group holding chunk f
     uint4 mk[C][GM];   // finished mark chunks of the current run
-    // bit buffer: bits [off, off + nbits) MSB-aligned in buf; nxt = ring word wn,
-    // the word after them ((off + nbits) % 32 == 0). The window comes from
-    // registers, so a step's dependent LDS chain is level 1 -> hot head only.
-    uint64_t buf[C];
-    uint32_t nbits[C], wn[C], nxt[C];
+    // window registers: the 32 bits at off are alignbit(w0, w1, sh) (sh in 0..31;
+    // 32 - sh bits of w0 consumed), nxt = ring word wn, the one after w1
+    uint32_t w0[C], w1[C], sh[C], wn[C], nxt[C];
+    bool gin[C];  // the payload group in pre[] lies inside the payload (no clamping)
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         ring[c] = lds + a.lds_words + ((wid * C + c) * 64 + lane) * kRingWords;
@@ -2142,6 +2141,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
 #pragma unroll
         for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch[c] + g));
         const uint64_t gb = (bch[c] + 3) & ~(uint64_t)(G - 1);
+        gin[c] = 4 * (gb + G) <= a.nwords && gb < a.nwords;
 #pragma unroll
         for (uint32_t g = 0; g < G; ++g) pre[c][g] = walk_load(a, 4 * (gb + g));
 #pragma unroll
@@ -2149,10 +2149,11 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             ring_put<kRow>(ring[c], (uint32_t)g, walk_fix(a, 4 * (bch[c] + g), v[g]));
         }
         f[c] = 3;
-        const uint32_t w0 = off[c] >> 5, sh = off[c] & 31;
-        buf[c] = (((uint64_t)ring[c][w0 * kRow] << 32) | ring[c][(w0 + 1) * kRow]) << sh;
-        nbits[c] = 64 - sh;
-        wn[c] = w0 + 2;
+        const uint32_t q0 = (off[c] - 1) >> 5;
+        w0[c] = ring[c][q0 * kRow];
+        w1[c] = ring[c][(q0 + 1) * kRow];
+        sh[c] = (0u - off[c]) & 31;
+        wn[c] = q0 + 2;
     }
     uint32_t pW[C];  // a parked chain's window
     // chunk f goes into the ring at a round's end when it fits (the chain no
@@ -2162,8 +2163,8 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
 #pragma unroll
         for (int c = 0; c < C; ++c) alive |= off[c] < end[c] || mcount[c] < nmc[c];
         if (!__any(alive)) break;
-        // the round's steps stay below: chain end, filled data (the buffer and the
-        // word after it, after a 32-bit step: off + 96 bits), free mark slots
+        // the round's steps stay below: chain end, filled data (w0, w1 and nxt: the
+        // bits below off + 96), free mark slots
         uint32_t lim[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -2180,7 +2181,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 ok[c] = !pk[c] & (off[c] < lim[c]);
-                W[c] = (uint32_t)(buf[c] >> 32);
+                W[c] = __builtin_amdgcn_alignbit(w0[c], w1[c], sh[c]);
                 e[c] = lds8[W[c] >> (32 - k)];
             }
             HZ_WALK_FENCE();
@@ -2193,12 +2194,12 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
                 atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
                 const uint32_t L = adv ? e[c] : 0u;
                 off[c] += L;
-                buf[c] <<= L;
-                nbits[c] -= L;
-                const bool rfl = nbits[c] <= 32;  // >= 1 (codes <= 32 bits)
-                buf[c] |= rfl ? (uint64_t)nxt[c] << ((32u - nbits[c]) & 31u) : 0ull;
-                nbits[c] += rfl ? 32u : 0u;
-                wn[c] += rfl ? 1u : 0u;
+                const int32_t r = (int32_t)sh[c] - (int32_t)L;  // >= -32 (codes <= 32 bits)
+                const bool cr = r < 0;                         // w0 used up: shift the words
+                w0[c] = cr ? w1[c] : w0[c];
+                w1[c] = cr ? nxt[c] : w1[c];
+                sh[c] = (uint32_t)(cr ? r + 32 : r);
+                wn[c] += cr ? 1u : 0u;
                 nxt[c] = ring[c][(wn[c] & 15) * kRow];
                 pk[c] |= park;
                 pW[c] = park ? W[c] : pW[c];
@@ -2218,19 +2219,21 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
                 }
                 const uint32_t L = g[c];
                 off[c] += L;
-                buf[c] <<= L;
-                nbits[c] -= L;
-                if (nbits[c] <= 32) {
-                    buf[c] |= (uint64_t)nxt[c] << ((32u - nbits[c]) & 31u);
-                    nbits[c] += 32;
+                const int32_t r = (int32_t)sh[c] - (int32_t)L;
+                if (r < 0) {
+                    w0[c] = w1[c];
+                    w1[c] = nxt[c];
                     ++wn[c];
                 }
+                sh[c] = (uint32_t)(r < 0 ? r + 32 : r);
                 pk[c] = false;
             }
             ld[c] = false;
             if (f[c] <= ((off[c] - 1) >> 7) + 3) {
                 const uint64_t q = bch[c] + f[c];
-                ring_put<kRow>(ring[c], f[c] & 3, walk_fix(a, 4 * q, pick_group<G>(pre[c], (uint32_t)q & (G - 1))));
+                uint4 x = pick_group<G>(pre[c], (uint32_t)q & (G - 1));
+                if (!gin[c]) x = walk_fix(a, 4 * q, x);
+                ring_put<kRow>(ring[c], f[c] & 3, x);
                 ++f[c];
                 ld[c] = ((q + 1) & (G - 1)) == 0;  // the group is in the ring: load the next one
             }
@@ -2251,8 +2254,15 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         for (int c = 0; c < C; ++c) {  // the next group's loads, then this round's bitmap stores
             if (!ld[c]) continue;
             const uint64_t q = bch[c] + f[c];
+            gin[c] = 4 * (q + G) <= a.nwords;
+            if (gin[c]) {
+                const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
 #pragma unroll
-            for (uint32_t i = 0; i < G; ++i) pre[c][i] = walk_load(a, 4 * (q + i));
+                for (uint32_t i = 0; i < G; ++i) pre[c][i] = src[i];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < G; ++i) pre[c][i] = walk_load(a, 4 * (q + i));
+            }
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
