@@ -2418,13 +2418,18 @@ __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint
 #pragma unroll
         for (int h = 1; h < 8; ++h) cum[h] = cum[h - 1] + c[h - 1];
         // the thread's boundary of rank r (0-based): word h = #(cum[1..7] <= r), bit = select in m[h]
+        // the select operands pass through an empty asm: a select between two loads
+        // of m[] / cum[] is otherwise folded into one dynamically indexed (scratch) load
         auto pos_of = [&](uint32_t r) -> uint64_t {
             uint32_t mh = m[0], ch0 = 0, sh = 0;
+            asm volatile("" : "+v"(mh));
 #pragma unroll
             for (int h = 1; h < 8; ++h) {
-                const bool in = r >= cum[h];
-                mh = in ? m[h] : mh;
-                ch0 = in ? cum[h] : ch0;
+                uint32_t mv = m[h], cv = cum[h];
+                asm volatile("" : "+v"(mv), "+v"(cv));
+                const bool in = r >= cv;
+                mh = in ? mv : mh;
+                ch0 = in ? cv : ch0;
                 sh = in ? 32u * h : sh;
             }
             return base + sh + select_bit(mh, r - ch0);
