@@ -350,7 +350,7 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.walk_lds_bytes = 0;
     if (mode != DEC_FIXED16 && cb->max_len >= 1 && cb->max_len <= kWalkMaxLen) {
         build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m);
-        if (wimg.size() * 4 + kWalkLdsRingBytes <= kLdsBytes) {
+        if (wimg.size() * 4 <= (1u << kWalkK)) {  // k_idx_walk's static table
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
             if (wesc.empty()) wesc.push_back(0x01010101u);
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;

@@ -82,6 +82,7 @@ constexpr int kWalkWaves = HZ_WALK_WAVES;
 constexpr uint32_t kRingWords = 33;  // odd stride: the lanes' rings start in distinct banks
 constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
 constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;
+static_assert((1u << kWalkK) + kWalkLdsRingBytes <= kLdsBytes, "walker LDS");
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
 
 // Per-wave LDS slot for one block's payload (u32 words), from the largest

@@ -2089,9 +2089,12 @@ HZ_DEV uint4 pick_group(const uint4 (&g)[G], uint32_t i) {
 }
 
 __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
+    // the length table at LDS address 0 (a static array: its address folds into
+    // the ds_read offset), the rings after it
+    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 4];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, a.lds_img, a.lds_words);
-    const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(lds);
+    copy_lds_table(wtab, a.lds_img, a.lds_words);
+    const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
     constexpr int C = kWalkChains;
     constexpr uint32_t kRow = 1;  // ring word stride
     constexpr uint32_t G = kWalkGroup, GM = kWalkMarkGroup;
@@ -2104,7 +2107,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     uint32_t* ring[C];
     uint32_t off[C], off0[C], ms[C], end[C], f[C], mcount[C], nmc[C], rc[C];
     uint64_t bch[C], x0[C], seg0[C], seg1[C];
-    bool live[C], pk[C];
+    bool live[C], pk[C], on[C];  // on: the walk has reached ms (marks count)
     uint4 pre[C][G];   // payload group holding chunk f
     uint4 mk[C][GM];   // finished mark chunks of the current run
     // window registers: the 32 bits at off are alignbit(w0, w1, sh) (sh in 0..31;
@@ -2113,7 +2116,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     bool gin[C];  // the payload group in pre[] lies inside the payload (no clamping)
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        ring[c] = lds + a.lds_words + ((wid * C + c) * 64 + lane) * kRingWords;
+        ring[c] = lds + ((wid * C + c) * 64 + lane) * kRingWords;
         const uint64_t ch = tid + c * T;
         live[c] = ch < a.nchains;
         const uint64_t chc = live[c] ? ch : 0;
@@ -2129,6 +2132,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         nmc[c] = live[c] ? (uint32_t)((ce - cs) / 128) : 0u;
         mcount[c] = rc[c] = 0;
         pk[c] = false;
+        on[c] = ms[c] == off[c];
 #pragma unroll
         for (uint32_t i = kMarkRow; i < kRingWords; ++i) ring[c][i * kRow] = 0u;
 #pragma unroll
@@ -2168,7 +2172,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         uint32_t lim[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            lim[c] = min(end[c], min(128 * f[c] - 96, ms[c] + 128 * (mcount[c] + 4)));
+            lim[c] = min(on[c] ? end[c] : ms[c], min(128 * f[c] - 96, ms[c] + 128 * (mcount[c] + 4)));
             nxt[c] = ring[c][(wn[c] & 15) * kRow];  // (re)read after the ring's refill
         }
         // branch-free steps: one LDS length lookup per chain and step; a chain that
@@ -2187,10 +2191,11 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             HZ_WALK_FENCE();
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const bool leaf = e[c] != 0u;
-                const bool adv = ok[c] & leaf, park = ok[c] & !leaf;
+                const bool adv = ok[c] & (e[c] != 0u), park = ok[c] ^ adv;
+                // lead-in marks (off < ms) land in the ring too; it is cleared when
+                // the walk reaches ms
                 const uint32_t rel = off[c] - ms[c];
-                const uint32_t bit = (adv & (off[c] >= ms[c])) ? (1u << (rel & 31)) : 0u;
+                const uint32_t bit = adv ? (1u << (rel & 31)) : 0u;
                 atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
                 const uint32_t L = adv ? e[c] : 0u;
                 off[c] += L;
@@ -2227,6 +2232,11 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
                 }
                 sh[c] = (uint32_t)(r < 0 ? r + 32 : r);
                 pk[c] = false;
+            }
+            if (!on[c] && off[c] >= ms[c]) {  // the lead-in is over: drop its marks
+#pragma unroll
+                for (uint32_t i = kMarkRow; i < kMarkRow + 16; ++i) ring[c][i * kRow] = 0u;
+                on[c] = true;
             }
             ld[c] = false;
             if (f[c] <= ((off[c] - 1) >> 7) + 3) {
@@ -2568,7 +2578,7 @@ static hipError_t scan_lut(const DecArgs& a, SyncArgs y, uint32_t lds, int ncu, 
 
 // Boundary bitmap by the long-chain walker.
 static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int ncu, hipStream_t s) {
-    hipError_t e = ensure_lds_limit((const void*)k_idx_walk, kLdsBytes);
+    hipError_t e = ensure_lds_limit((const void*)k_idx_walk, (int)kWalkLdsRingBytes);  // + the static table
     if (e != hipSuccess) return e;
     WalkArgs w;
     w.words = a.words; w.nwords = a.nwords; w.bit_adj = a.bit_adj;
@@ -2584,7 +2594,7 @@ static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int n
     const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
     uint64_t wgs = (threads_needed + kWalkWaves * 64 - 1) / (kWalkWaves * 64);
     wgs = wgs ? wgs : 1;
-    hipLaunchKernelGGL(k_idx_walk, dim3(wgs), dim3(kWalkWaves * 64), t.walk_lds_bytes + kWalkLdsRingBytes, s, w);
+    hipLaunchKernelGGL(k_idx_walk, dim3(wgs), dim3(kWalkWaves * 64), kWalkLdsRingBytes, s, w);
     return hipGetLastError();
 }
 
