@@ -60,26 +60,19 @@ constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-b
 constexpr int kDecLevelBits = HZ_DEC_LEVEL_BITS;  // bits per global subtable level
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
-// Index walker (k_idx_walk): per chain an LDS ring of 4 payload chunks (16 B)
-// and 4 mark chunks; kWalkChains chains per lane, kWalkWaves waves per CU,
+// Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
+// chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
 // beside a u8 code-length table of the top min(max_len, kWalkK) window bits.
-// Measured at 16 GiB Zipf (index build): 1 chain x 8 waves 38.4 ms; 1 x 6/10/12/13
-// waves 43.8/39.6/41.1/44.7; 2 chains x 4 waves 53.7; 3 x 3 78; 4 x 2 105 (more
-// chains per lane compile to worse code than more waves).
-#ifndef HZ_WALK_CHAINS
-#define HZ_WALK_CHAINS 1
-#endif
-#ifndef HZ_WALK_WAVES
-#define HZ_WALK_WAVES 10
-#endif
-#ifndef HZ_WALK_K
-#define HZ_WALK_K 16
-#endif
-constexpr int kWalkK = HZ_WALK_K;           // walker length table: 2^16 u8 in LDS
-constexpr int kWalkMaxLen = 22;             // escape table: 2^max_len u8 in global memory (<= 4 MiB)
-constexpr int kWalkChains = HZ_WALK_CHAINS;
-constexpr int kWalkWaves = HZ_WALK_WAVES;
-constexpr uint32_t kRingWords = 33;  // odd stride: the lanes' rings start in distinct banks
+// Measured at 16 GiB Zipf, index build (A/B runs, round 2): 10 waves with 4 mark
+// chunks 27.0 ms, 12 / 14 waves with 2 mark chunks 25.5 / 26.0 ms; 10 steps per
+// round 25.3 vs 8 steps 25.5 ms. With the earlier u32 LUT walker: 2 chains per
+// lane x 4 waves 53.7 vs 1 x 8 waves 38.4 ms.
+constexpr int kWalkK = 16;            // walker length table: 2^16 u8 in LDS
+constexpr int kWalkMaxLen = 22;       // escape table: 2^max_len u8 in global memory (<= 4 MiB)
+constexpr int kWalkChains = 1;
+constexpr int kWalkWaves = 12;
+constexpr uint32_t kWalkMarkChunks = 2;
+constexpr uint32_t kRingWords = 16 + 4 * kWalkMarkChunks + 1;  // odd stride: the lanes' rings start in distinct banks
 constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
 constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;
 static_assert((1u << kWalkK) + kWalkLdsRingBytes <= kLdsBytes, "walker LDS");

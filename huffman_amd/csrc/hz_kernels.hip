@@ -2007,10 +2007,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
 // when the lead-in resynchronised.
 // ---------------------------------------------------------------------------
-#ifndef HZ_WALK_STEPS
-#define HZ_WALK_STEPS 8
-#endif
-constexpr int kWalkSteps = HZ_WALK_STEPS;  // steps per round: ~92 bits consumed on Zipf, 128 refilled
+constexpr int kWalkSteps = 10;  // steps per round (8: 25.5 ms, 10: 25.3 ms, 12: slower)
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
@@ -2062,14 +2059,9 @@ HZ_DEV void ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
 // kWalkMarkGroup chunks: every lane touches a different stretch of the stream,
 // so 16-byte accesses spread over many rounds let L2 evict a line between them
 // (fetches ~10x the payload, writes ~3.5x the bitmap with single chunks).
-#ifndef HZ_WALK_GROUP
-#define HZ_WALK_GROUP 4
-#endif
-#ifndef HZ_WALK_MGROUP
-#define HZ_WALK_MGROUP 4
-#endif
-constexpr uint32_t kWalkGroup = HZ_WALK_GROUP;
-constexpr uint32_t kWalkMarkGroup = HZ_WALK_MGROUP;
+// Measured (u32 LUT walker): 1/1 chunks 41.7 ms, 4/4 38.7, 1/8 38.9, 8/8 41.7.
+constexpr uint32_t kWalkGroup = 4;
+constexpr uint32_t kWalkMarkGroup = 4;
 static_assert((kWalkGroup & (kWalkGroup - 1)) == 0 && kWalkGroup >= 1 && kWalkGroup <= 8, "walk group");
 static_assert((kWalkMarkGroup & (kWalkMarkGroup - 1)) == 0 && kWalkMarkGroup >= 1 && kWalkMarkGroup <= 8,
               "mark group");
@@ -2098,7 +2090,8 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     constexpr int C = kWalkChains;
     constexpr uint32_t kRow = 1;  // ring word stride
     constexpr uint32_t G = kWalkGroup, GM = kWalkMarkGroup;
-    constexpr uint32_t kMarkRow = 16;  // ring words 0..15 payload, 16..31 marks, 32 pad
+    constexpr uint32_t kMarkRow = 16;  // ring words 0..15 payload, then kWalkMarkChunks mark chunks, 1 pad
+    constexpr uint32_t kMW = 4 * kWalkMarkChunks;  // mark ring words
     const uint32_t k = (uint32_t)a.k;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = threadIdx.x >> 6;
@@ -2172,7 +2165,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         uint32_t lim[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            lim[c] = min(on[c] ? end[c] : ms[c], min(128 * f[c] - 96, ms[c] + 128 * (mcount[c] + 4)));
+            lim[c] = min(on[c] ? end[c] : ms[c], min(128 * f[c] - 96, ms[c] + 128 * (mcount[c] + kWalkMarkChunks)));
             nxt[c] = ring[c][(wn[c] & 15) * kRow];  // (re)read after the ring's refill
         }
         // branch-free steps: one LDS length lookup per chain and step; a chain that
@@ -2196,7 +2189,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
                 // the walk reaches ms
                 const uint32_t rel = off[c] - ms[c];
                 const uint32_t bit = adv ? (1u << (rel & 31)) : 0u;
-                atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, bit);  // the mark ring (a zero bit: no mark)
+                atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, bit);  // the mark ring (a zero bit: no mark)
                 const uint32_t L = adv ? e[c] : 0u;
                 off[c] += L;
                 const int32_t r = (int32_t)sh[c] - (int32_t)L;  // >= -32 (codes <= 32 bits)
@@ -2220,7 +2213,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             if (pk[c]) {
                 if (off[c] >= ms[c]) {
                     const uint32_t rel = off[c] - ms[c];
-                    atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & 15)) * kRow, 1u << (rel & 31));
+                    atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, 1u << (rel & 31));
                 }
                 const uint32_t L = g[c];
                 off[c] += L;
@@ -2235,7 +2228,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             }
             if (!on[c] && off[c] >= ms[c]) {  // the lead-in is over: drop its marks
 #pragma unroll
-                for (uint32_t i = kMarkRow; i < kMarkRow + 16; ++i) ring[c][i * kRow] = 0u;
+                for (uint32_t i = kMarkRow; i < kMarkRow + kMW; ++i) ring[c][i * kRow] = 0u;
                 on[c] = true;
             }
             ld[c] = false;
@@ -2250,7 +2243,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             // mark chunk mcount is done once the walk is past it
             fl[c] = mcount[c] < nmc[c] && off[c] >= ms[c] && off[c] - ms[c] >= 128 * (mcount[c] + 1);
             if (fl[c]) {
-                uint32_t* slot = ring[c] + (kMarkRow + 4 * (mcount[c] & 3)) * kRow;
+                uint32_t* slot = ring[c] + (kMarkRow + 4 * (mcount[c] & (kWalkMarkChunks - 1))) * kRow;
                 const uint4 m = make_uint4(slot[0], slot[kRow], slot[2 * kRow], slot[3 * kRow]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) slot[i * kRow] = 0u;
