@@ -307,6 +307,55 @@ def test_index_build_equals_pack_index(codec, kind, n):
     assert np.array_equal(a, b)
 
 
+def _shape_stream(name):
+    """Host streams whose codebooks take the index builder's different table
+    shapes: lengths <= 16 (walker, no escape table), 17..22 (walker with the
+    escape table), > 22 (segment walkers), equal lengths (DENSE decode mode)."""
+    rng = np.random.default_rng(17)
+    if name == "dense8":   # 256 symbols, every code 8 bits
+        return rng.integers(0, 16, size=(3 << 20) + 1, dtype=np.uint8)
+    if name == "short":    # ~600 symbols, geometric-ish weights: max length <= 16
+        sym = np.minimum(rng.geometric(0.01, size=(3 << 20) // 2), 599).astype(np.uint16)
+        return sym.view(np.uint8)
+    if name == "long24":   # weights 2^i: codes up to 24 bits (above the walker's 22)
+        counts = [1 << i for i in range(23)] + [1]
+        sym = np.repeat(np.arange(24, dtype=np.uint16) * 257, counts)
+        rng.shuffle(sym)
+        return sym.view(np.uint8)
+    if name == "mid20":    # Zipf-like over 4096 symbols: codes into the escape range
+        r = np.arange(1, 4097, dtype=np.float64)
+        p = r ** -1.3
+        p /= p.sum()
+        sym = rng.choice(4096, size=(6 << 20) // 2, p=p).astype(np.uint16) * 13
+        return sym.view(np.uint8)
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name", ["dense8", "short", "mid20", "long24"])
+def test_index_build_table_shapes(codec, name):
+    """hz_index_build == the index hz_pack wrote, for codebooks of every table
+    shape the index builder distinguishes (walker with and without escapes,
+    DENSE decode tables, the segment walkers past 22-bit codes)."""
+    import torch
+    from huffman_amd import index_bytes, codebook_arrays
+    host = _shape_stream(name)
+    x = torch.from_numpy(host).cuda()
+    n = x.numel()
+    plan, payload, index = codec.encode(x)
+    _, ln, _ = codebook_arrays(plan.cb)
+    mx = int(ln.max())
+    assert {"dense8": mx == 8, "short": mx <= 16, "mid20": 16 < mx <= 22, "long24": mx > 22}[name], mx
+    rebuilt = torch.full_like(index, -1)
+    codec.dev.index_build(payload.data_ptr(), payload.numel(), plan.start_bit, n // 2, rebuilt.data_ptr())
+    codec.sync()
+    nb = index_bytes(n // 2)
+    assert np.array_equal(index.cpu().numpy().view(np.uint8)[:nb], rebuilt.cpu().numpy().view(np.uint8)[:nb])
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(payload, n // 2, rebuilt, out)
+    codec.sync()
+    assert torch.equal(out[:n - (n & 1)], x[:n - (n & 1)])
+
+
 def test_pipeline_4gib_roundtrip_properties(codec):
     """Above the reference's 4 GiB int-index limit: u64 counts, round trip,
     total bits == sum(hist * len), index monotone."""
