@@ -559,17 +559,25 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
 }
 
 // Index walker tables (hz_kernels.hip k_idx_walk): a walk needs code LENGTHS
-// only. img: one byte per K-bit window, K = min(max_len, kWalkK): the length
-// of the code the window starts with, 0 when that code is longer than K.
-// esc (max_len > K): one byte per max_len-bit window, filled under the escape
-// prefixes. Windows no code starts (incomplete code spaces) read length 1, so
-// a walk past the stream's end keeps moving. Byte i of a table is byte i of
-// its u32 vector (little-endian).
-void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M) {
+// only. img: one nibble per K-bit window (window w in byte w / 2, the high
+// nibble for odd w), K = max(2, min(max_len, kWalkK, min_len + 14)): the length
+// of the code the window starts with, minus bias = min_len - 1; 0 when that code
+// is longer than K bits. esc (max_len > K): one byte per max_len-bit window, the
+// true length, filled under the escape prefixes. Windows no code starts
+// (incomplete code spaces) read min_len, so a walk past the stream's end keeps
+// moving. Byte i of a table is byte i of its u32 vector (little-endian).
+void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
+                    int& bias) {
     M = (int)cb->max_len;
-    K = std::min(M, kWalkK);
-    img.assign(std::max<size_t>((size_t)1 << K, 16) / 4, 0x01010101u);
+    const int lmin = (int)cb->min_len;
+    K = std::max(2, std::min(std::min(M, kWalkK), lmin + 14));
+    bias = lmin - 1;
+    img.assign(std::max<size_t>((size_t)1 << (K - 1), 16) / 4, 0x11111111u);
     uint8_t* t1 = reinterpret_cast<uint8_t*>(img.data());
+    auto put = [&](uint64_t w, uint32_t v) {
+        uint8_t& b = t1[w >> 1];
+        b = (w & 1) ? (uint8_t)((b & 0x0f) | (v << 4)) : (uint8_t)((b & 0xf0) | v);
+    };
     esc.clear();
     if (M > K) esc.assign(((size_t)1 << M) / 4, 0x01010101u);
     uint8_t* t2 = reinterpret_cast<uint8_t*>(esc.data());
@@ -578,9 +586,10 @@ void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vect
         if (!L) continue;
         const uint64_t c = cb->code[s];
         if (L <= K) {
-            memset(t1 + (c << (K - L)), L, (size_t)1 << (K - L));
+            const uint64_t w0 = c << (K - L), n = (uint64_t)1 << (K - L);
+            for (uint64_t w = w0; w < w0 + n; ++w) put(w, (uint32_t)(L - bias));
         } else {
-            t1[c >> (L - K)] = 0;
+            put(c >> (L - K), 0u);
             memset(t2 + (c << (M - L)), L, (size_t)1 << (M - L));
         }
     }

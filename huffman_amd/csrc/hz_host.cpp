@@ -32,7 +32,8 @@ std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
-void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M);
+void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
+                    int& bias);
 }  // namespace hz
 
 using namespace hz;
@@ -349,8 +350,8 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     // the index walker's length tables (FIXED16 streams have an arithmetic index)
     t.walk_lds_bytes = 0;
     if (mode != DEC_FIXED16 && cb->max_len >= 1 && cb->max_len <= kWalkMaxLen) {
-        build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m);
-        if (wimg.size() * 4 <= (1u << kWalkK)) {  // k_idx_walk's static table
+        build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m, t.walk_bias);
+        if (wimg.size() * 4 <= (1u << kWalkK) / 2) {  // k_idx_walk's static table
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
             if (wesc.empty()) wesc.push_back(0x01010101u);
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;

@@ -62,12 +62,12 @@ constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the L
 constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
-// beside a u8 code-length table of the top min(max_len, kWalkK) window bits.
+// beside a 4-bit code-length table of the top kWalkK window bits.
 // Measured at 16 GiB Zipf, index build (A/B runs, round 2): 10 waves with 4 mark
 // chunks 27.0 ms, 12 / 14 waves with 2 mark chunks 25.5 / 26.0 ms; 10 steps per
 // round 25.3 vs 8 steps 25.5 ms. With the earlier u32 LUT walker: 2 chains per
 // lane x 4 waves 53.7 vs 1 x 8 waves 38.4 ms.
-constexpr int kWalkK = 16;            // walker length table: 2^16 u8 in LDS
+constexpr int kWalkK = 17;            // walker length table: 2^17 4-bit lengths (64 KB) in LDS
 constexpr int kWalkMaxLen = 22;       // escape table: 2^max_len u8 in global memory (<= 4 MiB)
 constexpr int kWalkChains = 1;
 constexpr int kWalkWaves = 12;
@@ -75,7 +75,7 @@ constexpr uint32_t kWalkMarkChunks = 2;
 constexpr uint32_t kRingWords = 16 + 4 * kWalkMarkChunks + 1;  // odd stride: the lanes' rings start in distinct banks
 constexpr uint32_t kWalkWaveBytes = 64u * kWalkChains * kRingWords * 4u;
 constexpr uint32_t kWalkLdsRingBytes = kWalkWaves * kWalkWaveBytes;
-static_assert((1u << kWalkK) + kWalkLdsRingBytes <= kLdsBytes, "walker LDS");
+static_assert((1u << kWalkK) / 2 + kWalkLdsRingBytes <= kLdsBytes, "walker LDS");
 constexpr int kDecMinWaves = 8;  // DENSE only when this many staging slots fit
 
 // Per-wave LDS slot for one block's payload (u32 words), from the largest
@@ -111,10 +111,10 @@ struct Tables {
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
     uint64_t dec_l2_entries = 0;
-    uint32_t* d_walk_lds = nullptr; // index walker: u8 code length per walk_k-bit window (0 = longer code)
+    uint32_t* d_walk_lds = nullptr; // index walker: 4-bit code length - walk_bias per walk_k-bit window (0 = longer code)
     uint32_t walk_lds_bytes = 0;    // 0 = no walker tables (the segment walkers build the index)
     uint32_t* d_walk_esc = nullptr; // index walker: u8 code length per walk_m-bit window (walk_m > walk_k)
-    int walk_k = 0, walk_m = 0;
+    int walk_k = 0, walk_m = 0, walk_bias = 0;
 };
 
 // Count-pass length table layout: the high byte is XORed into the bank bits

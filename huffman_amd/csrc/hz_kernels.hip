@@ -2007,7 +2007,11 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
 // when the lead-in resynchronised.
 // ---------------------------------------------------------------------------
-constexpr int kWalkSteps = 10;  // steps per round (8: 25.5 ms, 10: 25.3 ms, 12: slower)
+#ifndef HZ_WALK_STEPS_AB
+constexpr int kWalkSteps = 10;
+#else
+constexpr int kWalkSteps = HZ_WALK_STEPS_AB;
+#endif  // steps per round (8: 25.5 ms, 10: 25.3 ms, 12: slower)
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
@@ -2016,9 +2020,9 @@ struct WalkArgs {
     uint32_t bit_adj;         // payload bit 0 = bit bit_adj of words
     uint64_t start;           // stream bit of the first symbol
     uint64_t nseg, spc, nchains;
-    const uint32_t* lds_img;  // u8 code length per k-bit window (0: longer than k bits)
+    const uint32_t* lds_img;  // 4-bit code length - bias per k-bit window (0: longer than k bits)
     uint32_t lds_words;
-    int k;
+    int k, bias;
     const uint8_t* esc;       // u8 code length per m-bit window (escapes only)
     int m;
     uint32_t* bmp;
@@ -2083,7 +2087,7 @@ HZ_DEV uint4 pick_group(const uint4 (&g)[G], uint32_t i) {
 __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     // the length table at LDS address 0 (a static array: its address folds into
     // the ds_read offset), the rings after it
-    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 8];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(wtab, a.lds_img, a.lds_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
@@ -2092,7 +2096,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
     constexpr uint32_t G = kWalkGroup, GM = kWalkMarkGroup;
     constexpr uint32_t kMarkRow = 16;  // ring words 0..15 payload, then kWalkMarkChunks mark chunks, 1 pad
     constexpr uint32_t kMW = 4 * kWalkMarkChunks;  // mark ring words
-    const uint32_t k = (uint32_t)a.k;
+    const uint32_t k = (uint32_t)a.k, bias = (uint32_t)a.bias;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = threadIdx.x >> 6;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
@@ -2179,18 +2183,19 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             for (int c = 0; c < C; ++c) {
                 ok[c] = !pk[c] & (off[c] < lim[c]);
                 W[c] = __builtin_amdgcn_alignbit(w0[c], w1[c], sh[c]);
-                e[c] = lds8[W[c] >> (32 - k)];
+                e[c] = lds8[W[c] >> (33 - k)];  // two windows per byte (k >= 2)
             }
             HZ_WALK_FENCE();
 #pragma unroll
             for (int c = 0; c < C; ++c) {
+                e[c] = __builtin_amdgcn_ubfe(e[c], (W[c] >> (30 - k)) & 4u, 4);  // the window's nibble
                 const bool adv = ok[c] & (e[c] != 0u), park = ok[c] ^ adv;
                 // lead-in marks (off < ms) land in the ring too; it is cleared when
                 // the walk reaches ms
                 const uint32_t rel = off[c] - ms[c];
                 const uint32_t bit = adv ? (1u << (rel & 31)) : 0u;
                 atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, bit);  // the mark ring (a zero bit: no mark)
-                const uint32_t L = adv ? e[c] : 0u;
+                const uint32_t L = adv ? e[c] + bias : 0u;
                 off[c] += L;
                 const int32_t r = (int32_t)sh[c] - (int32_t)L;  // >= -32 (codes <= 32 bits)
                 const bool cr = r < 0;                         // w0 used up: shift the words
@@ -2581,7 +2586,7 @@ static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int n
     w.spc = (y.nseg + target - 1) / target;
     w.nchains = (y.nseg + w.spc - 1) / w.spc;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
-    w.k = t.walk_k; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
+    w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
     w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0];
     // chains tid and tid + T of every thread
     const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
