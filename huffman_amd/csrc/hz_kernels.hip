@@ -2007,11 +2007,8 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
 // when the lead-in resynchronised.
 // ---------------------------------------------------------------------------
-#ifndef HZ_WALK_STEPS_AB
-constexpr int kWalkSteps = 10;
-#else
-constexpr int kWalkSteps = HZ_WALK_STEPS_AB;
-#endif  // steps per round (8: 25.5 ms, 10: 25.3 ms, 12: slower)
+// steps per round: u8 table 8: 25.5 ms, 10: 25.3 ms; 4-bit table 10/12/14: 24.7/24.4/24.6 ms
+constexpr int kWalkSteps = 12;
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
