@@ -2060,7 +2060,8 @@ HZ_DEV void ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
 // kWalkMarkGroup chunks: every lane touches a different stretch of the stream,
 // so 16-byte accesses spread over many rounds let L2 evict a line between them
 // (fetches ~10x the payload, writes ~3.5x the bitmap with single chunks).
-// Measured (u32 LUT walker): 1/1 chunks 41.7 ms, 4/4 38.7, 1/8 38.9, 8/8 41.7.
+// Measured (u32 LUT walker): 1/1 chunks 41.7 ms, 4/4 38.7, 1/8 38.9, 8/8 41.7; (4-bit walker)
+// 4/4 23.9-24.3 ms, 2/4 24.9, 8/4 24.9, 4/2 26.8, 4/8 24.1, 8/8 25.0.
 constexpr uint32_t kWalkGroup = 4;
 constexpr uint32_t kWalkMarkGroup = 4;
 static_assert((kWalkGroup & (kWalkGroup - 1)) == 0 && kWalkGroup >= 1 && kWalkGroup <= 8, "walk group");
