@@ -192,25 +192,23 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u) v[u] = nx[u];
             if (i + step < end) load(i + step, nx);
-            uint32_t old[kHistUnroll * 8];
+            // (i < end: every vector of the loop is whole; the half a symbol
+            // counts in is bit 0 of the symbol, its shift 16 * bit 0)
+            uint32_t old[kHistUnroll * 8], sh[kHistUnroll * 8];
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u) {
                 const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                const bool ok = i + (uint64_t)u * blockDim.x < end;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                    old[u * 8 + k] = atomicAdd(&lds[hist_word(s)], ok ? ((s & 1) ? 0x10000u : 1u) : 0u);
+                    sh[u * 8 + k] = (s << 4) & 16u;
+                    old[u * 8 + k] = atomicAdd(&lds[hist_word(s)], 1u << sh[u * 8 + k]);
                 }
             }
+            // a fix-up is due exactly when the incremented half was 0xffff
             bool any = false;
 #pragma unroll
-            for (int u = 0; u < kHistUnroll; ++u) {
-                const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    any |= hist_needs_fix((wd[k >> 1] >> (16 * (k & 1))) & 0xffffu, old[u * 8 + k]);
-            }
+            for (int k = 0; k < kHistUnroll * 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
             if (__builtin_expect(any, 0)) {
                 for (int u = 0; u < kHistUnroll; ++u) {
                     if (i + (uint64_t)u * blockDim.x >= end) continue;
