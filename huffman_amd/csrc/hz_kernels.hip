@@ -128,7 +128,6 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 // exactly through the value the LDS atomic returns (DESIGN.md "Histogram").
 // ===========================================================================
 constexpr int kHistThreads = 1024;
-constexpr int kHistUnroll = 1;
 
 // LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
 // their low bits (the first byte), which alone would pick the LDS bank: the
@@ -170,55 +169,42 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
     if (VEC) {
         const uint4* in4 = reinterpret_cast<const uint4*>(in);
         const uint64_t nvec = nsym / 8;
-        // the whole chip sweeps the input together (neighbouring 16 KiB pieces)
-        static_assert(kHistUnroll == 1, "sweep reads one vector per lane per step");
+        // the whole chip sweeps the input together (neighbouring 16 KiB pieces),
+        // one vector (8 symbols) per lane per step
         const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-        const uint64_t beg = (uint64_t)blockIdx.x * blockDim.x;
         const uint64_t end = nvec;
-        // software pipelined: the next iteration's loads are in flight while
-        // this one's LDS atomics run (loads and LDS ops use separate counters)
-        uint4 nx[kHistUnroll];
-        auto load = [&](uint64_t i0, uint4 (&v)[kHistUnroll]) {
+        // 8 LDS atomics; a fix-up is due exactly when the incremented half was
+        // 0xffff (the half a symbol counts in is its bit 0, the shift 16 * bit 0)
+        auto count8 = [&](const uint4& v) {
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+            uint32_t old[8], sh[8];
 #pragma unroll
-            for (int u = 0; u < kHistUnroll; ++u) {
-                const uint64_t j = i0 + (uint64_t)u * blockDim.x;
-                v[u] = j < end ? in4[j] : make_uint4(0, 0, 0, 0);
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                sh[k] = (s << 4) & 16u;
+                old[k] = atomicAdd(&lds[hist_word(s)], 1u << sh[k]);
             }
-        };
-        uint64_t i = beg + threadIdx.x;
-        if (i < end) load(i, nx);
-        for (; i < end; i += step) {
-            uint4 v[kHistUnroll];
-#pragma unroll
-            for (int u = 0; u < kHistUnroll; ++u) v[u] = nx[u];
-            if (i + step < end) load(i + step, nx);
-            // (i < end: every vector of the loop is whole; the half a symbol
-            // counts in is bit 0 of the symbol, its shift 16 * bit 0)
-            uint32_t old[kHistUnroll * 8], sh[kHistUnroll * 8];
-#pragma unroll
-            for (int u = 0; u < kHistUnroll; ++u) {
-                const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                    sh[u * 8 + k] = (s << 4) & 16u;
-                    old[u * 8 + k] = atomicAdd(&lds[hist_word(s)], 1u << sh[u * 8 + k]);
-                }
-            }
-            // a fix-up is due exactly when the incremented half was 0xffff
             bool any = false;
 #pragma unroll
-            for (int k = 0; k < kHistUnroll * 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
+            for (int k = 0; k < 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
             if (__builtin_expect(any, 0)) {
-                for (int u = 0; u < kHistUnroll; ++u) {
-                    if (i + (uint64_t)u * blockDim.x >= end) continue;
-                    const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                    for (int k = 0; k < 8; ++k) {
-                        const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                        if (hist_needs_fix(s, old[u * 8 + k])) hist_fix(lds, hist, s, old[u * 8 + k]);
-                    }
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                    if (hist_needs_fix(s, old[k])) hist_fix(lds, hist, s, old[k]);
                 }
             }
+        };
+        // software pipelined over two register buffers (no copies): the next
+        // vector's load is in flight while this one's LDS atomics run (loads
+        // and LDS ops use separate counters)
+        uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint4 va = i < end ? in4[i] : make_uint4(0, 0, 0, 0), vb;
+        for (; i < end; i += 2 * step) {
+            if (i + step < end) vb = in4[i + step];
+            count8(va);
+            if (i + step >= end) break;
+            if (i + 2 * step < end) va = in4[i + 2 * step];
+            count8(vb);
         }
         tail_begin = nvec * 8;
     }
