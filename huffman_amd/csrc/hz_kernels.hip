@@ -1993,6 +1993,9 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // ---------------------------------------------------------------------------
 // steps per round: u8 table 8: 25.5 ms, 10: 25.3 ms; 4-bit table 10/12/14: 24.7/24.4/24.6 ms
 constexpr int kWalkSteps = 12;
+// parked chains resume after each part of a round: 2 parts of 6 steps 23.6-23.9 ms, 1 part
+// 23.7-24.3, 2 x 8 23.4-23.9, 3 x 6 23.2-24.3, 3 x 4 24.8, 4 x 4 23.5-24.2 (A/B in one run)
+constexpr int kWalkHalves = 2;
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
@@ -2157,47 +2160,16 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         // branch-free steps: one LDS length lookup per chain and step; a chain that
         // cannot step only leaves off unchanged, a code longer than k bits parks the
         // chain for the rest of the round
+        // parked chains: one gather from the escape table for all of them, then
+        // the codeword is marked and stepped over (mid-round and at the round's end)
+        auto resolve = [&]() {
+            uint32_t g[C];
 #pragma unroll
-        for (int t = 0; t < kWalkSteps; ++t) {
-            uint32_t W[C], e[C];
-            bool ok[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                ok[c] = !pk[c] & (off[c] < lim[c]);
-                W[c] = __builtin_amdgcn_alignbit(w0[c], w1[c], sh[c]);
-                e[c] = lds8[W[c] >> (33 - k)];  // two windows per byte (k >= 2)
-            }
-            HZ_WALK_FENCE();
+            for (int c = 0; c < C; ++c)
+                if (pk[c]) g[c] = a.esc[pW[c] >> (32 - a.m)];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                e[c] = __builtin_amdgcn_ubfe(e[c], (W[c] >> (30 - k)) & 4u, 4);  // the window's nibble
-                const bool adv = ok[c] & (e[c] != 0u), park = ok[c] ^ adv;
-                // lead-in marks (off < ms) land in the ring too; it is cleared when
-                // the walk reaches ms
-                const uint32_t rel = off[c] - ms[c];
-                const uint32_t bit = adv ? (1u << (rel & 31)) : 0u;
-                atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, bit);  // the mark ring (a zero bit: no mark)
-                const uint32_t L = adv ? e[c] + bias : 0u;
-                off[c] += L;
-                const int32_t r = (int32_t)sh[c] - (int32_t)L;  // >= -32 (codes <= 32 bits)
-                const bool cr = r < 0;                         // w0 used up: shift the words
-                w0[c] = cr ? w1[c] : w0[c];
-                w1[c] = cr ? nxt[c] : w1[c];
-                sh[c] = (uint32_t)(cr ? r + 32 : r);
-                wn[c] += cr ? 1u : 0u;
-                nxt[c] = ring[c][(wn[c] & 15) * kRow];
-                pk[c] |= park;
-                pW[c] = park ? W[c] : pW[c];
-            }
-        }
-        uint32_t g[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            if (pk[c]) g[c] = a.esc[pW[c] >> (32 - a.m)];
-        bool fl[C], ld[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (pk[c]) {
+                if (!pk[c]) continue;
                 if (off[c] >= ms[c]) {
                     const uint32_t rel = off[c] - ms[c];
                     atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, 1u << (rel & 31));
@@ -2209,10 +2181,52 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
                     w0[c] = w1[c];
                     w1[c] = nxt[c];
                     ++wn[c];
+                    nxt[c] = ring[c][(wn[c] & 15) * kRow];
                 }
                 sh[c] = (uint32_t)(r < 0 ? r + 32 : r);
                 pk[c] = false;
             }
+        };
+#pragma unroll
+        for (int half = 0; half < kWalkHalves; ++half) {
+    #pragma unroll
+            for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
+                uint32_t W[C], e[C];
+                bool ok[C];
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    ok[c] = !pk[c] & (off[c] < lim[c]);
+                    W[c] = __builtin_amdgcn_alignbit(w0[c], w1[c], sh[c]);
+                    e[c] = lds8[W[c] >> (33 - k)];  // two windows per byte (k >= 2)
+                }
+                HZ_WALK_FENCE();
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    e[c] = __builtin_amdgcn_ubfe(e[c], (W[c] >> (30 - k)) & 4u, 4);  // the window's nibble
+                    const bool adv = ok[c] & (e[c] != 0u), park = ok[c] ^ adv;
+                    // lead-in marks (off < ms) land in the ring too; it is cleared when
+                    // the walk reaches ms
+                    const uint32_t rel = off[c] - ms[c];
+                    const uint32_t bit = adv ? (1u << (rel & 31)) : 0u;
+                    atomicOr(ring[c] + (kMarkRow + ((rel >> 5) & (kMW - 1))) * kRow, bit);  // the mark ring (a zero bit: no mark)
+                    const uint32_t L = adv ? e[c] + bias : 0u;
+                    off[c] += L;
+                    const int32_t r = (int32_t)sh[c] - (int32_t)L;  // >= -32 (codes <= 32 bits)
+                    const bool cr = r < 0;                         // w0 used up: shift the words
+                    w0[c] = cr ? w1[c] : w0[c];
+                    w1[c] = cr ? nxt[c] : w1[c];
+                    sh[c] = (uint32_t)(cr ? r + 32 : r);
+                    wn[c] += cr ? 1u : 0u;
+                    nxt[c] = ring[c][(wn[c] & 15) * kRow];
+                    pk[c] |= park;
+                    pW[c] = park ? W[c] : pW[c];
+                }
+            }
+            resolve();
+        }
+        bool fl[C], ld[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
             if (!on[c] && off[c] >= ms[c]) {  // the lead-in is over: drop its marks
 #pragma unroll
                 for (uint32_t i = kMarkRow; i < kMarkRow + kMW; ++i) ring[c][i * kRow] = 0u;
