@@ -2189,18 +2189,18 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         };
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
-    #pragma unroll
+#pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 uint32_t W[C], e[C];
                 bool ok[C];
-    #pragma unroll
+#pragma unroll
                 for (int c = 0; c < C; ++c) {
                     ok[c] = !pk[c] & (off[c] < lim[c]);
                     W[c] = __builtin_amdgcn_alignbit(w0[c], w1[c], sh[c]);
                     e[c] = lds8[W[c] >> (33 - k)];  // two windows per byte (k >= 2)
                 }
                 HZ_WALK_FENCE();
-    #pragma unroll
+#pragma unroll
                 for (int c = 0; c < C; ++c) {
                     e[c] = __builtin_amdgcn_ubfe(e[c], (W[c] >> (30 - k)) & 4u, 4);  // the window's nibble
                     const bool adv = ok[c] & (e[c] != 0u), park = ok[c] ^ adv;
