@@ -54,10 +54,7 @@ enum DecMode : int {
     DEC_FIXED16 = 2 // every code 16 bits: u16 symbol per code in LDS, positions are arithmetic
 };
 constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-bit codes
-#ifndef HZ_DEC_LEVEL_BITS
-#define HZ_DEC_LEVEL_BITS 9
-#endif
-constexpr int kDecLevelBits = HZ_DEC_LEVEL_BITS;  // bits per global subtable level
+constexpr int kDecLevelBits = 9;  // bits per global subtable level
 constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
 constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
