@@ -22,10 +22,11 @@ constexpr uint32_t kLdsBytes = 160u * 1024u;   // LDS per CU (gfx950)
 //   u64 start[nblocks + 1]      absolute start bit of every 2048-symbol block
 //                               (start[nblocks] = end of the stream)
 //   u64 max_bits                largest block (bits): sizes the decoder's LDS slots
-//   u16 sub[nblocks][256]       start bit of every 8-symbol chain relative to
-//                               start[b], mod 2^16 (a lane's four chains are
-//                               one u64); exact when block bits < 2^16,
-//                               otherwise recovered by a prefix over deltas.
+//   u16 sub[nblocks][256]       low 16 bits of the absolute start bit of every
+//                               8-symbol chain (a lane's four chains are one
+//                               u64); the decoder takes (sub - start[b]) mod 2^16,
+//                               exact when block bits < 2^16, otherwise recovered
+//                               by a prefix over deltas.
 __host__ __device__ inline uint64_t index_blocks(uint64_t nsym) { return (nsym + kBlockSyms - 1) / kBlockSyms; }
 __host__ __device__ inline uint64_t index_bytes(uint64_t nsym) {
     const uint64_t nb = index_blocks(nsym);

@@ -273,7 +273,7 @@ struct PackArgs {
     unsigned long long* blk;     // per block bit count (k_pack_count)
     const unsigned long long* blk_start;
     unsigned long long* index;   // block index start[] (optional, hz_internal.h)
-    unsigned long long* index_sub;  // block index sub[] (four u16 chain offsets per lane)
+    unsigned long long* index_sub;  // block index sub[] (four u16 chain start bits per lane, low 16 bits)
     uint32_t* err;
     uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
 };
@@ -675,7 +675,8 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     if (a.index) {  // block index (hz_internal.h): start bits + the lane's chain offsets
         uint64_t sub = 0;
 #pragma unroll
-        for (int c = 0; c < kChainsPerLane; ++c) sub |= (uint64_t)((ex_n + b.nc[c]) & 0xffffu) << (16 * c);
+        for (int c = 0; c < kChainsPerLane; ++c)
+            sub |= (uint64_t)(((uint32_t)bstart + ex_n + b.nc[c]) & 0xffffu) << (16 * c);
         a.index_sub[blk * kWave + lane] = sub;
         if (lane == 0) {
             a.index[blk] = bstart;
@@ -798,10 +799,11 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
             const uint32_t cnt = (uint32_t)(a.nsym - blk * kBlockSyms < (uint64_t)kBlockSyms ? a.nsym - blk * kBlockSyms
                                                                                         : (uint64_t)kBlockSyms);
             uint64_t sub = 0;
+            const uint32_t bs = (uint32_t)(start_bit + (uint64_t)blk * kBlockSyms * 16);
 #pragma unroll
             for (int c = 0; c < kChainsPerLane; ++c) {
                 const uint32_t at = kSPT * lane + kChainSyms * c;
-                sub |= (uint64_t)((16 * (at < cnt ? at : cnt)) & 0xffffu) << (16 * c);
+                sub |= (uint64_t)((bs + 16 * (at < cnt ? at : cnt)) & 0xffffu) << (16 * c);
             }
             a.index_sub[j] = sub;
             if (lane == 0) a.index[blk] = start_bit + (uint64_t)blk * kBlockSyms * 16;
@@ -990,7 +992,7 @@ struct DecArgs {
     uint64_t nsym;
     uint64_t nblocks;
     const unsigned long long* starts;  // block index (hz_internal.h)
-    const unsigned long long* subs;    // four u16 chain offsets per lane
+    const unsigned long long* subs;    // four u16 chain start bits per lane (low 16 bits)
     const uint32_t* lds_img;
     uint32_t lds_words;      // table words; the staging region follows
     uint32_t region_words;   // staging region per workgroup (slots sized in-kernel from max_bits)
@@ -1086,12 +1088,13 @@ HZ_DEV void dec_stage(const DecArgs& a, uint64_t b0, uint64_t b1, uint32_t npc_m
     }
 }
 
-// Chain start bits of the lane relative to the block start (index sub[]);
+// Chain start bits of the lane relative to the block start: index sub[] holds
+// the low 16 bits of each chain's stream bit, bs the block's start bit; the
 // offsets are mod 2^16, rebuilt from deltas when the block is that long.
-HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bits, int lane, uint32_t (&off)[kChainsPerLane]) {
+HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bs, uint64_t bits, int lane, uint32_t (&off)[kChainsPerLane]) {
     constexpr int C = kChainsPerLane;
 #pragma unroll
-    for (int c = 0; c < C; ++c) off[c] = (uint32_t)(sub >> (16 * c)) & 0xffffu;
+    for (int c = 0; c < C; ++c) off[c] = ((uint32_t)(sub >> (16 * c)) - (uint32_t)bs) & 0xffffu;
     if (bits >= 65536) {
         uint32_t pv = shfl_up_u32(off[C - 1], 1);
         if (lane == 0) pv = 0;
@@ -1144,7 +1147,7 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
         uint64_t w0;
         dec_stage<WIDE>(a, b0, b1, npc_max, stg0 + g * slot, lane, w0);
         uint32_t off[C1];
-        dec_chain_offsets(sub, b1 - b0, lane, off);
+        dec_chain_offsets(sub, b0 - a.bit_adj, b1 - b0, lane, off);
         const uint32_t base = (uint32_t)(b0 - (w0 << 5)) + (uint32_t)g * slot * 32u;
 #pragma unroll
         for (int c = 0; c < C1; ++c) pos[g * C1 + c] = base + off[c];
@@ -1412,7 +1415,7 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
         uint64_t w0;
         dec_stage_commit(a, mc, slot >> 2, stg, lane, sc, w0);
         uint32_t off[C];
-        dec_chain_offsets(mc.sub, mc.b1 - mc.b0, lane, off);
+        dec_chain_offsets(mc.sub, mc.b0, mc.b1 - mc.b0, lane, off);
         const uint32_t base = (uint32_t)(mc.b0 + a.bit_adj - (w0 << 5));
         uint32_t pos[C];
 #pragma unroll
@@ -1481,7 +1484,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             uint64_t w0;
             dec_stage_commit(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
             uint32_t off[kChainsPerLane];
-            dec_chain_offsets(mc[j].sub, mc[j].b1 - mc[j].b0, lane, off);
+            dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
             const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u;
 #pragma unroll
             for (int c = 0; c < kChainsPerLane; ++c) pos[j * kChainsPerLane + c] = base + off[c];
@@ -2357,7 +2360,7 @@ HZ_DEV uint32_t select_bit(uint32_t m, uint32_t r) {
 // holds words [8 t, 8 t + 8). A workgroup scan of popcounts numbers every
 // boundary from the tile's first (first[] of its first row). Boundary i < nsym
 // with i % 8 == 0 is a chain start (raw position, low 16 bits, staged in LDS
-// and stored as one contiguous run; k_sync_subs makes it block-relative),
+// and stored as one contiguous run, the form hz_pack writes),
 // i % 2048 == 0 also a block start; boundary nsym is the end of the stream.
 constexpr int kSelectThreads = 256;
 constexpr uint32_t kSelTileSegs = 16;
@@ -2457,31 +2460,29 @@ __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint
     }
 }
 
-// Chain positions relative to their block start (mod 2^16), chains past the
-// stream's end at the end, and the largest block. One thread per lane word
-// (four chains, one u64) of the index.
+// Chains past the stream's end (all in the last block) start at the end, and
+// the largest block's bits. The select already wrote every other chain's
+// start (low 16 bits of its stream bit, as hz_pack does).
 __global__ __launch_bounds__(256) void k_sync_subs(uint64_t nsym, uint64_t nblocks, unsigned long long* starts,
                                                    unsigned long long* sub64) {
-    const uint64_t nq = nblocks * kWave;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t end = starts[nblocks];
-    unsigned long long mx = 0;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
-        const uint64_t b = q / kWave;
-        const uint64_t bs = starts[b];
+    if (blockIdx.x == 0 && threadIdx.x < kWave) {
+        const uint64_t q = (nblocks - 1) * kWave + threadIdx.x;
         const uint64_t raw = sub64[q];
         uint64_t out = 0;
 #pragma unroll
         for (int t = 0; t < kChainsPerLane; ++t) {
             const uint64_t c = q * kChainsPerLane + t;
-            const uint64_t p = c * kChainSyms < nsym ? (raw >> (16 * t)) & 0xffffu : end;
-            out |= ((p - bs) & 0xffffu) << (16 * t);
+            const uint64_t p = c * kChainSyms < nsym ? (raw >> (16 * t)) & 0xffffu : end & 0xffffu;
+            out |= p << (16 * t);
         }
         sub64[q] = out;
-        if (q % kWave == 0) {
-            const unsigned long long bits = starts[b + 1] - bs;
-            mx = bits > mx ? bits : mx;
-        }
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long mx = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += stride) {
+        const unsigned long long bits = starts[b + 1] - starts[b];
+        mx = bits > mx ? bits : mx;
     }
     for (int m = 32; m >= 1; m >>= 1) {
         const uint32_t lo = shfl_xor_u32((uint32_t)mx, m), hi = shfl_xor_u32((uint32_t)(mx >> 32), m);
@@ -2540,8 +2541,8 @@ static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long*
         hipLaunchKernelGGL(k_sync_select, dim3(sg), dim3(kSelectThreads), 0, s, y, a.nsym, a.nblocks,
                            (const unsigned long long*)first, d_index, subs);
     }
-    uint64_t sw = (a.nblocks * kWave + 255) / 256;
-    sw = sw < (uint64_t)ncu * 8 ? (sw ? sw : 1) : (uint64_t)ncu * 8;
+    uint64_t sw = (a.nblocks + 255) / 256;
+    sw = sw < (uint64_t)ncu * 4 ? (sw ? sw : 1) : (uint64_t)ncu * 4;
     hipLaunchKernelGGL(k_sync_subs, dim3(sw), dim3(256), 0, s, a.nsym, a.nblocks, d_index,
                        d_index + index_sub_offset(a.nblocks));
     return hipGetLastError();
@@ -2607,7 +2608,8 @@ __global__ __launch_bounds__(256) void k_idx_fixed16(uint64_t start, uint64_t ns
 #pragma unroll
         for (int c = 0; c < kChainsPerLane; ++c) {
             const uint32_t at = kSPT * lane + kChainSyms * c;
-            v |= (uint64_t)((16 * (at < cnt ? at : cnt)) & 0xffffu) << (16 * c);
+            v |= (uint64_t)(((uint32_t)(start + blk * kBlockSyms * 16) + 16 * (at < cnt ? at : cnt)) & 0xffffu)
+                 << (16 * c);
         }
         sub[j] = v;
         if (lane == 0) index[blk] = start + blk * kBlockSyms * 16;

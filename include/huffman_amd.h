@@ -140,8 +140,9 @@ int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
  * (hz_index_bytes(nsym) bytes, 8-byte aligned): u64 start[nblocks + 1] -- the
  * absolute start bit of every hz_index_stride() = 2048-symbol block, then the
  * stream's end bit -- then u64 max_bits, the largest block in bits (sizes the
- * decoder's LDS slots), then u16 sub[nblocks][256]: the start bit of every
- * 8-symbol chain of the block relative to start[b], mod 2^16. The reference
+ * decoder's LDS slots), then u16 sub[nblocks][256]: the low 16 bits of the
+ * absolute start bit of every 8-symbol chain of the block (its offset from
+ * start[b] is (sub - start[b]) mod 2^16). The reference
  * has no index (its decoder is serial,
  * Decompressor.cu:259-291); this is the side band that makes decode parallel. */
 uint64_t hz_index_stride(void);
