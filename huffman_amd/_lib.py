@@ -86,6 +86,7 @@ PROTOTYPES = [
     ("hz_codebook_upload", _I, [_P, ctypes.POINTER(Codebook)]),
     ("hz_codebook_upload_encode", _I, [_P, ctypes.POINTER(Codebook)]),
     ("hz_codebook_upload_decode", _I, [_P, ctypes.POINTER(Codebook)]),
+    ("hz_index_format", _I, []),
     ("hz_index_stride", _U64, []),
     ("hz_index_bytes", _U64, [_U64]),
     ("hz_scratch_bytes", _U64, [_U64]),
@@ -126,7 +127,10 @@ def load():
         raise ImportError(f"{LIB_PATH} is missing: build it with `python huffman_amd/build.py` "
                           "(the HIP library is required; there is no fallback)")
     lib = ctypes.CDLL(LIB_PATH)
+    variant = "HZ_LIB_VARIANT" in os.environ  # an A/B build of older sources may lack newer entry points
     for name, res, args in PROTOTYPES:
+        if variant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

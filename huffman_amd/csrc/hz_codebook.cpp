@@ -412,7 +412,7 @@ inline uint32_t leaf(uint32_t L, uint32_t sym) { return kLeafBit | (L << 16) | s
 // longer ones are grouped by their next nb bits (counting sort) and each
 // group gets a subtable of its own, appended to l2, at most kDecLevelBits wide.
 static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t base, uint32_t nb, uint32_t D,
-                      const uint32_t* syms, size_t nsyms, std::vector<uint32_t>& l2) {
+                      const uint32_t* syms, size_t nsyms, std::vector<uint32_t>& l2, uint32_t lvl) {
     const uint32_t E = 1u << nb;
     std::vector<uint32_t> cnt(E + 1, 0u), maxd(E, 0u);
     size_t ndeep = 0;
@@ -450,12 +450,13 @@ static int fill_level(const hz_codebook* cb, std::vector<uint32_t>& tab, size_t 
     for (uint32_t q = 0; q < E; ++q) {
         if (cnt[q + 1] == cnt[q]) continue;
         if (tab[base + q]) return HZ_EFORMAT;
-        const uint32_t nb2 = std::min<uint32_t>(maxd[q], (uint32_t)kDecLevelBits);
+        const uint32_t nb2 = std::min<uint32_t>(maxd[q], lvl);
         const size_t off = l2.size();
-        if (off + (1ull << nb2) >= (1ull << 26)) return HZ_ENOMEM;
+        if (off + (1ull << nb2) > kLutMaxL2) return HZ_ENOMEM;
         l2.resize(off + (1ull << nb2), 0u);
-        tab[base + q] = (nb2 << 26) | (uint32_t)off;  // nb2 <= 8 (4 bits); bit 30 = LDS link  // (tab may alias l2: index, not pointer)
-        const int rc = fill_level(cb, l2, off, nb2, D + nb, order.data() + cnt[q], cnt[q + 1] - cnt[q], l2);
+        // (tab may alias l2: index, not pointer)
+        tab[base + q] = lut_link((uint32_t)off + kLutGlobal, nb2, D + nb);
+        const int rc = fill_level(cb, l2, off, nb2, D + nb, order.data() + cnt[q], cnt[q + 1] - cnt[q], l2, lvl);
         if (rc) return rc;
     }
     return HZ_OK;
@@ -476,7 +477,7 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
     for (uint32_t q = 0; q < img.size(); ++q) {
         const uint32_t e = img[q];
         if (e & kLeafBit) continue;
-        const uint32_t nb = (e >> 26) & 15u, off = e & 0x3ffffffu;
+        const uint32_t nb = (e >> 5) & 15u, off = (e >> 10) - kLutGlobal;
         std::vector<uint32_t> r(nb + 1, 0u);
         for (uint32_t t = 0; t < (1u << nb); ++t) {
             const uint32_t x = l2[off + t];
@@ -521,26 +522,32 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
             const uint32_t t0 = hd.off + (j << rest);
             const uint32_t x = l2[t0];
             const bool done = (x & kLeafBit) && ((x >> 16) & 63u) - (uint32_t)K1 <= hd.c;
-            img.push_back(done ? x : (rest ? ((rest << 26) | t0) : x));
+            img.push_back(done ? x : (rest ? lut_link(t0 + kLutGlobal, rest, (uint32_t)K1 + hd.c) : x));
         }
-        img[hd.q] = kDecLdsLink | (hd.c << 26) | o;
+        img[hd.q] = lut_link(o, hd.c, (uint32_t)K1);
     }
     while (img.size() & 3) img.push_back(leaf(1, 0));
 }
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global
 // memory.
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1) {
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl) {
     K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
-    img.assign(1u << K1, 0u);
-    l2.clear();
-    l2.reserve(1u << 19);
     std::vector<uint32_t> syms;
     syms.reserve(HZ_NSYM);
     for (uint32_t s = 0; s < HZ_NSYM; ++s)
         if (cb->len[s]) syms.push_back(s);
-    const int rc = fill_level(cb, img, 0, (uint32_t)K1, 0, syms.data(), syms.size(), l2);
+    // Global subtables of kDecLevelBits index bits; narrower (more levels, fewer entries) for a
+    // codebook whose global table would not fit the link's 21-bit raw field.
+    int rc = HZ_ENOMEM;
+    for (lvl = kDecLevelBits; lvl >= 4 && rc == HZ_ENOMEM; --lvl) {
+        img.assign(1u << K1, 0u);
+        l2.clear();
+        l2.reserve(1u << 19);
+        rc = fill_level(cb, img, 0, (uint32_t)K1, 0, syms.data(), syms.size(), l2, (uint32_t)lvl);
+    }
+    ++lvl;
     if (rc) return rc;
     // Unused windows (incomplete codes) decode as a 1-bit filler so a lane
     // that runs past its unit's end never stalls.

@@ -31,7 +31,7 @@ std::vector<uint32_t> build_len8(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl);
 void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
                     int& bias);
 }  // namespace hz
@@ -337,7 +337,7 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     std::vector<uint32_t> dimg, l2, wimg, wesc;
     if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
     else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
-    else rc = build_dec_lut(cb, dimg, l2, t.dec_k);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, t.dec_level_bits);
     if (rc) return rc;
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
@@ -372,6 +372,7 @@ extern "C" int hz_codebook_upload(hz_ctx* c, const hz_codebook* cb) {
     return rc ? rc : hz_codebook_upload_decode(c, cb);
 }
 
+extern "C" int hz_index_format(void) { return HZ_INDEX_FORMAT; }
 extern "C" uint64_t hz_index_stride(void) { return kBlockSyms; }
 extern "C" uint64_t hz_index_bytes(uint64_t nsym) { return index_bytes(nsym); }
 extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) { return pack_scratch_words(nsym) * sizeof(uint64_t); }

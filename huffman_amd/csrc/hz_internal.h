@@ -55,8 +55,19 @@ enum DecMode : int {
     DEC_FIXED16 = 2 // every code 16 bits: u16 symbol per code in LDS, positions are arithmetic
 };
 constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-bit codes
-constexpr int kDecLevelBits = 9;  // bits per global subtable level
-constexpr uint32_t kDecLdsLink = 1u << 30;  // LUT link entry: subtable in the LDS image (else global l2)
+constexpr int kDecLevelBits = 9;  // bits per global subtable level (fewer when the table would exceed kLutMaxL2)
+// LUT entries (DEC_LUT; hz_codebook.cpp build_dec_lut):
+//   leaf  1 << 31 | L << 16 | sym
+//   link  raw << 10 | nb << 5 | pos   (bit 31 clear). raw < kLutGlobal: the subtable starts at word raw of
+//         the LDS image; else at l2[raw - kLutGlobal]. nb (<= 15) index bits follow the D code bits
+//         already consumed; pos = 32 - D - nb (0 when D + nb > 32): the index is bits [pos, pos + nb) of
+//         a 32-bit window whose bit 31 is the code's first bit, one v_bfe_u32(W, e, e >> 5) -- no depth
+//         bookkeeping in the decoder's hot loop.
+constexpr uint32_t kLutGlobal = 65536;                      // > any LDS word index (160 KiB / 4)
+constexpr uint32_t kLutMaxL2 = (1u << 21) - kLutGlobal;     // global entries a 21-bit raw field reaches
+__host__ __device__ inline uint32_t lut_link(uint32_t raw, uint32_t nb, uint32_t D) {
+    return (raw << 10) | (nb << 5) | (D + nb <= 32 ? 32 - D - nb : 0u);
+}
 constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
@@ -96,6 +107,7 @@ struct Tables {
     int max_len = 0;
     int min_len = 0;
     int dec_k = 0;                 // DENSE window bits / LUT level-1 bits
+    int dec_level_bits = 0;        // LUT: widest global subtable (kDecLevelBits unless reduced to fit kLutMaxL2)
     int dec_max_len = 0;           // of the codebook the decode tables were built for
     int dec_min_len = 0;
     uint32_t enc_lds_bytes = 0;

@@ -19,6 +19,9 @@
 namespace hz {
 
 #define HZ_DEV __device__ __forceinline__
+#ifndef HZ_EXP_PACK
+#define HZ_EXP_PACK 0
+#endif
 
 // Dynamic-LDS limit of a kernel: hipFuncSetAttribute is per device, so the
 // (kernel, device) pairs already raised are remembered under a lock (any
@@ -369,6 +372,11 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         // of later loads and stores static. The escape table holds entries in
         // the register format, so each load lands in its e[k] directly.
         (void)any;
+#if HZ_EXP_PACK == 1
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) e[k] = (T)((uint32_t)e[k] & 0x7fffffffu);
+        xe = (T)(xx & 0x7fffffffu);
+#else
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const bool miss = (uint32_t)e[k] >> 31;
@@ -380,6 +388,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             const uint32_t v = a.esc[miss ? xs : 0u];
             xe = miss ? (T)v : xe;
         }
+#endif
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
@@ -999,10 +1008,28 @@ struct DecArgs {
     int k;
     int min_len;
     int max_len;
+    int level_bits;          // LUT: widest global subtable (Tables::dec_level_bits)
     const uint32_t* l2;
     uint8_t* out;
     uint32_t* err;
 };
+
+// LUT entries (hz_internal.h): a link's subtable index is the next nb window
+// bits; pos (bits [4:0]) places them in a 32-bit window, so a pipelined
+// decoder extracts them with one v_bfe_u32 and no depth bookkeeping.
+HZ_DEV bool lut_leaf(uint32_t e) { return (int32_t)e < 0; }
+HZ_DEV bool lut_lds_link(uint32_t e) { return e < (kLutGlobal << 10); }  // false for leaves (bit 31)
+HZ_DEV uint32_t lut_nb(uint32_t e) { return (e >> 5) & 15u; }
+// index (raw space: < kLutGlobal LDS, else global + kLutGlobal) of window W's entry under link e
+HZ_DEV uint32_t lut_next32(uint32_t e, uint32_t W) { return (e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5); }
+// entry at raw index i
+HZ_DEV uint32_t lut_at(const uint32_t* lds, const uint32_t* l2, uint32_t i) {
+    return i < kLutGlobal ? lds[i] : l2[i - kLutGlobal];
+}
+// l2 index of window W's entry under a global link e (one v_add3 after the bfe)
+HZ_DEV uint32_t lut_gnext32(uint32_t e, uint32_t W) {
+    return (e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5) - kLutGlobal;
+}
 
 template <int MODE>
 HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint32_t& sym, uint32_t& L) {
@@ -1017,10 +1044,9 @@ HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint
     } else {
         uint32_t e = lds[(uint32_t)(win >> (64 - a.k))];
         uint32_t D = (uint32_t)a.k;
-        while (!(e >> 31)) {  // link: bit 30 = subtable in the LDS image, else in l2
-            const uint32_t nb = (e >> 26) & 15u;
-            const uint32_t i = (e & 0x3ffffffu) + (uint32_t)((win << D) >> (64 - nb));
-            e = (e & kDecLdsLink) ? lds[i] : a.l2[i];
+        while (!lut_leaf(e)) {  // 64-bit windows: depth tracked here (pos covers 32-bit windows only)
+            const uint32_t nb = lut_nb(e);
+            e = lut_at(lds, a.l2, (e >> 10) + (uint32_t)((win << D) >> (64 - nb)));
             D += nb;
         }
         L = (e >> 16) & 63u;
@@ -1186,28 +1212,28 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
             for (int c = 0; c < C; ++c) { e[c] = lds[(uint32_t)(win[c] >> (WB - (uint32_t)a.k))]; D[c] = (uint32_t)a.k; }
 #pragma unroll
             for (int c = 0; c < C; ++c) {  // LDS-resident second level (hot subtables)
-                if ((e[c] >> 30) == 1u) {
-                    const uint32_t nb = (e[c] >> 26) & 15u;
-                    e[c] = lds[(e[c] & 0x3ffffffu) + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
+                if (lut_lds_link(e[c])) {
+                    const uint32_t nb = lut_nb(e[c]);
+                    e[c] = lds[(e[c] >> 10) + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
                     D[c] += nb;
                 }
             }
 #pragma unroll
             for (int c = 0; c < C; ++c) {  // first global level of every chain before one wait
                 e2[c] = e[c];
-                if (!(e[c] >> 31)) {
-                    const uint32_t nb = (e[c] >> 26) & 15u;
-                    e2[c] = a.l2[(e[c] & 0x3ffffffu) + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
+                if (!lut_leaf(e[c])) {
+                    const uint32_t nb = lut_nb(e[c]);
+                    e2[c] = a.l2[(e[c] >> 10) - kLutGlobal + (uint32_t)((Win)(win[c] << D[c]) >> (WB - nb))];
                 }
             }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 uint32_t ee = e2[c];
-                if (!(e[c] >> 31)) {
-                    uint32_t Dd = D[c] + ((e[c] >> 26) & 15u);
-                    while (!(ee >> 31)) {  // deeper global levels: rare
-                        const uint32_t nb = (ee >> 26) & 15u;
-                        ee = a.l2[(ee & 0x3ffffffu) + (uint32_t)((Win)(win[c] << Dd) >> (WB - nb))];
+                if (!lut_leaf(e[c])) {
+                    uint32_t Dd = D[c] + lut_nb(e[c]);
+                    while (!lut_leaf(ee)) {  // deeper global levels: rare
+                        const uint32_t nb = lut_nb(ee);
+                        ee = a.l2[(ee >> 10) - kLutGlobal + (uint32_t)((Win)(win[c] << Dd) >> (WB - nb))];
                         Dd += nb;
                     }
                 }
@@ -1231,7 +1257,7 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
 }
 
 // Two-level LUT decode of one block with the global lookups software
-// pipelined. Needs max_len <= k + kDecLevelBits (every global lookup ends in
+// pipelined. Needs max_len <= k + level bits (every global lookup ends in
 // a leaf) and max_len <= 32. The lane's chains are two halves, {0,1} and
 // {2,3}; a half's LDS step (window, level 1, LDS second level) issues its
 // global lookups unconditionally (lanes that do not need one read l2[0]:
@@ -1242,22 +1268,18 @@ struct PipeLane {
     uint32_t e, gi;
 };
 
+// One chain's LDS step: window, level 1, the LDS second level (hot heads).
+// r.gi: the l2 index of the global entry to read (0 -- one coalesced address
+// -- when the chain is resolved in LDS).
 HZ_DEV PipeLane dec_pipe_lds(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, uint32_t pos) {
     const uint32_t p1 = pos - 1u;  // >= 127 (staging pad)
     const uint32_t* w = stg + (p1 >> 5);
     const uint32_t W = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
     uint32_t e = lds[W >> (32 - a.k)];
-    uint32_t D = (uint32_t)a.k;
-    if ((e >> 30) == 1u) {  // LDS second level
-        const uint32_t nb = (e >> 26) & 15u;
-        e = lds[(e & 0x3ffffffu) + ((W << D) >> (32 - nb))];
-        D += nb;
-    }
-    const bool lk = !(e >> 31);
-    const uint32_t nb = (e >> 26) & 15u;
+    if (lut_lds_link(e)) e = lds[lut_next32(e, W)];
     PipeLane r;
     r.e = e;
-    r.gi = lk ? (e & 0x3ffffffu) + ((W << D) >> (32 - nb)) : 0u;
+    r.gi = lut_leaf(e) ? 0u : lut_gnext32(e, W);
     return r;
 }
 
@@ -1277,19 +1299,14 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
     const uint32_t Wb = __builtin_amdgcn_alignbit(b0, b1, 31u - pb);
     uint32_t ea = lds[Wa >> (32 - k)];
     uint32_t eb = lds[Wb >> (32 - k)];
-    const bool ha = (ea >> 30) == 1u, hb = (eb >> 30) == 1u;
-    const uint32_t na = (ea >> 26) & 15u, nb = (eb >> 26) & 15u;
-    const uint32_t ia = ha ? (ea & 0x3ffffffu) + ((Wa << k) >> (32 - na)) : 0u;
-    const uint32_t ib = hb ? (eb & 0x3ffffffu) + ((Wb << k) >> (32 - nb)) : 0u;
-    const uint32_t xa = lds[ia], xb = lds[ib];
-    const uint32_t Da = ha ? k + na : k, Db = hb ? k + nb : k;
+    const bool ha = lut_lds_link(ea), hb = lut_lds_link(eb);
+    const uint32_t xa = lds[ha ? lut_next32(ea, Wa) : 0u], xb = lds[hb ? lut_next32(eb, Wb) : 0u];
     ea = ha ? xa : ea;
     eb = hb ? xb : eb;
-    const uint32_t ga = (ea >> 26) & 15u, gb = (eb >> 26) & 15u;
     r0.e = ea;
     r1.e = eb;
-    r0.gi = (ea >> 31) ? 0u : (ea & 0x3ffffffu) + ((Wa << Da) >> (32 - ga));
-    r1.gi = (eb >> 31) ? 0u : (eb & 0x3ffffffu) + ((Wb << Db) >> (32 - gb));
+    r0.gi = lut_leaf(ea) ? 0u : lut_gnext32(ea, Wa);
+    r1.gi = lut_leaf(eb) ? 0u : lut_gnext32(eb, Wb);
 }
 
 // The LDS steps of NC chains at once (dec_pipe_lds2 generalised): all window
@@ -1299,37 +1316,52 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
 // together whatever the scheduler would do (the decoder is order-sensitive).
 #define HZ_WALK_FENCE() __builtin_amdgcn_sched_barrier(0)
 
+// LDS word at byte address `byte` of a kernel without static LDS (its dynamic
+// LDS starts at address 0): no base add per access.
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte); }
+
+// Global table l2 as a buffer whose byte 0 lies kLutGlobal words before l2[0]:
+// the byte offset of a global link's entry is (raw + index bits) * 4, one
+// v_add_lshl_u32, and a chain resolved in LDS reads offset 4 * kLutGlobal = l2[0].
+HZ_DEV __amdgpu_buffer_rsrc_t lut_l2_rsrc(const uint32_t* l2) {
+    return __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(l2) - 4ull * kLutGlobal), 0, 0xffffffffu, 0x00020000);
+}
+
+// The LDS steps of NC chains at once: all window reads, then all level-1
+// reads, then all LDS-second-level reads in flight together, so NC chain
+// steps cost three LDS round trips. p1[c] = the LDS bit address of chain c's
+// next bit, minus 1 (>= 127 bits into its staging slot); k_decode has no
+// static LDS, so the table and slots are addressed from LDS byte 0. r[c].e: the entry
+// after LDS; r[c].gi: byte offset of its global entry in lut_l2_rsrc.
 template <int NC>
-HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* stg, const uint32_t* pos,
-                          PipeLane* r) {
+HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* p1, PipeLane* r) {
     const uint32_t k = (uint32_t)a.k;
-    uint32_t W[NC], e[NC], x[NC], D[NC];
+    uint32_t W[NC], e[NC], x[NC];
     bool h[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        const uint32_t p1 = pos[c] - 1u;  // >= 127 (staging pad)
-        const uint32_t* w = stg + (p1 >> 5);
-        W[c] = __builtin_amdgcn_alignbit(w[0], w[1], 31u - p1);
+        const uint32_t wb = (p1[c] >> 3) & ~3u;
+        W[c] = __builtin_amdgcn_alignbit(lds_at(wb), lds_at(wb + 4), ~p1[c]);
     }
     HZ_WALK_FENCE();
 #pragma unroll
-    for (int c = 0; c < NC; ++c) e[c] = lds[W[c] >> (32 - k)];
+    for (int c = 0; c < NC; ++c) e[c] = lds_at((W[c] >> (32 - k)) << 2);
     HZ_WALK_FENCE();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        h[c] = (e[c] >> 30) == 1u;
-        const uint32_t nb = (e[c] >> 26) & 15u;
-        const uint32_t i = h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u;
-        D[c] = h[c] ? k + nb : k;
-        x[c] = lds[i];
+        h[c] = lut_lds_link(e[c]);
+        const uint32_t byte = ((e[c] >> 10) + __builtin_amdgcn_ubfe(W[c], e[c], e[c] >> 5)) << 2;
+        x[c] = lds_at(h[c] ? byte : 0u);
     }
     HZ_WALK_FENCE();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t ee = h[c] ? x[c] : e[c];
-        const uint32_t g = (ee >> 26) & 15u;
+        const uint32_t byte = ((ee >> 10) + __builtin_amdgcn_ubfe(W[c], ee, ee >> 5)) << 2;
         r[c].e = ee;
-        r[c].gi = (ee >> 31) ? 0u : (ee & 0x3ffffffu) + ((W[c] << D[c]) >> (32 - g));
+        r[c].gi = lut_leaf(ee) ? 4u * kLutGlobal : byte;
     }
 }
 
@@ -1404,6 +1436,7 @@ constexpr int kPfStep = 4;  // chain step at which the next block's staging load
 // loaded halfway through this block's steps, so no block waits on HBM.
 HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, uint32_t slot, uint64_t b,
                           uint64_t stride, int lane) {
+    const uint32_t* l2g = a.l2;
     constexpr int C = kChainsPerLane;
     static_assert(C == 4, "two halves of two chains");
     PipeMeta mc, mn, mn2;
@@ -1434,8 +1467,8 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
         };
         auto issue2 = [&](int c) {
             dec_pipe_lds2(a, lds, stg, pos[c], pos[c + 1], st[c], st[c + 1]);
-            g[c] = a.l2[st[c].gi];
-            g[c + 1] = a.l2[st[c + 1].gi];
+            g[c] = l2g[st[c].gi];
+            g[c + 1] = l2g[st[c + 1].gi];
         };
         issue2(0);
 #pragma unroll
@@ -1468,6 +1501,8 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
                            uint64_t stride, int lane) {
     constexpr int C = 2 * kChainsPerLane;
     static_assert(kChainsPerLane == 4, "four pairs of chains over two blocks");
+    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(a.l2);
+    const uint32_t stg_bit = (uint32_t)(stg - lds) * 32u - 1u;  // LDS bit address of the slots, minus 1
     PipeMeta mc[2], mn[2], mn2[2];
     uint4 sc[2][kStageUnroll], sn[2][kStageUnroll];
 #pragma unroll
@@ -1478,24 +1513,24 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
     for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mc[j], lane, sc[j]);
     for (; b < a.nblocks; b += stride) {
-        uint32_t pos[C];
+        uint32_t p1[C];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint64_t w0;
             dec_stage_commit(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
             uint32_t off[kChainsPerLane];
             dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
-            const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u;
+            const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u + stg_bit;
 #pragma unroll
-            for (int c = 0; c < kChainsPerLane; ++c) pos[j * kChainsPerLane + c] = base + off[c];
+            for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base + off[c];
         }
         __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
         uint32_t pk[2][kSPT / 2];
         PipeLane st[C];
         uint32_t g[C];
         auto finish = [&](int c, int q) {
-            const uint32_t ee = (st[c].e >> 31) ? st[c].e : g[c];
-            pos[c] += (ee >> 16) & 63u;
+            const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
+            p1[c] += (ee >> 16) & 63u;
             const uint32_t sym = ee & 0xffffu;
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
             if (q & 1) pk[c / kChainsPerLane][i] |= sym << 16;
@@ -1503,9 +1538,9 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
         auto issue4 = [&](int c) {
-            dec_pipe_ldsn<4>(a, lds, stg, pos + c, st + c);
+            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) g[c + t] = a.l2[st[c + t].gi];
+            for (int t = 0; t < 4; ++t) g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
         };
         issue4(0);
 #pragma unroll
@@ -1636,6 +1671,7 @@ static void fill_dec_args(DecArgs& a, const Tables& t, const uint8_t* d_payload,
     a.lds_img = t.d_dec_lds;
     a.lds_words = t.dec_lds_bytes / 4;
     a.k = t.dec_k;
+    a.level_bits = t.dec_level_bits;
     a.min_len = t.dec_min_len;
     a.max_len = t.dec_max_len;
     a.l2 = t.d_dec_l2;
@@ -1710,7 +1746,7 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     if (wide) return run_decode<DEC_LUT, true, 0>(a, pbits, ncu, s);
     // two levels suffice (no lookup chain past a global subtable): pipelined gathers
     static const int pipe_env = [] { const char* v = getenv("HZ_DEC_PIPE"); return v ? atoi(v) : 2; }();
-    if (pipe_env && t.dec_max_len <= t.dec_k + kDecLevelBits && a.nwords >= 4)
+    if (pipe_env && t.dec_max_len <= t.dec_k + t.dec_level_bits && a.nwords >= 4)
         return pipe_env == 1 ? run_decode<DEC_LUT, false, 1>(a, pbits, ncu, s)
                              : run_decode<DEC_LUT, false, 2>(a, pbits, ncu, s);
     return run_decode<DEC_LUT, false, 0>(a, pbits, ncu, s);
@@ -1884,7 +1920,7 @@ HZ_DEV void br_refill(BitReader& r, const A& a) {
 // Lengths of the codewords at two readers (top 32 bits of each window).
 HZ_DEV void lut_len2(const DecArgs& a, const uint32_t* lds, const BitReader (&r)[2], uint32_t (&L)[2]) {
     const uint32_t k = (uint32_t)a.k;
-    uint32_t W[2], e[2], x[2], D[2], gi[2];
+    uint32_t W[2], e[2], x[2], gi[2];
     bool h[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) W[c] = (uint32_t)(r[c].buf >> 32);
@@ -1892,17 +1928,13 @@ HZ_DEV void lut_len2(const DecArgs& a, const uint32_t* lds, const BitReader (&r)
     for (int c = 0; c < 2; ++c) e[c] = lds[W[c] >> (32 - k)];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        h[c] = (e[c] >> 30) == 1u;
-        const uint32_t nb = (e[c] >> 26) & 15u;
-        const uint32_t i = h[c] ? (e[c] & 0x3ffffffu) + ((W[c] << k) >> (32 - nb)) : 0u;
-        D[c] = h[c] ? k + nb : k;
-        x[c] = lds[i];
+        h[c] = lut_lds_link(e[c]);
+        x[c] = lds[h[c] ? lut_next32(e[c], W[c]) : 0u];
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         e[c] = h[c] ? x[c] : e[c];
-        const uint32_t g = (e[c] >> 26) & 15u;
-        gi[c] = (e[c] >> 31) ? 0u : (e[c] & 0x3ffffffu) + ((W[c] << D[c]) >> (32 - g));
+        gi[c] = lut_leaf(e[c]) ? 0u : lut_gnext32(e[c], W[c]);
     }
     const uint32_t g0 = a.l2[gi[0]], g1 = a.l2[gi[1]];
     L[0] = (((e[0] >> 31) ? e[0] : g0) >> 16) & 63u;
@@ -2465,6 +2497,7 @@ __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint
 // start (low 16 bits of its stream bit, as hz_pack does).
 __global__ __launch_bounds__(256) void k_sync_subs(uint64_t nsym, uint64_t nblocks, unsigned long long* starts,
                                                    unsigned long long* sub64) {
+    if (nblocks == 0) return;  // no block: nothing to fix (the launcher never sends one; a guard, not a path)
     const uint64_t end = starts[nblocks];
     if (blockIdx.x == 0 && threadIdx.x < kWave) {
         const uint64_t q = (nblocks - 1) * kWave + threadIdx.x;
@@ -2560,7 +2593,7 @@ static hipError_t scan_lut(const DecArgs& a, SyncArgs y, uint32_t lds, int ncu, 
     const uint64_t cap = (uint64_t)ncu * (lds ? (kLdsBytes / lds < 2 ? 1 : 2) : 2);
     wgs = wgs < cap ? (wgs ? wgs : 1) : cap;
     // two segments per lane where the pipelined decoder's table shape holds
-    const bool two = MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + kDecLevelBits;
+    const bool two = MODE == DEC_LUT && a.max_len <= 32 && a.max_len <= a.k + a.level_bits;
     if (two) {
         hipError_t e = ensure_lds_limit((const void*)k_sync_scan2, kLdsBytes);
         if (e != hipSuccess) return e;

@@ -22,6 +22,12 @@ import torch
 import torch.distributed as dist
 
 
+def _global(group, r):
+    """Global rank of rank `r` of `group`: torch.distributed's src/dst/peer
+    arguments are global ranks even when a group is passed."""
+    return r if group is None else dist.get_global_rank(group, r)
+
+
 def shard_range(n_total, world, rank):
     """Byte range of rank `rank`: equal, even-sized shards (the last takes the rest)."""
     per = (n_total // world) & ~1
@@ -48,7 +54,7 @@ def odd_last_byte(shard, n_total, group=None):
     if rank == world - 1:
         assert len(shard) % 2 == 1, "the last shard of an odd stream holds the odd byte"
         v[0] = int(shard[-1])
-    dist.broadcast(v, src=world - 1, group=group)
+    dist.broadcast(v, src=_global(group, world - 1), group=group)
     return int(v.item())
 
 
@@ -109,7 +115,7 @@ def gather_to(payload, nbytes_local, dst=0, group=None):
     pad[:nbytes_local] = payload[:nbytes_local]
     bufs = [torch.zeros(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if dist.get_rank(group) == dst \
         else None
-    dist.gather(pad, bufs, dst=dst, group=group)
+    dist.gather(pad, bufs, dst=_global(group, dst), group=group)
     if bufs is None:
         return None
     return [b[:int(s)].cpu().numpy() for b, s in zip(bufs, sizes)]
@@ -153,15 +159,16 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
     w0 = [int(v) for v in meta[:, 1]]
     total = max(4 * w + n for w, n in zip(w0, nb))
     head_n = [min(4, n) for n in nb]
+    gdst = _global(group, dst)
     if rank != dst:
         if via_host:
             if nb[rank] > 4:
-                dist.send(payload[4:nb[rank]].cpu(), dst, group=group)
-            dist.send(payload[:4].cpu(), dst, group=group)
+                dist.send(payload[4:nb[rank]].cpu(), gdst, group=group)
+            dist.send(payload[:4].cpu(), gdst, group=group)
         else:
-            ops = [dist.P2POp(dist.isend, payload[:4], dst, group=group)]
+            ops = [dist.P2POp(dist.isend, payload[:4], gdst, group=group)]
             for a, b in _chunks(4, nb[rank]):
-                ops.append(dist.P2POp(dist.isend, payload[a:b], dst, group=group))
+                ops.append(dist.P2POp(dist.isend, payload[a:b], gdst, group=group))
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
         return None, total
@@ -177,15 +184,15 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
         elif via_host:
             if body is not None:
                 tmp = torch.empty(body.numel(), dtype=torch.uint8)
-                dist.recv(tmp, r, group=group)
+                dist.recv(tmp, _global(group, r), group=group)
                 body.copy_(tmp)
             tmp = torch.empty(4, dtype=torch.uint8)
-            dist.recv(tmp, r, group=group)
+            dist.recv(tmp, _global(group, r), group=group)
             heads[r] = tmp
         else:
-            ops.append(dist.P2POp(dist.irecv, heads[r], r, group=group))
+            ops.append(dist.P2POp(dist.irecv, heads[r], _global(group, r), group=group))
             for a, b in _chunks(4, nb[r]):
-                ops.append(dist.P2POp(dist.irecv, out[4 * w0[r] + a:4 * w0[r] + b], r, group=group))
+                ops.append(dist.P2POp(dist.irecv, out[4 * w0[r] + a:4 * w0[r] + b], _global(group, r), group=group))
     if ops:
         for q in dist.batch_isend_irecv(ops):
             q.wait()

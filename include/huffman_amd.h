@@ -144,7 +144,20 @@ int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
  * absolute start bit of every 8-symbol chain of the block (its offset from
  * start[b] is (sub - start[b]) mod 2^16). The reference
  * has no index (its decoder is serial,
- * Decompressor.cu:259-291); this is the side band that makes decode parallel. */
+ * Decompressor.cu:259-291); this is the side band that makes decode parallel.
+ *
+ * Bits are counted from byte 0 of the d_payload pointer the index is used
+ * with. A caller that hands hz_decode a pointer D bytes before (after) the one
+ * the index was built for must rebase BOTH arrays together: add (subtract)
+ * 8*D to every start[] entry and 8*D mod 2^16 to every sub[] entry; max_bits
+ * is unchanged. Rebasing start[] alone decodes wrong data.
+ *
+ * hz_index_format() identifies this layout. Format 2 (this build) stores
+ * sub[] as absolute low bits; format 1 (builds before it) stored offsets
+ * from start[b]. An index kept across builds must be rebuilt (hz_index_build)
+ * when the formats differ. */
+#define HZ_INDEX_FORMAT 2
+int hz_index_format(void);
 uint64_t hz_index_stride(void);
 uint64_t hz_index_bytes(uint64_t nsym);
 uint64_t hz_scratch_bytes(uint64_t nsym);

@@ -337,6 +337,49 @@ int hzo_decode(const uint8_t *f, uint64_t flen, uint8_t *out, uint64_t cap, uint
     return rc;
 }
 
+/*
+ * Header alone (Decompressor.cu:65-103, read :69-71, :74-80, :90-96,
+ * readFileSize :243-255): entry i of the file -> order[i] = symbol,
+ * len[symbol] = L, code[symbol] = its L bits right aligned. info[6] = N, the
+ * payload's first byte and bit (MSB = 0), isOdd, lastByte, U. The checker of
+ * the product's header parsers (host and device). Returns 0 or -4 (malformed
+ * or truncated: L == 0 / > HZO_MAXLEN, a duplicate symbol, EOF in the header).
+ */
+int hzo_parse_header(const uint8_t *f, uint64_t flen, uint16_t *order, uint8_t *len, uint64_t *code,
+                     uint64_t *info)
+{
+    if (flen < 3) return -4;
+    uint32_t U = (uint32_t)f[0] | ((uint32_t)f[1] << 8);
+    int odd = f[2] != 0;
+    uint8_t last = 0;
+    uint64_t pre = 3;
+    if (odd) { if (flen < 4) return -4; last = f[3]; pre = 4; }
+    if (U == 0) U = (flen == pre + 8) ? 0 : 65536;
+    memset(len, 0, HZO_NSYM);
+    memset(code, 0, sizeof(uint64_t) * HZO_NSYM);
+    hzo_br r = {f, flen, pre * 8, 0};
+    for (uint32_t i = 0; i < U; ++i) {
+        uint32_t s = br_bits(&r, 16);
+        uint32_t L = br_bits(&r, 8);
+        if (r.eof || L == 0 || L > HZO_MAXLEN || len[s]) return -4;
+        uint64_t c = 0;
+        for (uint32_t b = 0; b < L; ++b) c = (c << 1) | br_bit(&r);
+        order[i] = (uint16_t)s;
+        len[s] = (uint8_t)L;
+        code[s] = c;
+    }
+    uint64_t n = 0;
+    for (int b = 0; b < 8; ++b) n |= (uint64_t)br_bits(&r, 8) << (8 * b);
+    if (r.eof) return -4;
+    info[0] = n;
+    info[1] = r.bit >> 3;
+    info[2] = r.bit & 7;
+    info[3] = (uint64_t)odd;
+    info[4] = last;
+    info[5] = U;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Synthetic inputs (this build's generator, not a reference function;      */
 /* DESIGN.md "Synthetic inputs"). byte i of the stream, i counted from 0:    */

@@ -30,6 +30,8 @@ def load():
     lib.hzo_decode.argtypes = [P, U64, P, U64, ctypes.POINTER(U64)]
     lib.hzo_decode.restype = ctypes.c_int
     lib.hzo_pack_range.argtypes = [P, U64, U64, P, P, U64, P]
+    lib.hzo_parse_header.argtypes = [P, U64, P, P, P, P]
+    lib.hzo_parse_header.restype = ctypes.c_int
     lib.hzo_encoded_bits.argtypes = [U64, ctypes.c_uint32, P, P, ctypes.POINTER(U64)]
     lib.hzo_encoded_bits.restype = U64
     lib.hzo_zipf_thresholds.argtypes = [ctypes.c_double, P]
@@ -127,6 +129,22 @@ def reference_header(n, last_byte, order, ln, code):
     if k < 0:
         raise RuntimeError(f"hzl_header {k}")
     return out[:k].tobytes(), pb.value, pend.value
+
+
+def parse_header(blob):
+    """Oracle header parse (Decompressor.cu:65-103): (order[:U], len, code,
+    [N, payload byte, payload bit, isOdd, lastByte, U]); raises ValueError on a
+    malformed or truncated header."""
+    a = as_u8(blob)
+    order = np.zeros(65536, dtype=np.uint16)
+    ln = np.zeros(65536, dtype=np.uint8)
+    code = np.zeros(65536, dtype=np.uint64)
+    info = np.zeros(6, dtype=np.uint64)
+    rc = load().hzo_parse_header(_p(a), a.size, _p(order), _p(ln), _p(code), _p(info))
+    if rc:
+        raise ValueError(f"hzo_parse_header: {rc}")
+    u = int(info[5])
+    return order[:u], ln, code, [int(v) for v in info]
 
 
 def pack_range(data, sym0, count, ln, code, bit0, nbytes):

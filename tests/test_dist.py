@@ -89,3 +89,56 @@ def test_shard_ranges_cover_and_align():
         assert rs[0][0] == 0 and rs[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
         assert all(b % 2 == 0 for b, _ in rs)
+
+
+def _subgroup_worker(rank, world, port, n_total, result_dir):
+    """Two 2-rank subgroups of a 4-rank job, {0, 2} and {1, 3}: each encodes the
+    whole (odd) stream sharded over its members. The members' group ranks differ
+    from their global ranks, so every src/dst/peer must be translated
+    (dist._global): the odd byte comes from global rank 2 (resp. 3), the stream
+    lands on global rank 0 (resp. 1)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import huffman_amd
+        from huffman_amd import dist as hd
+        groups = [dist.new_group([0, 2]), dist.new_group([1, 3])]
+        g = groups[rank % 2]
+        gr, gw = dist.get_rank(g), dist.get_world_size(g)
+        data = oracle_lib.generate(n_total, offset=0, kind=1, seed=13)
+        beg, end = hd.shard_range(n_total, gw, gr)
+        shard = data[beg:end]
+        hist_local = torch.from_numpy(oracle_lib.hist16(shard).astype(np.int64))
+        h = hd.global_histogram(hist_local, group=g).numpy().astype(np.uint64)
+        cb = huffman_amd.build_codebook(h)
+        hb = huffman_amd.header_bits(cb, n_total)
+        pbits = huffman_amd.payload_bits(cb, hist_local.numpy().astype(np.uint64))
+        off, totals = hd.shard_bit_offsets(pbits, torch.device("cpu"), group=g)
+        word0, start, words = hd.local_geometry(hb, off, pbits, gr == 0)
+        _, ln, code = huffman_amd.codebook_arrays(cb)
+        buf = oracle_lib.pack_range(shard, 0, shard.size // 2, ln, code, start, words * 4 + 8)
+        last = hd.odd_last_byte(shard, n_total, group=g)
+        header = None
+        if gr == 0:
+            header, _, pend = huffman_amd.write_header(cb, n_total, last)
+            buf[0] |= pend
+        nbytes = (start + pbits + 7) // 8
+        stream, total = hd.reassemble_on_device(torch.from_numpy(buf.copy()), nbytes, word0, dst=0, group=g)
+        shards = hd.gather_to(torch.from_numpy(buf), nbytes, dst=0, group=g)
+        if gr == 0:
+            word0s = [hd.local_geometry(hb, sum(totals[:k]), totals[k], k == 0)[0] for k in range(gw)]
+            payload = hd.reassemble(shards, word0s, sum(totals), hb)
+            ref = oracle_lib.encode(data)
+            ok = header + payload.tobytes() == ref and header + stream[:total].numpy().tobytes() == ref
+            with open(os.path.join(result_dir, f"g{rank % 2}.txt"), "w") as f:
+                f.write("ok" if ok else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_subgroups_use_global_ranks(tmp_path):
+    mp.start_processes(_subgroup_worker, args=(4, _free_port(), 200003, str(tmp_path)), nprocs=4, join=True,
+                       start_method="spawn")
+    for k in (0, 1):
+        assert (tmp_path / f"g{k}.txt").read_text() == "ok"

@@ -307,6 +307,34 @@ def test_index_build_equals_pack_index(codec, kind, n):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("shift", [5000, 12345, 8192 * 3 + 1])
+def test_index_rebased_with_moved_payload(codec, shift):
+    """Index format 2 (include/huffman_amd.h): a payload handed to hz_decode
+    `shift` bytes further into its buffer decodes with the index rebased -- start[]
+    and sub[] moved together by 8*shift bits (sub[] mod 2^16), max_bits kept.
+    The shifts are not multiples of 8 KiB, so sub[] changes."""
+    import torch
+    n = (8 << 20) + 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=11)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    nsym = n // 2
+    nb = (nsym + 2047) // 2048
+    moved = torch.zeros(payload.numel() + shift + 64, dtype=torch.uint8, device="cuda")
+    moved[shift:shift + payload.numel()] = payload
+    idx = index.cpu().numpy().copy()
+    starts = idx[:nb + 1].view(np.uint64)
+    starts += np.uint64(8 * shift)
+    sub = idx[nb + 2:].view(np.uint16)
+    sub += np.uint16((8 * shift) & 0xffff)
+    rebased = torch.from_numpy(idx).cuda()
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(moved, nsym, rebased, out)
+    codec.sync()
+    assert torch.equal(out[:n], x)
+
+
 def _shape_stream(name):
     """Host streams whose codebooks take the index builder's different table
     shapes: lengths <= 16 (walker, no escape table), 17..22 (walker with the

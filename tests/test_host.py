@@ -119,6 +119,7 @@ def test_header_parse_empty_conventions(built_lib):
 
 def test_index_geometry(built_lib):
     """Block index: u64 start[nblocks + 1] + u64 max_bits + u16 sub[nblocks][256] (include/huffman_amd.h)."""
+    assert built_lib.hz_index_format() == 2  # sub[] = absolute low 16 bits (include/huffman_amd.h)
     assert built_lib.hz_index_stride() == 2048
     assert built_lib.hz_index_bytes(0) == 0
     assert built_lib.hz_index_bytes(1) == 8 * 3 + 512

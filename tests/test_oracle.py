@@ -148,3 +148,29 @@ def test_generator_zipf_distribution():
     assert np.abs(counts - p).max() < 2e-3
     b = oracle_lib.generate(1 << 16, offset=12345, kind=1)
     assert np.array_equal(b[100:200], oracle_lib.generate(100, offset=12445, kind=1))
+
+
+def test_oracle_header_parse_pins():
+    """oracle_lib.parse_header (Decompressor.cu:65-103) on the golden files: the
+    entries follow the oracle codebook of the input's histogram ((count, symbol)
+    order for this encoder's files; any order for the reference baseline's), N and
+    the odd byte match the input, and the payload decodes from the parsed position."""
+    for name in ["romeo.txt", "synth_zipf_4099.bin", "synth_zipf_65537.bin", "synth_unif_65536.bin"]:
+        data = open(os.path.join(GOLD, name), "rb").read()
+        h = oracle_lib.hist16(data)
+        order, ln, code = oracle_lib.codebook(h)
+        for suffix in (".compressed", ".baseline.compressed"):
+            blob = open(os.path.join(GOLD, name + suffix), "rb").read()
+            porder, pln, pcode, info = oracle_lib.parse_header(blob)
+            assert info[0] == len(data) and info[3] == len(data) % 2 and info[5] == int((h > 0).sum())
+            if len(data) % 2:
+                assert info[4] == data[-1]
+            assert set(porder.tolist()) == set(np.nonzero(h)[0].tolist())
+            if suffix == ".compressed":
+                assert np.array_equal(porder, order) and np.array_equal(pln, ln)
+                assert np.array_equal(pcode[ln > 0], code[ln > 0])
+            bits = 8 * info[1] + info[2] + int(np.sum(h * pln.astype(np.uint64)))
+            assert (bits + 7) // 8 == len(blob)
+    for cut in (2, 5, 100):
+        with pytest.raises(ValueError):
+            oracle_lib.parse_header(open(os.path.join(GOLD, "romeo.txt.compressed"), "rb").read()[:cut])

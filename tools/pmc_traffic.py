@@ -8,14 +8,18 @@ command, one with --pmc FETCH_SIZE and one with --pmc WRITE_SIZE):
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB per dispatch. gfx950 correction
 (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE counts exactly half
-of the bytes of wide (16 B per lane) coalesced streaming reads, which is what
-every kernel of this path issues (hist16 and pack_count: 16-B vector loads;
-decode: 64-B chunk loads as dwordx4), so fetch bytes = 2 x FETCH_SIZE x 1024.
-WRITE_SIZE is exact for 16-B-per-lane streaming stores (decode output bursts,
-pack output words are 4-B stores and are reported as counted). The stage
+of the bytes of wide (16 B per lane) streaming reads. Our own calibration
+(tools/microbench/mb_pmc_calib.hip, profiles/r01_pmc_calibration.json) shows
+exactly 0.5x for three shapes: coalesced 16-B loads, 64 contiguous bytes per
+lane, 64-byte chunks. The doubling is applied PER KERNEL, only to the kernels
+whose HBM reads are those shapes (WIDE_READ below); the others (scan kernels,
+the index builder's fix-up / select / subs passes, whose reads are 4- or 8-B
+accesses of an uncalibrated shape) are reported as counted, and each stage
+entry lists which kernels were corrected. WRITE_SIZE is exact for 16-B-per-lane
+streaming stores and 4-B stores (calibrated) and is never corrected. The stage
 figures are summed over the kernels of a stage and divided by the number of
-launches of the stage's marker kernel (k_hist16 / k_pack_write or k_pack_fixed16 / k_decode or
-k_decode_fixed16), so they are per launch of the stage like bench.py's `achieved`.
+launches of the stage's marker kernel, so they are per launch of the stage
+like bench.py's `achieved`.
 """
 import argparse
 import csv
@@ -35,6 +39,11 @@ STAGES = {
 }
 
 
+# kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
+WIDE_READ = ("k_hist16", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16", "k_decode",
+             "k_decode_fixed16", "k_idx_walk")
+
+
 def _is(name, k):
     return k + "<" in name or k + "(" in name
 
@@ -47,8 +56,11 @@ def stage_of(name):
 
 
 def read_counter(d, counter):
+    """Per stage: (corrected bytes, raw bytes, corrected kernel names), launches."""
     path = os.path.join(d, "run_counter_collection.csv")
     per = defaultdict(float)
+    raw = defaultdict(float)
+    fixed = defaultdict(set)
     calls = defaultdict(set)
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -57,10 +69,15 @@ def read_counter(d, counter):
             st = stage_of(row["Kernel_Name"])
             if st is None:
                 continue
-            per[st] += float(row["Counter_Value"]) * 1024.0
+            v = float(row["Counter_Value"]) * 1024.0
+            wide = counter == "FETCH_SIZE" and any(_is(row["Kernel_Name"], k) for k in WIDE_READ)
+            per[st] += 2.0 * v if wide else v
+            raw[st] += v
+            if wide:
+                fixed[st].update(k for k in WIDE_READ if _is(row["Kernel_Name"], k))
             if any(_is(row["Kernel_Name"], k) for k in STAGES[st][1]):
                 calls[st].add(row["Dispatch_Id"])
-    return per, {k: len(v) for k, v in calls.items()}
+    return per, raw, fixed, {k: len(v) for k, v in calls.items()}
 
 
 def main():
@@ -71,8 +88,8 @@ def main():
     ap.add_argument("--size", type=int, required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fetch, fcalls = read_counter(a.fetch, "FETCH_SIZE")
-    write, wcalls = read_counter(a.write, "WRITE_SIZE")
+    fetch, fraw, ffixed, fcalls = read_counter(a.fetch, "FETCH_SIZE")
+    write, _, _, wcalls = read_counter(a.write, "WRITE_SIZE")
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     try:
@@ -84,7 +101,7 @@ def main():
         if st not in fetch or st not in write:
             continue
         nf, nw = max(fcalls.get(st, 0), 1), max(wcalls.get(st, 0), 1)
-        f = 2.0 * fetch[st] / nf
+        f = fetch[st] / nf
         w = write[st] / nw
         ent[st] = {
             "size": a.size,
@@ -92,7 +109,10 @@ def main():
             "write_bytes_per_launch": round(w),
             "hbm_bytes_per_launch": round(f + w),
             "dispatches": {"fetch_pass": fcalls.get(st, 0), "write_pass": wcalls.get(st, 0)},
-            "correction": "fetch = 2 x FETCH_SIZE (gfx950 wide-read undercount); write = WRITE_SIZE",
+            "fetch_size_raw_bytes_per_launch": round(fraw[st] / nf),
+            "correction": "fetch = 2 x FETCH_SIZE for the kernels in fetch_doubled (gfx950 wide-read "
+                          "undercount, calibrated shapes), FETCH_SIZE as counted for the rest; write = WRITE_SIZE",
+            "fetch_doubled": sorted(ffixed[st]),
             "build_id": bid,
         }
     res[a.dist] = ent
