@@ -167,7 +167,7 @@ def reassemble(codec, plan, payload, rank, world, n_total, kind, args, dev):
     if rank == 0:
         res = {"ms": round(ms, 3), "stream_bytes": int(total), "GBps_into_rank0": round(total / ms / 1e6, 1),
                "transport": "gloo via host (rehearsal)" if args.rehearse else "RCCL isend/irecv"}
-        if n_total <= (8 << 30):
+        if n_total <= (9 << 30):  # the 8-rank rehearsal's 8 GiB stream (tests/test_gpu_dist.py); not 8 x 16 GiB
             nsym = n_total // 2
             idx = torch.empty((index_bytes(nsym) + 7) // 8 + 1, dtype=torch.int64, device=dev)
             codec.dev.index_build(stream.data_ptr(), stream.numel(), plan.header_bits % 8, nsym, idx.data_ptr())

@@ -161,9 +161,9 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
     head_n = [min(4, n) for n in nb]
     gdst = _global(group, dst)
     if rank != dst:
-        if via_host:
-            if nb[rank] > 4:
-                dist.send(payload[4:nb[rank]].cpu(), gdst, group=group)
+        if via_host:  # the same messages as the RCCL path, through host copies
+            for a, b in _chunks(4, nb[rank]):
+                dist.send(payload[a:b].cpu(), gdst, group=group)
             dist.send(payload[:4].cpu(), gdst, group=group)
         else:
             ops = [dist.P2POp(dist.isend, payload[:4], gdst, group=group)]
@@ -182,10 +182,10 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
             if body is not None:
                 body.copy_(payload[4:nb[r]])
         elif via_host:
-            if body is not None:
-                tmp = torch.empty(body.numel(), dtype=torch.uint8)
+            for a, b in _chunks(4, nb[r]):
+                tmp = torch.empty(b - a, dtype=torch.uint8)
                 dist.recv(tmp, _global(group, r), group=group)
-                body.copy_(tmp)
+                out[4 * w0[r] + a:4 * w0[r] + b].copy_(tmp)
             tmp = torch.empty(4, dtype=torch.uint8)
             dist.recv(tmp, _global(group, r), group=group)
             heads[r] = tmp

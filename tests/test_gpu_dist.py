@@ -77,7 +77,13 @@ def _worker(rank, world, port, n_total, kind, result_dir):
         flags = torch.tensor([0 if local_ok else 1], dtype=torch.int64)
         dist.all_reduce(flags)
         if rank == 0:
-            data = oracle_lib.generate(n_total, offset=0, kind=kind, seed=42)
+            if n_total > (64 << 20):  # the device generator (== oracle_lib.generate, test_gpu.py) is faster
+                g = torch.empty(n_total, dtype=torch.uint8, device=dev)
+                codec.dev.generate(g.data_ptr(), n_total, offset=0, kind=kind, alpha=1.1, seed=42)
+                data = g.cpu().numpy()
+                del g
+            else:
+                data = oracle_lib.generate(n_total, offset=0, kind=kind, seed=42)
             ref = oracle_lib.encode(data)
             blob = plan.header + stream[:total].cpu().numpy().tobytes()
             checks = {
@@ -96,7 +102,9 @@ def _worker(rank, world, port, n_total, kind, result_dir):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world,n_total,kind", [(8, 8 * (1 << 20) + 4097, 1), (8, 8 * (256 << 10) + 2, 0),
-                                                (3, (3 << 20) + 1, 1)])
+                                                (3, (3 << 20) + 1, 1),
+                                                # real shard sizes: 4 x 256 MiB, the last shard odd (256 MiB + 3)
+                                                (4, 4 * (256 << 20) + 3, 1)])
 def test_sharded_rehearsal_equals_single_stream(tmp_path, world, n_total, kind):
     mp.start_processes(_worker, args=(world, _free_port(), n_total, kind, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
@@ -121,3 +129,31 @@ def test_bench_rehearsal_three_ranks(tmp_path):
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 3 and line["roundtrip_bit_exact"]
     assert line["reassembly_outside_step"]["whole_stream_decoded_bit_exact"]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dist_kind", ["uniform", "zipf"])
+def test_bench_rehearsal_eight_ranks_1gib_shards(tmp_path, dist_kind):
+    """The 128 GiB config's geometry at real shard sizes: bench.py's N = 8 step with
+    1 GiB + 64 B per rank (an 8 GiB stream), every rank on cuda:0. Uniform shards pack to
+    just over 1 GiB of payload each, so the reassembly's messages cross
+    huffman_amd/dist.py _P2P_CHUNK (1 GiB); the reassembled 8 GiB stream is then
+    decoded whole on rank 0 (index rebuilt from the stream alone) and compared with
+    the generator's bytes."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "8", "--rehearse", "--size", str((1 << 30) + 64), "--dist", dist_kind, "--steps", "1", "--warmup", "0",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=840)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["roundtrip_bit_exact"]
+    re = line["reassembly_outside_step"]
+    assert re["whole_stream_decoded_bit_exact"]
+    if dist_kind == "uniform":
+        assert line["config"]["payload_bytes_rank0"] > (1 << 30) + 4  # a shard body spans two messages
