@@ -7,13 +7,17 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <iostream>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "huffman_amd.h"
@@ -705,14 +709,74 @@ int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
     return ok ? HZ_OK : HZ_EIO;
 }
 
-int write_exact(FILE* fp, const uint8_t* p, uint64_t n) {
-    if (n == 0) return HZ_OK;
-    const auto t0 = Clock::now();
-    const bool ok = fwrite(p, 1, n, fp) == n;
-    g_timing.fwrite_ms += ms_since(t0);
-    g_timing.bytes_out += ok ? n : 0;
-    return ok ? HZ_OK : HZ_EIO;
-}
+// Output file written by background positional writes, so a chunk's write
+// overlaps the next chunk's device work. One thread's write into the page
+// cache moves ~5 GB/s on the MI355X host; 8 threads with pwrite measured the
+// same and 8 threads copying into a shared mmap 1.7 GB/s (tools/debug/write_bw.py):
+// that rate bounds extract's wall time. start() hands a buffer to kWriters
+// threads (one slice each) and returns; wait() joins them. One write is in
+// flight at a time, so the caller double-buffers.
+class FileWriter {
+  public:
+    ~FileWriter() {
+        (void)wait();
+        if (fd_ >= 0) ::close(fd_);
+    }
+    int open(const char* path) {
+        fd_ = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        return fd_ >= 0 ? HZ_OK : HZ_EIO;
+    }
+    void start(const uint8_t* p, uint64_t n, uint64_t off) {
+        if (n == 0) return;
+        t0_ = Clock::now();
+        const uint64_t nt = n < (8u << 20) ? 1 : kWriters;
+        const uint64_t piece = ((n + nt - 1) / nt + 4095) & ~(uint64_t)4095;
+        for (uint64_t a = 0; a < n; a += piece) {
+            const uint64_t len = std::min(piece, n - a);
+            th_.emplace_back([this, p, a, len, off] {
+                uint64_t done = 0;
+                while (done < len) {
+                    const ssize_t w = ::pwrite(fd_, p + a + done, len - done, (off_t)(off + a + done));
+                    if (w <= 0) { err_ = true; return; }
+                    done += (uint64_t)w;
+                }
+            });
+        }
+        g_timing.bytes_out += n;
+    }
+    int wait() {
+        if (th_.empty()) return err_ ? HZ_EIO : HZ_OK;
+        for (auto& t : th_) t.join();
+        th_.clear();
+        g_timing.fwrite_ms += ms_since(t0_);
+        return err_ ? HZ_EIO : HZ_OK;
+    }
+    int write_now(const uint8_t* p, uint64_t n, uint64_t off) {
+        int rc = wait();
+        if (rc) return rc;
+        start(p, n, off);
+        return wait();
+    }
+    int close() {
+        int rc = wait();
+        if (fd_ >= 0 && ::close(fd_) != 0) rc = HZ_EIO;
+        fd_ = -1;
+        return rc;
+    }
+  private:
+    static constexpr uint64_t kWriters = 1;  // 8 writers measured the same (the file's inode lock serialises them)
+    int fd_ = -1;
+    std::vector<std::thread> th_;
+    std::atomic<bool> err_{false};
+    Clock::time_point t0_;
+};
+
+// Declared after the host buffers a FileWriter reads: an early return waits
+// for the writes in flight before those buffers are freed.
+struct WriterDrain {
+    FileWriter& w;
+    ~WriterDrain() { (void)w.wait(); }
+};
 
 struct StreamGuard {
     hipStream_t s = nullptr;
@@ -753,7 +817,11 @@ extern "C" int hz_stream_last_timing(hz_stream_timing* t) {
     return HZ_OK;
 }
 
-static int hz_archive_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+// resident: keep the input on the device after pass 1 when the file fits
+// (hz_archive_file; Compressor.cu:324-367 reads the file once into pinned
+// memory), so pass 2 packs it in one launch without reading the file again.
+static int hz_archive_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose,
+                                  bool resident) {
     if (!in_path || !out_path || chunk_bytes < 64) return HZ_EINVAL;
     chunk_bytes &= ~(uint64_t)15;  // even (whole symbols) and 16-byte aligned device reads
     struct stat st;
@@ -768,11 +836,18 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     Spans spans;
     const uint64_t chunk = std::min<uint64_t>(chunk_bytes, std::max<uint64_t>(n, 16));
     PinnedBuf hin[2];
-    DevBuf din[2], dhist;
+    DevBuf din[2], dhist, dall;
     const auto ta = Clock::now();
+    if (resident && n > chunk) {
+        // the whole input plus a payload of the same size must fit in free device memory
+        size_t fr = 0, tot = 0;
+        resident = hipMemGetInfo(&fr, &tot) == hipSuccess && 2 * n + (1ull << 30) <= fr && dall.alloc(n + 16) == HZ_OK;
+    } else {
+        resident = false;
+    }
     for (int i = 0; i < 2; ++i) {
         if ((rc = hin[i].alloc(chunk))) return rc;
-        if ((rc = din[i].alloc(chunk + 16))) return rc;
+        if (!resident && (rc = din[i].alloc(chunk + 16))) return rc;
     }
     if ((rc = dhist.alloc(HZ_NSYM * 8))) return rc;
     g_timing.alloc_ms += ms_since(ta);
@@ -781,7 +856,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     FILE* fp = fopen(in_path, "rb");
     if (!fp) return HZ_EIO;
     std::unique_ptr<FILE, int (*)(FILE*)> fin(fp, fclose);
-    // ---- pass 1: histogram
+    // ---- pass 1: histogram (resident: the chunks stay in dall)
     HZ_TRY(hipMemsetAsync(dhist.p, 0, HZ_NSYM * 8, c->stream));
     EventPair done;
     if ((rc = done.create())) return rc;
@@ -792,11 +867,12 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         spans.fold();
         if ((rc = read_exact(fp, hin[b].p, len))) return rc;
         if (off + len == n && (n & 1)) last_byte = hin[b].p[len - 1];
+        uint8_t* dst = resident ? (uint8_t*)dall.p + off : (uint8_t*)din[b].p;
         hipEvent_t t0 = spans.mark(c->stream);
-        HZ_TRY(hipMemcpyAsync(din[b].p, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
+        HZ_TRY(hipMemcpyAsync(dst, hin[b].p, len, hipMemcpyHostToDevice, c->stream));
         spans.add(t0, spans.mark(c->stream), &g_timing.h2d_ms);
         hipEvent_t t1 = spans.mark(c->stream);
-        if ((rc = hz_hist16(c, (const uint8_t*)din[b].p, len, (uint64_t*)dhist.p, 1))) return rc;
+        if ((rc = hz_hist16(c, dst, len, (uint64_t*)dhist.p, 1))) return rc;
         spans.add(t1, spans.mark(c->stream), &g_timing.kernel_ms);
         HZ_TRY(hipEventRecord(done.e[b], c->stream));
     }
@@ -824,16 +900,53 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     uint8_t pend;
     if ((rc = hz_header_write(cb.get(), n, last_byte, head.data(), head.size(), &hb, &pend_bits, &pend))) return rc;
     g_timing.host_ms += ms_since(th);
-    FILE* fo = fopen(out_path, "wb");
-    if (!fo) return HZ_EIO;
-    std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
-    if ((rc = write_exact(fo, head.data(), hb))) return rc;
+    FileWriter fout;
+    if ((rc = fout.open(out_path))) return rc;
+    if ((rc = fout.write_now(head.data(), hb, 0))) return rc;
     uint64_t written = hb;
     const uint64_t nsym_total = n / 2;
+    const uint64_t body = 2 * nsym_total;  // the odd last byte travels in the header
+    uint32_t lead = pend_bits ? (uint32_t)(pend >> (8 - pend_bits)) : 0u;
+    DevBuf dpay;
+    if (resident && nsym_total) {
+        const uint64_t pay_bytes = (pend_bits + pbits + 7) / 8;
+        const uint64_t cap = ((pend_bits + pbits + 31) / 32 + 1) * 4;
+        const auto tb = Clock::now();
+        resident = dpay.alloc(cap) == HZ_OK;
+        g_timing.alloc_ms += ms_since(tb);
+        if (resident) {
+            // ---- pass 2, resident: one pack launch over the whole input, then the payload
+            // leaves in chunks (copy-out double-buffered against the parallel file writes)
+            const auto tu = Clock::now();
+            if ((rc = hz_codebook_upload_encode(c, cb.get()))) return rc;
+            g_timing.host_ms += ms_since(tu);
+            hipEvent_t t1 = spans.mark(c->stream);
+            if ((rc = hz_pack(c, (const uint8_t*)dall.p, body, pend_bits, lead, (uint8_t*)dpay.p, cap, nullptr)))
+                return rc;
+            spans.add(t1, spans.mark(c->stream), &g_timing.kernel_ms);
+            for (uint64_t off = 0, k = 0; off < pay_bytes; off += chunk, ++k) {
+                const int b = (int)(k & 1);
+                const uint64_t len = std::min(chunk, pay_bytes - off);
+                hipEvent_t t2 = spans.mark(c->stream);
+                HZ_TRY(hipMemcpyAsync(hin[b].p, (const uint8_t*)dpay.p + off, len, hipMemcpyDeviceToHost, c->stream));
+                spans.add(t2, spans.mark(c->stream), &g_timing.d2h_ms);
+                HZ_TRY(hipEventRecord(done.e[b], c->stream));
+                HZ_TRY(hipEventSynchronize(done.e[b]));
+                if ((rc = hz_ctx_sync(c))) return rc;
+                spans.fold();
+                if ((rc = fout.wait())) return rc;  // the write of chunk k - 1 (buffer 1 - b)
+                fout.start(hin[b].p, len, written);
+                written += len;
+            }
+        } else {  // no room for the payload beside the input: stream pass 2 from the file
+            (void)hipFree(dall.p);
+            dall.p = nullptr;
+        }
+    }
     if (nsym_total == 0) {
-        if (pend_bits && (rc = write_exact(fo, &pend, 1))) return rc;
+        if (pend_bits && (rc = fout.write_now(&pend, 1, written))) return rc;
         written += pend_bits ? 1 : 0;
-    } else {
+    } else if (!resident) {
         // ---- pass 2: pack chunk by chunk at the running bit offset
         const auto tu = Clock::now();
         if ((rc = hz_codebook_upload_encode(c, cb.get()))) return rc;
@@ -844,11 +957,13 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         PinnedBuf hout[2];
         const auto tb = Clock::now();
         for (int i = 0; i < 2; ++i) {
+            if (!din[i].p && (rc = din[i].alloc(chunk + 16))) return rc;
             if ((rc = dout[i].alloc(out_cap))) return rc;
             if ((rc = hout[i].alloc(out_cap))) return rc;
         }
         if ((rc = didx.alloc(hz_index_bytes(csym)))) return rc;
         g_timing.alloc_ms += ms_since(tb);
+        WriterDrain wdrain{fout};
         DrainGuard drain_out(c->stream);
         StreamGuard cs;  // copy-out stream
         HZ_TRY(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
@@ -856,10 +971,8 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         if ((rc = packed.create()) || (rc = copied.create())) return rc;
         if (fseek(fp, 0, SEEK_SET) != 0) return HZ_EIO;
         uint32_t sbit = pend_bits;                       // bit of the chunk's first code in its first word
-        uint32_t lead = pend_bits ? (uint32_t)(pend >> (8 - pend_bits)) : 0u;
-        const uint64_t body = 2 * nsym_total;             // the odd last byte travels in the header
         if ((rc = read_exact(fp, hin[0].p, std::min(chunk, body)))) return rc;
-        int wbuf = -1;          // chunk waiting for its fwrite: buffer, bytes
+        int wbuf = -1;          // chunk waiting for its write: buffer, bytes
         uint64_t wbytes = 0;
         for (uint64_t off = 0, k = 0; off < body; off += chunk, ++k) {
             const int b = (int)(k & 1);
@@ -877,10 +990,11 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
             const uint64_t nb = (len / 2 + 2047) / 2048;
             uint64_t end_bit = 0;
             HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + nb, 8, hipMemcpyDeviceToHost, c->stream));
-            // host work beside the upload and pack: the previous chunk's fwrite, the next chunk's fread
+            // host work beside the upload and pack: the previous chunk's write, the next chunk's fread
             if (wbuf >= 0) {
                 HZ_TRY(hipEventSynchronize(copied.e[wbuf]));
-                if ((rc = write_exact(fo, hout[wbuf].p, wbytes))) return rc;
+                if ((rc = fout.wait())) return rc;  // hout[b] (two chunks back) is free again after this
+                fout.start(hout[wbuf].p, wbytes, written);
                 written += wbytes;
                 wbuf = -1;
             }
@@ -898,6 +1012,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
                 if ((rc = hz_ctx_sync(c))) return rc;
                 lead = __builtin_bswap32(w) >> (32 - sbit);
             }
+            if ((rc = fout.wait())) return rc;  // hout[b] may still be leaving from two chunks back
             HZ_TRY(hipStreamWaitEvent(cs.s, packed.e[b], 0));
             hipEvent_t t2 = spans.mark(cs.s);
             if (bytes) HZ_TRY(hipMemcpyAsync(hout[b].p, dout[b].p, bytes, hipMemcpyDeviceToHost, cs.s));
@@ -908,11 +1023,14 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         }
         if (wbuf >= 0) {
             HZ_TRY(hipEventSynchronize(copied.e[wbuf]));
-            if ((rc = write_exact(fo, hout[wbuf].p, wbytes))) return rc;
+            if ((rc = fout.wait())) return rc;
+            fout.start(hout[wbuf].p, wbytes, written);
             written += wbytes;
         }
+        if ((rc = fout.wait())) return rc;
         HZ_TRY(hipStreamSynchronize(cs.s));
     }
+    if ((rc = fout.close())) return rc;
     spans.fold();
     if (written != (hbits + pbits + 7) / 8) return HZ_EFORMAT;
     if (verbose) {
@@ -929,7 +1047,16 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
 extern "C" int hz_archive_stream(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     g_timing = hz_stream_timing();
     const auto t0 = Clock::now();
-    const int rc = guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose); });
+    const int rc = guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose, false); });
+    g_timing.total_ms = ms_since(t0);
+    return rc;
+}
+
+// hz_archive_file's archive: the input stays on the device between the passes when it fits.
+static int archive_resident(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
+    g_timing = hz_stream_timing();
+    const auto t0 = Clock::now();
+    const int rc = guarded([&] { return hz_archive_stream_impl(in_path, out_path, chunk_bytes, verbose, true); });
     g_timing.total_ms = ms_since(t0);
     return rc;
 }
@@ -959,9 +1086,9 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
     hz_header_info info;
     if ((rc = hz_header_parse(head.data(), head.size(), cb.get(), &info))) return rc;
     g_timing.host_ms += ms_since(th);
-    FILE* fo = fopen(out_path, "wb");
-    if (!fo) return HZ_EIO;
-    std::unique_ptr<FILE, int (*)(FILE*)> fout(fo, fclose);
+    FileWriter fout;
+    if ((rc = fout.open(out_path))) return rc;
+    uint64_t out_off = 0;
     const uint64_t nsym = info.n / 2;
     if (nsym > 0) {
         hz_ctx* c;
@@ -981,14 +1108,17 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
         const double mean = pay_total ? ((double)pay_total * 8 - info.payload_bit) / (double)nsym : (double)max_len;
         const uint64_t sym_cap = std::max<uint64_t>(W / 2, kBlockSyms);  // output per round <= W bytes
         DevBuf dwin[2], didx, dout;
-        PinnedBuf hin, hout;
+        PinnedBuf hin, hout[2];  // hout: a round's output leaves (parallel writes) beside the next round
+        int ob = 0;
         const auto ta = Clock::now();
         for (int i = 0; i < 2; ++i)
             if ((rc = dwin[i].alloc(W + 16))) return rc;
         if ((rc = didx.alloc(hz_index_bytes(sym_cap)))) return rc;
         if ((rc = dout.alloc(2 * sym_cap + 16))) return rc;
         if ((rc = hin.alloc(W))) return rc;
-        if ((rc = hout.alloc(2 * sym_cap))) return rc;
+        for (int i = 0; i < 2; ++i)
+            if ((rc = hout[i].alloc(2 * sym_cap))) return rc;
+        WriterDrain wdrain{fout};
         g_timing.alloc_ms += ms_since(ta);
         DrainGuard drain(c->stream);
         if (fseek(fp, (long)info.payload_byte, SEEK_SET) != 0) return HZ_EIO;
@@ -1040,7 +1170,7 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
                 return rc;
             spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
             hipEvent_t t1 = spans.mark(c->stream);
-            HZ_TRY(hipMemcpyAsync(hout.p, dout.p, 2 * k, hipMemcpyDeviceToHost, c->stream));
+            HZ_TRY(hipMemcpyAsync(hout[ob].p, dout.p, 2 * k, hipMemcpyDeviceToHost, c->stream));
             spans.add(t1, spans.mark(c->stream), &g_timing.d2h_ms);
             // move the unconsumed tail to the other window and read the refill behind the decode
             const uint64_t used = end_bit / 8, tail = have - used;
@@ -1073,14 +1203,19 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
             } else {
                 done += kdone;
             }
-            if ((rc = write_exact(fo, hout.p, 2 * kdone))) return rc;
+            if ((rc = fout.wait())) return rc;  // the previous round's write: hout[ob ^ 1] free for the next
+            fout.start(hout[ob].p, 2 * kdone, out_off);
+            out_off += 2 * kdone;
+            ob ^= 1;
         }
+        if ((rc = fout.wait())) return rc;
         spans.fold();
     }
     if (info.is_odd) {
         const uint8_t b = (uint8_t)info.last_byte;
-        if ((rc = write_exact(fo, &b, 1))) return rc;
+        if ((rc = fout.write_now(&b, 1, out_off))) return rc;
     }
+    if ((rc = fout.close())) return rc;
     if (verbose) std::cout << "Decompression is complete" << std::endl;
     return HZ_OK;
 }
@@ -1151,7 +1286,10 @@ extern "C" int hz_archive_file(const char* path, int verbose) {
         return HZ_ENOENT;
     }
     const std::string outname = std::string(path) + ".compressed";
-    const int rc = hz_archive_stream(path, outname.c_str(), kArchiveChunk, verbose);
+    // HZ_ARCHIVE_CHUNK: chunk bytes of the file reads and payload writes (tests use small ones)
+    const char* ce = getenv("HZ_ARCHIVE_CHUNK");
+    const uint64_t chunk = ce && strtoull(ce, nullptr, 10) >= 64 ? strtoull(ce, nullptr, 10) : kArchiveChunk;
+    const int rc = archive_resident(path, outname.c_str(), chunk, verbose);
     if (rc) {
         remove(outname.c_str());  // never leave a truncated archive behind
         if (verbose) std::cerr << "archive: " << hz_strerror(rc) << std::endl;

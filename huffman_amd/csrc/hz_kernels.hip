@@ -19,9 +19,6 @@
 namespace hz {
 
 #define HZ_DEV __device__ __forceinline__
-#ifndef HZ_EXP_PACK
-#define HZ_EXP_PACK 0
-#endif
 
 // Dynamic-LDS limit of a kernel: hipFuncSetAttribute is per device, so the
 // (kernel, device) pairs already raised are remembered under a lock (any
@@ -315,7 +312,7 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
     x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
-    x.bstart = a.blk_start[blk];
+    x.bstart = a.blk_start ? a.blk_start[blk] : 0;  // one-pass pack (k_pack_lb): from the look-back
 }
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
@@ -372,11 +369,6 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         // of later loads and stores static. The escape table holds entries in
         // the register format, so each load lands in its e[k] directly.
         (void)any;
-#if HZ_EXP_PACK == 1
-#pragma unroll
-        for (int k = 0; k < kSPT; ++k) e[k] = (T)((uint32_t)e[k] & 0x7fffffffu);
-        xe = (T)(xx & 0x7fffffffu);
-#else
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             const bool miss = (uint32_t)e[k] >> 31;
@@ -388,7 +380,6 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             const uint32_t v = a.esc[miss ? xs : 0u];
             xe = miss ? (T)v : xe;
         }
-#endif
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
@@ -722,6 +713,192 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
+// ---- one-pass pack: block starts by a resolver wave ------------------------
+// Replaces k_pack_count + the scan kernels for HOT and DENSE tables, so pack
+// reads its input once (Compressor.cu:543-576 computes the same start bits
+// with populateCWLength + transform_inclusive_scan). Wave 0 of workgroup 0 is
+// the RESOLVER; every other wave is a packer, and packer w of W packs blocks
+// w, w + W, w + 2W, ... (the grid is sized to be co-resident, as
+// k_pack_write's). A packer looks the codes of a block up, counts its bits and
+// publishes the count, then looks up and publishes its NEXT block, and only
+// then takes the first block's start bit and emits it. The resolver walks the
+// blocks in order, kRsvBatch x 64 counts in flight per round trip, and
+// publishes every block's start as a running sum -- an exclusive scan with no
+// look-back and no contention. No workgroup barrier.
+//   - counts and starts are self-validating granules (a flag bit in the word,
+//     written and read with agent-scope relaxed atomics = sc1), so no fence
+//     orders them against anything else;
+//   - a wave that finds an unpublished count or start sleeps and re-reads it
+//     (its producer publishes without waiting); the spins are bounded
+//     (HZ_ETIMEOUT), so the kernel never hangs.
+constexpr uint32_t kAggValid = 1u << 31;
+constexpr uint64_t kStartValid = 1ull << 63;
+constexpr uint32_t kLbMaxSpins = 1u << 24;  // then flag HZ_ETIMEOUT (err bit 8) and go on: never a hang
+constexpr int kRsvBatch = 16;               // 64-block groups per resolver round trip
+
+struct LbArgs {
+    uint32_t* blk_agg;              // per block: kAggValid | bits
+    unsigned long long* blk_start;  // per block: kStartValid | start bit
+    uint64_t start_bit;
+};
+
+HZ_DEV uint32_t lb_ld32(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+HZ_DEV uint64_t lb_ld64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+HZ_DEV void lb_st32(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+HZ_DEV void lb_st64(unsigned long long* p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The resolver: block starts in order, kRsvPer blocks per lane and kRsvPer * 64
+// per batch (lane i: blocks [base + kRsvPer i, + kRsvPer)); the next batch's
+// counts are in flight while this batch's starts are summed and stored. The
+// counts and starts move as 16-byte sc1 buffer accesses (every u32 count and
+// u64 start validates itself, so a torn 16-byte access is harmless).
+constexpr int kRsvPer = 16;
+constexpr uint32_t kRsvBatchBlocks = kRsvPer * kWave;
+
+HZ_DEV void rsv_load(__amdgpu_buffer_rsrc_t r, uint64_t base, int lane, uint32_t (&c)[kRsvPer]) {
+    const uint32_t off = (uint32_t)((base + (uint64_t)kRsvPer * lane) * 4);
+#pragma unroll
+    for (int q = 0; q < kRsvPer / 4; ++q) {
+        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 16));
+        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+    }
+}
+
+constexpr int kRsvRing = 4;  // batches whose counts are in flight
+
+HZ_DEV void lb_resolver(const PackArgs& a, const LbArgs& l, int lane) {
+    // reads past the last block fall outside the buffers' ranges: they return 0 and stores are dropped
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(l.blk_agg, 0, (uint32_t)(a.nblocks * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(l.blk_start, 0, (uint32_t)(a.nblocks * 8), 0x00020000);
+    uint64_t run = l.start_bit;
+    uint32_t c[kRsvRing][kRsvPer];
+#pragma unroll
+    for (int r = 0; r < kRsvRing - 1; ++r) rsv_load(ra, (uint64_t)r * kRsvBatchBlocks, lane, c[r]);
+    // one batch: wait for its counts, publish its starts; then issue the loads kRsvRing - 1 batches ahead
+    auto batch = [&](uint32_t (&cur)[kRsvPer], uint32_t (&ahead)[kRsvPer], uint64_t base) {
+        const uint64_t b0 = base + (uint64_t)kRsvPer * lane;
+        for (uint32_t n = 0;; ++n) {  // every count published (blocks past the end count as published zeros)
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < kRsvPer; ++k) ok &= (cur[k] & kAggValid) || b0 + k >= a.nblocks;
+            if (!__ballot(!ok)) break;
+            if (n == kLbMaxSpins) {
+                if (lane == 0) atomicOr(a.err, 8u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (!ok) {
+#pragma unroll
+                for (int k = 0; k < kRsvPer; ++k)
+                    if (!(cur[k] & kAggValid) && b0 + k < a.nblocks) cur[k] = lb_ld32(l.blk_agg + b0 + k);
+            }
+        }
+        rsv_load(ra, base + (uint64_t)(kRsvRing - 1) * kRsvBatchBlocks, lane, ahead);  // harmless past the end
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < kRsvPer; ++k) sum += cur[k] & ~kAggValid;  // < 16 * 2^17
+        const uint32_t incl = wave_incl_sum(sum);                        // < 2^27
+        uint64_t st = run + (incl - sum);
+        const uint32_t off = (uint32_t)(b0 * 8);
+#pragma unroll
+        for (int q = 0; q < kRsvPer / 2; ++q) {
+            const uint64_t s0 = st, s1 = st + (cur[2 * q] & ~kAggValid);
+            st = s1 + (cur[2 * q + 1] & ~kAggValid);
+            const uint4 v = make_uint4((uint32_t)s0, (uint32_t)(s0 >> 32) | 0x80000000u, (uint32_t)s1,
+                                       (uint32_t)(s1 >> 32) | 0x80000000u);  // kStartValid
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                   rs, off + 16 * q, 0, 16);
+        }
+        run += readlane(incl, 63);
+    };
+    static_assert(kRsvRing == 4, "ring of four");
+    for (uint64_t base = 0; base < a.nblocks; base += kRsvRing * kRsvBatchBlocks) {  // unrolled: no copies
+        batch(c[0], c[3], base);
+        if (base + kRsvBatchBlocks >= a.nblocks) break;
+        batch(c[1], c[0], base + kRsvBatchBlocks);
+        if (base + 2 * kRsvBatchBlocks >= a.nblocks) break;
+        batch(c[2], c[1], base + 2 * kRsvBatchBlocks);
+        if (base + 3 * kRsvBatchBlocks >= a.nblocks) break;
+        batch(c[3], c[2], base + 3 * kRsvBatchBlocks);
+    }
+}
+
+// Block b's start bit; `v` is a poll issued earlier (its latency hidden behind
+// a block's lookup), re-polled only while the start is unpublished.
+HZ_DEV uint64_t lb_wait_start(const PackArgs& a, const LbArgs& l, uint64_t b, uint64_t v, int lane) {
+    for (uint32_t n = 0; !(v & kStartValid); ++n) {
+        if (n == kLbMaxSpins) {
+            if (lane == 0) atomicOr(a.err, 8u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        v = lb_ld64(l.blk_start + b);
+    }
+    return v & ~kStartValid;
+}
+
+// Blocks a packer has counted and published ahead of the one it emits: the
+// resolver's two hops (packer -> resolver -> packer, ~1-2 us each under load)
+// hide behind that many blocks of lookup work (one block ahead measured
+// 16.0 ms at 16 GiB Zipf with 45 % of the packers' time in the wait).
+#ifndef HZ_LB_AHEAD
+#define HZ_LB_AHEAD 2
+#endif
+constexpr int kLbAhead = HZ_LB_AHEAD;
+
+template <int MODE>
+__global__ __launch_bounds__(kPackWriteThreads) void k_pack_lb(PackArgs a, LbArgs l) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);  // the kernel's only workgroup barrier
+    const int lane = threadIdx.x & 63;
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (gw == 0) {
+        lb_resolver(a, l, lane);
+        return;
+    }
+    uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6) - 1;  // packers
+    uint64_t max_bits = 0;
+    const uint64_t first = gw - 1;
+    if (first < a.nblocks) {
+        // ring of kLbAhead + 1 counted blocks; block j of this packer (first + j W) sits in p[j % 3]
+        PackBlk<MODE> p[kLbAhead + 1];
+        PackIn in;
+        pack_prefetch(a, first, lane, in);
+        // steps j = 0, 1, ...: count + publish block j + kLbAhead (input prefetched), then emit block j
+        auto count = [&](PackBlk<MODE>& q, uint64_t b) {
+            pack_block_lookup<MODE>(a, lds, b, lane, in, q);
+            pack_prefetch(a, b + W < a.nblocks ? b + W : b, lane, in);
+            pack_block_count<MODE>(lane, q);
+            if (lane == 0) lb_st32(l.blk_agg + b, kAggValid | q.bits);
+        };
+#pragma unroll
+        for (int j = 0; j < kLbAhead; ++j)
+            if (first + j * W < a.nblocks) count(p[j], first + j * W);
+        // one step: emit block b (slot pe) after counting block b + 2W into slot pc
+        auto step = [&](PackBlk<MODE>& pe, PackBlk<MODE>& pc, uint64_t b) -> bool {
+            const uint64_t poll = lb_ld64(l.blk_start + b);  // lands during the lookup below
+            const uint64_t bc = b + kLbAhead * W;
+            if (bc < a.nblocks) count(pc, bc);
+            const uint64_t bst = lb_wait_start(a, l, b, poll, lane);
+            pack_block_emit<MODE>(a, slot, b, lane, pe, bst, max_bits);
+            return b + W < a.nblocks;
+        };
+        for (uint64_t b = first;; b += (kLbAhead + 1) * W) {  // unrolled by the ring size: no register rotation
+            bool more = true;
+#pragma unroll
+            for (int j = 0; j <= kLbAhead && more; ++j)
+                more = step(p[j], p[(j + kLbAhead) % (kLbAhead + 1)], b + j * W);
+            if (!more) break;
+        }
+    }
+    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
+}
+
 // ---- every code 16 bits (U = 65 536, min_len = max_len = 16) ---------------
 // Symbol i starts at bit start_bit + 16 i: no count pass and no scan. Lane j
 // packs symbols [32 j, 32 j + 32) into the 16 words whose last bit lies in its
@@ -897,10 +1074,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long
     }
 }
 
+// k_pack_lb's scratch (u64 words): block starts, then u32 block counts.
+static uint64_t lb_scratch_words(uint64_t nblocks) { return nblocks + (nblocks + 1) / 2; }
+
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
-    return 2 * nblocks + ntiles;
+    const uint64_t three = 2 * nblocks + ntiles, one = lb_scratch_words(nblocks);
+    return three > one ? three : one;
 }
 
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
@@ -952,6 +1133,24 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t lds = 4 * (table_words + waves * a.slot_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
+    // one pass (k_pack_lb) on request: HZ_PACK_LB=1 (slower on MI355X than count + scan + write)
+    static const bool one_pass = [] { const char* v = getenv("HZ_PACK_LB"); return v && v[0] == '1'; }();
+    if (one_pass && t.enc_mode != ENC_WIDE && (wgs > 1 || waves > 1)) {  // a packer beside the resolver
+        LbArgs l;
+        l.blk_start = d_scratch;
+        l.blk_agg = reinterpret_cast<uint32_t*>(d_scratch + nblocks);
+        l.start_bit = start_bit;
+        a.blk_start = nullptr;
+        hipError_t e = hipMemsetAsync(d_scratch, 0, lb_scratch_words(nblocks) * 8, s);
+        if (e != hipSuccess) return e;
+        const void* fn = t.enc_mode == ENC_HOT ? (const void*)k_pack_lb<ENC_HOT> : (const void*)k_pack_lb<ENC_DENSE>;
+        if ((e = ensure_lds_limit(fn, kLdsBytes)) != hipSuccess) return e;
+        if (t.enc_mode == ENC_HOT)
+            hipLaunchKernelGGL(k_pack_lb<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a, l);
+        else
+            hipLaunchKernelGGL(k_pack_lb<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a, l);
+        return hipGetLastError();
+    }
     {
         hipError_t e = ensure_lds_limit((const void*)k_pack_count, kLen8LdsBytes);
         if (e != hipSuccess) return e;

@@ -166,6 +166,43 @@ def test_decode_variants_cli(hz, tmp_path, pipe, kind):
     assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
 
 
+@pytest.mark.parametrize("name,chunk", [("romeo.txt", 4096), ("romeo.txt", 64), ("zipf", 1 << 20)])
+def test_cli_archive_resident(hz, tmp_path, name, chunk):
+    """`archive` keeps a file that fits on the device resident between its two passes
+    (one read of the file, one pack launch, the payload leaving in `chunk`-byte pieces
+    through parallel positional writes): the file equals the oracle's / the golden
+    archive, and `extract` (double-buffered parallel writes) restores the input."""
+    data = read(name) if name != "zipf" else _zipf_bytes((20 << 20) + 1, 3)
+    (tmp_path / "in.bin").write_bytes(data)
+    env = dict(os.environ, HZ_ARCHIVE_CHUNK=str(chunk), HZ_TIMING="1")
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "archive"), "in.bin"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    import json
+    stage = json.loads([l for l in r.stderr.splitlines() if l.startswith("{")][-1])
+    blob = (tmp_path / "in.bin.compressed").read_bytes()
+    assert stage["bytes_in"] == len(data) and stage["bytes_out"] == len(blob)  # the file was read once
+    assert blob == (read(name + ".compressed") if name != "zipf" else oracle_lib.encode(data))
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "in.bin.compressed"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
+
+
+@pytest.mark.parametrize("kind", ["zipf", "skewed"])
+def test_one_pass_pack_opt_in(hz, tmp_path, kind):
+    """The one-pass pack (HZ_PACK_LB=1: one resolver wave chains block starts while
+    packer waves count, wait and emit; DESIGN.md records why it is not the default)
+    writes the same archive as count + scan + write."""
+    data = _zipf_bytes((24 << 20) + 1, 17) if kind == "zipf" else _skewed_bytes(24 << 20, 9)
+    (tmp_path / "in.bin").write_bytes(data)
+    env = dict(os.environ, HZ_PACK_LB="1")
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "archive"), "in.bin"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "in.bin.compressed").read_bytes() == oracle_lib.encode(data)
+
+
 def test_cli_exit_codes(hz, tmp_path):
     a = os.path.join(hz.BIN_DIR, "archive")
     e = os.path.join(hz.BIN_DIR, "extract")
