@@ -54,6 +54,23 @@ def source_id():
     return h.hexdigest()[:16]
 
 
+def build_variant(name, defines, verbose=False):
+    """An A/B build of the library with extra -D flags into huffman_amd/lib_<name>/
+    (loaded with HZ_LIB_VARIANT=lib_<name>; tools/ab.sh)."""
+    obj_dir = os.path.join(PKG, "_build_" + name)
+    lib = os.path.join(PKG, "lib_" + name, "libhuffman_amd.so")
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    objs = []
+    for src in LIB_SOURCES:
+        obj = os.path.join(obj_dir, src + ".o")
+        lang = ["-x", "hip"] if src.endswith(".hip") else []
+        _run([HIPCC] + CFLAGS + defines + lang + ["-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        objs.append(obj)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs, verbose)
+    return lib
+
+
 def build(verbose=False, force=False):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -82,5 +99,9 @@ def build(verbose=False, force=False):
 
 
 if __name__ == "__main__":
-    build(verbose="-v" in sys.argv, force="-f" in sys.argv)
-    print(LIB)
+    if "--variant" in sys.argv:  # python huffman_amd/build.py --variant NAME -DFLAG ...
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")], "-v" in sys.argv))
+    else:
+        build(verbose="-v" in sys.argv, force="-f" in sys.argv)
+        print(LIB)

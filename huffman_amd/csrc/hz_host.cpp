@@ -218,6 +218,14 @@ extern "C" int hz_codebook_build_device(hz_ctx* c, const uint64_t* d_hist, hz_co
     return arm_err_check(c);
 }
 
+#ifdef HZ_CB_PROF  // variant builds only: k_cb_generate's phase timestamps (tools/debug/cb_prof.py)
+extern "C" int hz_debug_cb_prof(hz_ctx* c, uint64_t* out) {
+    HZ_TRY(hipStreamSynchronize(c->stream));
+    HZ_TRY(hipMemcpy(out, c->d_cbws + 65536, 512 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return HZ_OK;
+}
+#endif
+
 extern "C" int hz_header_write_device(hz_ctx* c, const hz_codebook* d_cb, uint64_t n, uint8_t last_byte,
                                       uint8_t* d_out, uint64_t cap, uint64_t* d_info) {
     if (!c || !d_cb || !d_out || !d_info || (((uintptr_t)d_out) & 3)) return HZ_EINVAL;

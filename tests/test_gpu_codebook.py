@@ -202,3 +202,80 @@ def test_device_header_parse_rejects_truncated(env, cut):
     blob = open(os.path.join(GOLD, "romeo.txt.compressed"), "rb").read()
     with pytest.raises(hz.HZError):
         _device_parse(env, blob[:cut])
+
+
+def _parse_both(env, blob):
+    """(device result or None if rejected, oracle result or None if rejected)."""
+    torch, hz, codec = env
+    try:
+        dev = _device_parse(env, blob)
+    except hz.HZError:
+        dev = None
+    try:
+        ora = oracle_lib.parse_header(blob)
+    except ValueError:
+        ora = None
+    return dev, ora
+
+
+def _assert_parse_equal(dev, ora):
+    (cb, info), (order, ln, code, oinfo) = dev, ora
+    u = len(order)
+    assert cb.nsym == u and info == oinfo
+    assert np.array_equal(np.frombuffer(cb.order, dtype=np.uint16)[:u], order)
+    assert np.array_equal(np.frombuffer(cb.len, dtype=np.uint8), ln)
+    assert np.array_equal(np.frombuffer(cb.code, dtype=np.uint64)[ln > 0], code[ln > 0])
+    if u:
+        assert cb.max_len == int(ln.max()) and cb.min_len == int(ln[ln > 0].min())
+
+
+def _header_blob(hz, h, odd):
+    n = 2 * int(h.sum()) + odd
+    head, pbits, pend = hz.write_header(hz.build_codebook(h), n, 0xa5 if odd else 0)
+    return head + (bytes([pend]) if pbits else b"") + bytes(16)
+
+
+@pytest.mark.parametrize("name", sorted(HISTS))
+@pytest.mark.parametrize("odd", [0, 1])
+def test_device_header_parse_synthetic_headers(env, name, odd):
+    """Headers from U = 1 to U = 65 536 (a 2.7 Mbit entry stream, 660 segments),
+    40-bit codes (fibonacci_41) and tie-dense tables: the segment-parallel parser
+    equals the oracle's sequential restatement of Decompressor.cu:65-103."""
+    torch, hz, codec = env
+    dev, ora = _parse_both(env, _header_blob(hz, HISTS[name], odd))
+    assert dev is not None and ora is not None
+    _assert_parse_equal(dev, ora)
+
+
+@pytest.mark.parametrize("name", ["romeo", "rand_U5000_hi1000", "rand_U65536_hi100000"])
+def test_device_header_parse_mutations(env, name):
+    """Bit flips, a changed U field and truncations anywhere in the header: the
+    device parser rejects exactly what the oracle rejects (invalid length, a
+    duplicate symbol, entries or N past the end) and parses the rest identically."""
+    torch, hz, codec = env
+    base = _header_blob(hz, HISTS[name], 1)
+    rng = np.random.default_rng(len(base))
+    blobs = []
+    for _ in range(24):
+        b = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            bit = int(rng.integers(32, 8 * (len(b) - 16)))
+            b[bit // 8] ^= 0x80 >> (bit % 8)
+        blobs.append(bytes(b))
+    for du in (1, -1, 7):
+        b = bytearray(base)
+        u = (b[0] | b[1] << 8) + du
+        b[0], b[1] = u & 0xff, (u >> 8) & 0xff
+        blobs.append(bytes(b))
+    for cut in (len(base) - 17, len(base) - 24, len(base) // 2, 600):
+        blobs.append(base[:cut])
+    rejected = 0
+    for b in blobs:
+        dev, ora = _parse_both(env, b)
+        if ora is not None and ora[3][5] == 0 and ora[3][0] // 2 > 0:
+            continue  # U = 0 with symbols: rejected by the product on purpose (B4 convention)
+        assert (dev is None) == (ora is None)
+        rejected += ora is None
+        if ora is not None:
+            _assert_parse_equal(dev, ora)
+    assert rejected >= 4
