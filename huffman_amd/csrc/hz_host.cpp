@@ -884,16 +884,28 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         spans.add(t1, spans.mark(c->stream), &g_timing.kernel_ms);
         HZ_TRY(hipEventRecord(done.e[b], c->stream));
     }
+    // the codebook is built on the device from the device histogram (k_cb_*, 0.26 ms for
+    // U = 65 536 against 0.43 ms on the host plus the histogram's D2H; profiles/r03_codebook_*);
+    // HZ_HOST_CODEBOOK=1 builds it on the host instead. Both are bit-exact with GenerateCL.
+    static const bool host_cb = [] { const char* v = getenv("HZ_HOST_CODEBOOK"); return v && v[0] == '1'; }();
     std::vector<uint64_t> hist(HZ_NSYM);
+    std::unique_ptr<hz_codebook> cb(new hz_codebook());
+    DevBuf dcb;
+    if (!host_cb) {
+        if ((rc = dcb.alloc(sizeof(hz_codebook)))) return rc;
+        hipEvent_t t0 = spans.mark(c->stream);
+        if ((rc = hz_codebook_build_device(c, (const uint64_t*)dhist.p, (hz_codebook*)dcb.p))) return rc;
+        spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
+    }
     {
         hipEvent_t t0 = spans.mark(c->stream);
         HZ_TRY(hipMemcpyAsync(hist.data(), dhist.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
+        if (!host_cb) HZ_TRY(hipMemcpyAsync(cb.get(), dcb.p, sizeof(hz_codebook), hipMemcpyDeviceToHost, c->stream));
         spans.add(t0, spans.mark(c->stream), &g_timing.d2h_ms);
     }
     if ((rc = hz_ctx_sync(c))) return rc;
     const auto th = Clock::now();
-    std::unique_ptr<hz_codebook> cb(new hz_codebook());
-    if ((rc = hz_codebook_build(hist.data(), cb.get()))) return rc;
+    if (host_cb && (rc = hz_codebook_build(hist.data(), cb.get()))) return rc;
     uint64_t hbits = 0, pbits = 0;
     hz_header_bits(cb.get(), n, &hbits);
     hz_payload_bits(cb.get(), hist.data(), &pbits);
@@ -1069,6 +1081,43 @@ static int archive_resident(const char* in_path, const char* out_path, uint64_t 
     return rc;
 }
 
+// The header of a file to extract: parsed on the device (k_hdr_*, 0.05 ms for
+// U = 65 536 against 0.25+ ms on the host; profiles/r03_codebook_*), the codebook
+// and the info copied back for the host-built decode tables. HZ_HOST_HEADER=1
+// parses on the host. Both follow Decompressor.cu:65-103 and reject the same files.
+static int parse_header_for_extract(const std::vector<uint8_t>& head, hz_codebook* cb, hz_header_info* info) {
+    static const bool host_hdr = [] { const char* v = getenv("HZ_HOST_HEADER"); return v && v[0] == '1'; }();
+    const auto th = Clock::now();
+    int rc;
+    if (host_hdr || head.size() < 12) {  // a header-only file: no device work at all
+        rc = hz_header_parse(head.data(), head.size(), cb, info);
+        g_timing.host_ms += ms_since(th);
+        return rc;
+    }
+    hz_ctx* c;
+    if ((rc = default_ctx(&c))) return rc;
+    HZ_TRY(hipSetDevice(c->device));
+    DevBuf dhead, dcb, dinfo;
+    if ((rc = dhead.alloc(head.size())) || (rc = dcb.alloc(sizeof(hz_codebook))) || (rc = dinfo.alloc(6 * 8))) return rc;
+    g_timing.alloc_ms += ms_since(th);  // context and buffers: allocation, as on the host path
+    const auto tp = Clock::now();
+    uint64_t hi[6];
+    HZ_TRY(hipMemcpyAsync(dhead.p, head.data(), head.size(), hipMemcpyHostToDevice, c->stream));
+    if ((rc = hz_header_parse_device(c, (const uint8_t*)dhead.p, head.size(), (hz_codebook*)dcb.p, (uint64_t*)dinfo.p)))
+        return rc;
+    HZ_TRY(hipMemcpyAsync(cb, dcb.p, sizeof(hz_codebook), hipMemcpyDeviceToHost, c->stream));
+    HZ_TRY(hipMemcpyAsync(hi, dinfo.p, sizeof(hi), hipMemcpyDeviceToHost, c->stream));
+    if ((rc = hz_ctx_sync(c))) return rc;  // HZ_EFORMAT for a malformed header
+    info->n = hi[0];
+    info->payload_byte = hi[1];
+    info->payload_bit = (uint32_t)hi[2];
+    info->is_odd = (uint32_t)hi[3];
+    info->last_byte = (uint32_t)hi[4];
+    info->nsym = (uint32_t)hi[5];
+    g_timing.host_ms += ms_since(tp);
+    return HZ_OK;
+}
+
 // Streaming extract: the payload passes through a device window of chunk_bytes.
 // Each round decodes as many symbols as the window surely holds (the file's
 // mean code length with a margin; a round whose codes overrun the window is
@@ -1089,11 +1138,9 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
     std::vector<uint8_t> head(std::min<uint64_t>(fsize, 1u << 20));
     int rc = read_exact(fp, head.data(), head.size());
     if (rc) return rc;
-    const auto th = Clock::now();
     std::unique_ptr<hz_codebook> cb(new hz_codebook());
     hz_header_info info;
-    if ((rc = hz_header_parse(head.data(), head.size(), cb.get(), &info))) return rc;
-    g_timing.host_ms += ms_since(th);
+    if ((rc = parse_header_for_extract(head, cb.get(), &info))) return rc;
     FileWriter fout;
     if ((rc = fout.open(out_path))) return rc;
     uint64_t out_off = 0;
