@@ -491,7 +491,7 @@ extern "C" int hz_generate(hz_ctx* c, uint8_t* d_out, uint64_t n, uint64_t offse
 namespace {
 
 constexpr uint64_t kArchiveChunk = 256ull << 20;  // archive: 256 MiB per streamed chunk (~1.2 GB pinned)
-constexpr uint64_t kExtractWindow = 512ull << 20; // extract: 512 MiB payload windows
+constexpr uint64_t kExtractWindow = 256ull << 20; // extract: 256 MiB payload windows (16 GiB: 1.9 s vs 2.6 s at 512 MiB, 3.2 s at 128)
 
 std::mutex g_mu;
 hz_ctx* g_ctx = nullptr;
@@ -708,22 +708,49 @@ class Spans {
     std::vector<hipEvent_t> free_;
 };
 
+// Reads of 16 MiB and more go through 8 threads' positional reads (from the
+// stream's logical position, which is then moved past them): a single fread
+// copies out of the page cache at ~15 GB/s on the MI355X host.
 int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
     if (n == 0) return HZ_OK;
     const auto t0 = Clock::now();
-    const bool ok = fread(p, 1, n, fp) == n;
+    bool ok;
+    if (n < (16u << 20)) {
+        ok = fread(p, 1, n, fp) == n;
+    } else {
+        const off_t pos = ftello(fp);
+        const int fd = fileno(fp);
+        constexpr uint64_t kReaders = 8;
+        const uint64_t piece = ((n + kReaders - 1) / kReaders + 4095) & ~(uint64_t)4095;
+        std::atomic<bool> bad{pos < 0};
+        std::vector<std::thread> th;
+        for (uint64_t a = 0; a < n && !bad; a += piece) {
+            const uint64_t len = std::min(piece, n - a);
+            th.emplace_back([&bad, fd, p, a, len, pos] {
+                uint64_t done = 0;
+                while (done < len) {
+                    const ssize_t r = ::pread(fd, p + a + done, len - done, (off_t)(pos + a + done));
+                    if (r <= 0) { bad = true; return; }
+                    done += (uint64_t)r;
+                }
+            });
+        }
+        for (auto& t : th) t.join();
+        ok = !bad && fseeko(fp, pos + (off_t)n, SEEK_SET) == 0;
+    }
     g_timing.fread_ms += ms_since(t0);
     g_timing.bytes_in += ok ? n : 0;
     return ok ? HZ_OK : HZ_EIO;
 }
 
 // Output file written by background positional writes, so a chunk's write
-// overlaps the next chunk's device work. One thread's write into the page
-// cache moves ~5 GB/s on the MI355X host; 8 threads with pwrite measured the
-// same and 8 threads copying into a shared mmap 1.7 GB/s (tools/debug/write_bw.py):
-// that rate bounds extract's wall time. start() hands a buffer to kWriters
-// threads (one slice each) and returns; wait() joins them. One write is in
-// flight at a time, so the caller double-buffers.
+// overlaps the next chunk's device work. The file's final size is reserved
+// first (posix_fallocate): into page cache, 8 threads then write ~12 GB/s on
+// the MI355X host, against ~5 GB/s for one or 8 threads into a file that grows
+// (block allocation under the inode lock), 6.8 GB/s with O_DIRECT and 1.7 GB/s
+// copying into a shared mmap (tools/debug/write_bw.py, 8 GiB). start() hands a
+// buffer to kWriters threads (one slice each) and returns; wait() joins them.
+// One write is in flight at a time, so the caller double-buffers.
 class FileWriter {
   public:
     ~FileWriter() {
@@ -734,9 +761,15 @@ class FileWriter {
         fd_ = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
         return fd_ >= 0 ? HZ_OK : HZ_EIO;
     }
+    // Reserve the file's final size (best effort: a file system without
+    // fallocate only loses the speed-up).
+    void reserve(uint64_t size) {
+        if (fd_ >= 0 && size > 0) reserved_ = ::posix_fallocate(fd_, 0, (off_t)size) == 0;
+    }
     void start(const uint8_t* p, uint64_t n, uint64_t off) {
         if (n == 0) return;
         t0_ = Clock::now();
+        end_ = std::max(end_, off + n);
         const uint64_t nt = n < (8u << 20) ? 1 : kWriters;
         const uint64_t piece = ((n + nt - 1) / nt + 4095) & ~(uint64_t)4095;
         for (uint64_t a = 0; a < n; a += piece) {
@@ -767,13 +800,17 @@ class FileWriter {
     }
     int close() {
         int rc = wait();
+        // the file ends at its last written byte, whatever reserve() allocated
+        if (fd_ >= 0 && reserved_ && ::ftruncate(fd_, (off_t)end_) != 0) rc = HZ_EIO;
         if (fd_ >= 0 && ::close(fd_) != 0) rc = HZ_EIO;
         fd_ = -1;
         return rc;
     }
   private:
-    static constexpr uint64_t kWriters = 1;  // 8 writers measured the same (the file's inode lock serialises them)
+    static constexpr uint64_t kWriters = 8;
     int fd_ = -1;
+    bool reserved_ = false;
+    uint64_t end_ = 0;
     std::vector<std::thread> th_;
     std::atomic<bool> err_{false};
     Clock::time_point t0_;
@@ -922,6 +959,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     g_timing.host_ms += ms_since(th);
     FileWriter fout;
     if ((rc = fout.open(out_path))) return rc;
+    fout.reserve(hb + (pend_bits + pbits + 7) / 8);
     if ((rc = fout.write_now(head.data(), hb, 0))) return rc;
     uint64_t written = hb;
     const uint64_t nsym_total = n / 2;
@@ -1143,6 +1181,7 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
     if ((rc = parse_header_for_extract(head, cb.get(), &info))) return rc;
     FileWriter fout;
     if ((rc = fout.open(out_path))) return rc;
+    fout.reserve(info.n);
     uint64_t out_off = 0;
     const uint64_t nsym = info.n / 2;
     if (nsym > 0) {
@@ -1361,7 +1400,10 @@ extern "C" int hz_extract_file(const char* path, char* out_name, size_t out_name
         return HZ_ENOENT;
     }
     std::string name = output_name();
-    int rc = hz_extract_stream(path, name.c_str(), kExtractWindow, 0);
+    // HZ_EXTRACT_WINDOW: payload window bytes (>= 4096)
+    const char* we = getenv("HZ_EXTRACT_WINDOW");
+    const uint64_t window = we && strtoull(we, nullptr, 10) >= 4096 ? strtoull(we, nullptr, 10) : kExtractWindow;
+    int rc = hz_extract_stream(path, name.c_str(), window, 0);
     if (rc) {
         remove(name.c_str());
         if (verbose) std::cerr << "extract: " << hz_strerror(rc) << std::endl;
