@@ -7,9 +7,9 @@
 //                   GenerateCL's rounds and GenerateCW in one workgroup over
 //                   implicit lists, every leaf's code on all CUs (see the
 //                   section).
-//   k_header_write  the header (Compressor.cu:431-487, writers :637-669): one
-//                   thread per codebook entry at its scanned bit offset,
-//                   words ORed together.
+//   k_hw_*          the header (Compressor.cu:431-487, writers :637-669): 64
+//                   workgroups of 1024 entries at scanned bit offsets, each
+//                   assembled in LDS and stored as words.
 //   k_hdr_*         the header parse (Decompressor.cu:65-103): per-segment
 //                   entry-offset maps walked in parallel for every candidate
 //                   first-entry offset, composed into the true path, then
@@ -426,70 +426,133 @@ __global__ __launch_bounds__(kCbTileKeys) void k_cb_leaves(hz_codebook* __restri
 
 // ---- header writer ---------------------------------------------------------
 // Bit stream MSB first: bit b of the header is bit 7 - b % 8 of byte b / 8.
-// `put` ORs the low `nb` (<= 64) bits of v, first bit = bit nb - 1, at bit b.
-HZ_DEV void hdr_put(uint32_t* w32, uint64_t b, uint64_t v, uint32_t nb) {
+// 64 workgroups own 1024 entries each (Compressor.cu:454-483: symbol, L, code):
+// k_hw_sum sums each workgroup's entry bits, k_hw_prep scans the 64 sums into
+// start bits, zeroes the output words two workgroups share and writes the
+// info, k_hw_write assembles each workgroup's bits in LDS (prefix :434-443 in
+// workgroup 0, N :661-669 in workgroup 63) and stores its words -- the two
+// shared ones with atomicOr, the rest with plain stores.
+constexpr int kHwGroups = 64, kHwThreads = 1024;
+constexpr uint32_t kHwWords = (kHwThreads * (24 + HZ_MAXLEN) + 64 + 32 + 31) / 32 + 2;  // one workgroup's bits
+
+struct HwWs {
+    unsigned long long* sum;   // [64] entry bits per workgroup
+    unsigned long long* off;   // [65] first bit per workgroup, then the N field's first bit
+    unsigned long long* meta;  // [0] total bits, [1] capacity failure
+};
+
+HZ_DEV HwWs hw_ws(unsigned long long* w) { return HwWs{w, w + 64, w + 64 + 65}; }
+
+// ORs the low nb (<= 64) bits of v, first bit = bit nb - 1, at bit b of an LDS
+// run of big-endian-valued words.
+HZ_DEV void hw_put(uint32_t* lw, uint32_t b, uint64_t v, uint32_t nb) {
     while (nb) {
-        const uint32_t off = (uint32_t)(b & 31), take = 32 - off < nb ? 32 - off : nb;
+        const uint32_t off = b & 31, take = 32 - off < nb ? 32 - off : nb;
         const uint32_t bits = (uint32_t)(v >> (nb - take)) & (take == 32 ? 0xffffffffu : ((1u << take) - 1u));
-        const uint32_t be = bits << (32 - off - take);  // big-endian word value
-        atomicOr(&w32[b >> 5], __builtin_bswap32(be));
+        atomicOr(&lw[b >> 5], bits << (32 - off - take));
         b += take;
         nb -= take;
     }
 }
 
-constexpr int kHdrThreads = 1024;
+__global__ __launch_bounds__(kHwThreads) void k_hw_sum(const hz_codebook* __restrict__ cb, unsigned long long* wsp) {
+    __shared__ uint32_t part[kHwThreads / 64];
+    const HwWs w = hw_ws(wsp);
+    const uint32_t i = blockIdx.x * kHwThreads + threadIdx.x, U = cb->nsym;
+    uint32_t v = i < U ? 24u + cb->len[cb->order[i]] : 0u;
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int k = 0; k < kHwThreads / 64; ++k) s += part[k];
+        w.sum[blockIdx.x] = s;
+    }
+}
 
 // info (device): [0] complete header bytes, [1] pending bits, [2] pending byte (MSB aligned), [3] header bits
-__global__ __launch_bounds__(kHdrThreads) void k_header_write(const hz_codebook* __restrict__ cb, uint64_t n,
-                                                              uint32_t last_byte, uint8_t* out, uint64_t cap,
-                                                              unsigned long long* info, uint32_t* err) {
-    __shared__ unsigned long long part[kHdrThreads + 1];
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t U = cb->nsym;
-    const uint32_t odd = (uint32_t)(n & 1);
-    const uint32_t per = (U + nt - 1) / nt, i0 = tid * per < U ? tid * per : U, i1 = i0 + per < U ? i0 + per : U;
-    unsigned long long mine = 0;
-    for (uint32_t i = i0; i < i1; ++i) mine += 24u + cb->len[cb->order[i]];
-    part[tid] = mine;
-    __syncthreads();
-    if (tid == 0) {  // exclusive scan of the per-thread sums (1024 values)
-        unsigned long long acc = 8ull * (3 + odd);
-        for (uint32_t t = 0; t < nt; ++t) { const unsigned long long v = part[t]; part[t] = acc; acc += v; }
-        part[nt] = acc + 64;  // + N
+__global__ __launch_bounds__(64) void k_hw_prep(const hz_codebook* __restrict__ cb, uint64_t n, uint8_t* out,
+                                                uint64_t cap, unsigned long long* info, unsigned long long* wsp,
+                                                uint32_t* err) {
+    const HwWs w = hw_ws(wsp);
+    const uint32_t t = threadIdx.x;
+    const unsigned long long v = w.sum[t];
+    unsigned long long incl = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)incl, d), hi = (uint32_t)__shfl_up((int)(uint32_t)(incl >> 32), d);
+        if ((int)t >= d) incl += ((unsigned long long)hi << 32) | lo;
     }
-    __syncthreads();
-    const unsigned long long total = part[nt];
-    const uint64_t words = (total + 31) / 32;
-    if (words * 4 > cap) {
-        if (tid == 0) atomicOr(err, 4u);
-        return;
-    }
-    uint32_t* w32 = reinterpret_cast<uint32_t*>(out);
-    for (uint64_t k = tid; k < words; k += nt) w32[k] = 0;
-    __syncthreads();
-    if (tid == 0) {
-        hdr_put(w32, 0, U & 0xffffu ? ((U & 0xffu) << 8) | ((U >> 8) & 0xffu) : 0u, 16);  // u16 LE (:434)
-        hdr_put(w32, 16, odd, 8);                                                          // isOdd (:438)
-        if (odd) hdr_put(w32, 24, last_byte & 0xffu, 8);                                   // lastByte (:439-443)
-        uint64_t nn = n;                                                                   // writeFileSize (:661-669)
-        for (int k = 0; k < 8; ++k, nn >>= 8) hdr_put(w32, total - 64 + 8 * k, nn & 0xff, 8);
-    }
-    unsigned long long b = part[tid];
-    for (uint32_t i = i0; i < i1; ++i) {  // writeFromUShort, writeFromUChar, code bits (:454-483)
-        const uint32_t sym = cb->order[i], L = cb->len[sym];
-        hdr_put(w32, b, ((uint64_t)sym << 8) | L, 24);
-        hdr_put(w32, b + 24, cb->code[sym], L);
-        b += 24 + L;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        // the words were built by atomics at L2: read the pending byte the same way
-        const uint32_t wv = atomicOr(&w32[(total / 8) / 4], 0u);
+    const uint64_t pre = 8ull * (3 + (n & 1));
+    const uint64_t start = pre + incl - v, nstart = pre + (uint64_t)__shfl((int)(uint32_t)incl, 63) +
+                                                    ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(incl >> 32), 63) << 32);
+    const uint64_t total = nstart + 64, words = (total + 31) / 32;
+    const bool fail = words * 4 > cap;
+    w.off[t] = start;
+    if (t == 0) {
+        w.off[64] = nstart;
+        w.meta[0] = total;
+        w.meta[1] = fail;
+        if (fail) atomicOr(err, 4u);
+        const uint32_t r = (uint32_t)(total % 8), last = (uint32_t)(n >> 56) & 0xffu;  // N's last byte ends the header
         info[0] = total / 8;
-        info[1] = total % 8;
-        info[2] = (total % 8) ? (wv >> (8 * ((total / 8) % 4))) & 0xffu : 0;
+        info[1] = r;
+        info[2] = r ? ((last & ((1u << r) - 1u)) << (8 - r)) & 0xffu : 0u;
         info[3] = total;
+    }
+    if (!fail && t > 0 && (start & 31)) reinterpret_cast<uint32_t*>(out)[start >> 5] = 0;  // shared with group t - 1
+}
+
+__global__ __launch_bounds__(kHwThreads) void k_hw_write(const hz_codebook* __restrict__ cb, uint64_t n,
+                                                         uint32_t last_byte, uint8_t* out, unsigned long long* wsp) {
+    __shared__ uint32_t lw[kHwWords];
+    __shared__ uint32_t part[kHwThreads / 64];
+    const HwWs w = hw_ws(wsp);
+    if (w.meta[1]) return;
+    const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, U = cb->nsym;
+    const uint64_t s0 = t == 0 ? 0 : w.off[t], s1 = t + 1 < kHwGroups ? w.off[t + 1] : w.meta[0];
+    if (s1 <= s0) return;
+    const uint64_t base = s0 & ~31ull;
+    const uint32_t nw = (uint32_t)((s1 + 31) / 32 - base / 32);
+    for (uint32_t k = tid; k < nw; k += kHwThreads) lw[k] = 0;
+    const uint32_t i = t * kHwThreads + tid;
+    uint32_t sym = 0, L = 0;
+    if (i < U) {
+        sym = cb->order[i];
+        L = cb->len[sym];
+    }
+    const uint32_t bits = i < U ? 24u + L : 0u;
+    uint32_t incl = bits;  // exclusive scan of the entries' bits in the workgroup
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_up((int)incl, d);
+        if ((int)lane >= d) incl += x;
+    }
+    if (lane == 63) part[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < (tid >> 6); ++k) before += part[k];
+    const uint32_t rel = (uint32_t)(w.off[t] - base) + before + incl - bits;
+    if (i < U) {  // writeFromUShort, writeFromUChar, code bits (:454-483)
+        hw_put(lw, rel, ((uint64_t)sym << 8) | L, 24);
+        hw_put(lw, rel + 24, cb->code[sym], L);
+    }
+    if (tid == 0 && t == 0) {
+        const uint32_t U16 = U & 0xffffu, odd = (uint32_t)(n & 1);
+        hw_put(lw, 0, U16 ? ((U16 & 0xffu) << 8) | (U16 >> 8) : 0u, 16);  // u16 LE (:434)
+        hw_put(lw, 16, odd, 8);                                           // isOdd (:438)
+        if (odd) hw_put(lw, 24, last_byte & 0xffu, 8);                    // lastByte (:439-443)
+    }
+    if (tid == 0 && t + 1 == kHwGroups) {  // writeFileSize (:661-669): 8 LE bytes, each MSB first
+        uint64_t nn = n;
+        const uint32_t nb = (uint32_t)(w.off[64] - base);
+        for (int k = 0; k < 8; ++k, nn >>= 8) hw_put(lw, nb + 8 * k, nn & 0xffu, 8);
+    }
+    __syncthreads();
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(out) + base / 32;
+    const bool shared_first = t > 0 && (s0 & 31), shared_last = t + 1 < kHwGroups && (s1 & 31);
+    for (uint32_t k = tid; k < nw; k += kHwThreads) {
+        const uint32_t v = __builtin_bswap32(lw[k]);
+        if ((k == 0 && shared_first) || (k + 1 == nw && shared_last)) atomicOr(&o32[k], v);
+        else o32[k] = v;
     }
 }
 
@@ -805,8 +868,11 @@ __global__ __launch_bounds__(64) void k_hdr_finish(const uint8_t* __restrict__ f
 }
 
 hipError_t launch_header_write(const hz_codebook* d_cb, uint64_t n, uint32_t last_byte, uint8_t* d_out, uint64_t cap,
-                               unsigned long long* d_info, uint32_t* d_err, hipStream_t s) {
-    hipLaunchKernelGGL(k_header_write, dim3(1), dim3(kHdrThreads), 0, s, d_cb, n, last_byte, d_out, cap, d_info, d_err);
+                               unsigned long long* d_info, unsigned long long* d_ws, uint32_t* d_err, hipStream_t s) {
+    unsigned long long* w = d_ws + codebook_ws_words() - 256;  // the workspace's last 256 words
+    hipLaunchKernelGGL(k_hw_sum, dim3(kHwGroups), dim3(kHwThreads), 0, s, d_cb, w);
+    hipLaunchKernelGGL(k_hw_prep, dim3(1), dim3(64), 0, s, d_cb, n, d_out, cap, d_info, w, d_err);
+    hipLaunchKernelGGL(k_hw_write, dim3(kHwGroups), dim3(kHwThreads), 0, s, d_cb, n, last_byte, d_out, w);
     return hipGetLastError();
 }
 
@@ -847,7 +913,7 @@ hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, 
 // Workspace (u64 words) shared by the codebook build and the header parse.
 uint64_t codebook_ws_words() {
     const uint64_t hp = (18ull * kHpMaxSeg * kHpCand + 5ull * (kHpMaxSeg + 64) + 4 * 2048 + 64) / 8 + 8;
-    return kCbWsWords > hp ? kCbWsWords : hp;
+    return (kCbWsWords > hp ? kCbWsWords : hp) + 256;  // + the header writer's scan
 }
 
 }  // namespace hz

@@ -230,8 +230,9 @@ extern "C" int hz_header_write_device(hz_ctx* c, const hz_codebook* d_cb, uint64
                                       uint8_t* d_out, uint64_t cap, uint64_t* d_info) {
     if (!c || !d_cb || !d_out || !d_info || (((uintptr_t)d_out) & 3)) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
-    HZ_TRY(launch_header_write(d_cb, n, last_byte, d_out, cap, reinterpret_cast<unsigned long long*>(d_info), c->d_err,
-                               c->stream));
+    if (!c->d_cbws) HZ_TRY(hipMalloc(&c->d_cbws, codebook_ws_words() * sizeof(unsigned long long)));
+    HZ_TRY(launch_header_write(d_cb, n, last_byte, d_out, cap, reinterpret_cast<unsigned long long*>(d_info), c->d_cbws,
+                               c->d_err, c->stream));
     return arm_err_check(c);
 }
 

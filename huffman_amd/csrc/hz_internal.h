@@ -156,7 +156,7 @@ hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, 
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();
 hipError_t launch_header_write(const hz_codebook* d_cb, uint64_t n, uint32_t last_byte, uint8_t* d_out, uint64_t cap,
-                               unsigned long long* d_info, uint32_t* d_err, hipStream_t s);
+                               unsigned long long* d_info, unsigned long long* d_ws, uint32_t* d_err, hipStream_t s);
 hipError_t launch_header_parse(const uint8_t* d_file, uint64_t len, hz_codebook* d_cb, unsigned long long* d_info,
                                unsigned long long* d_ws, uint32_t* d_err, hipStream_t s);
 hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
