@@ -926,19 +926,31 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     // U = 65 536 against 0.43 ms on the host plus the histogram's D2H; profiles/r03_codebook_*);
     // HZ_HOST_CODEBOOK=1 builds it on the host instead. Both are bit-exact with GenerateCL.
     static const bool host_cb = [] { const char* v = getenv("HZ_HOST_CODEBOOK"); return v && v[0] == '1'; }();
+    // and so is the header (k_hw_*, 0.014 ms against 0.25 ms on the host)
     std::vector<uint64_t> hist(HZ_NSYM);
     std::unique_ptr<hz_codebook> cb(new hz_codebook());
-    DevBuf dcb;
+    constexpr uint64_t kHeadCap = 16 + 65536ull * 11;  // the longest header
+    std::vector<uint8_t> head;
+    uint64_t dinfo_h[4] = {0, 0, 0, 0};
+    DevBuf dcb, dhead, dinfo;
     if (!host_cb) {
-        if ((rc = dcb.alloc(sizeof(hz_codebook)))) return rc;
+        if ((rc = dcb.alloc(sizeof(hz_codebook))) || (rc = dhead.alloc(kHeadCap)) || (rc = dinfo.alloc(4 * 8))) return rc;
+        head.resize(kHeadCap);
         hipEvent_t t0 = spans.mark(c->stream);
         if ((rc = hz_codebook_build_device(c, (const uint64_t*)dhist.p, (hz_codebook*)dcb.p))) return rc;
+        if ((rc = hz_header_write_device(c, (const hz_codebook*)dcb.p, n, last_byte, (uint8_t*)dhead.p, kHeadCap,
+                                         (uint64_t*)dinfo.p)))
+            return rc;
         spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
     }
     {
         hipEvent_t t0 = spans.mark(c->stream);
         HZ_TRY(hipMemcpyAsync(hist.data(), dhist.p, HZ_NSYM * 8, hipMemcpyDeviceToHost, c->stream));
-        if (!host_cb) HZ_TRY(hipMemcpyAsync(cb.get(), dcb.p, sizeof(hz_codebook), hipMemcpyDeviceToHost, c->stream));
+        if (!host_cb) {
+            HZ_TRY(hipMemcpyAsync(cb.get(), dcb.p, sizeof(hz_codebook), hipMemcpyDeviceToHost, c->stream));
+            HZ_TRY(hipMemcpyAsync(dinfo_h, dinfo.p, sizeof(dinfo_h), hipMemcpyDeviceToHost, c->stream));
+            HZ_TRY(hipMemcpyAsync(head.data(), dhead.p, kHeadCap, hipMemcpyDeviceToHost, c->stream));
+        }
         spans.add(t0, spans.mark(c->stream), &g_timing.d2h_ms);
     }
     if ((rc = hz_ctx_sync(c))) return rc;
@@ -952,11 +964,18 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         std::cout << "Unique symbols count: " << cb->nsym << std::endl;
     }
     // ---- header
-    std::vector<uint8_t> head(hbits / 8 + 8);
     uint64_t hb;
     uint32_t pend_bits;
     uint8_t pend;
-    if ((rc = hz_header_write(cb.get(), n, last_byte, head.data(), head.size(), &hb, &pend_bits, &pend))) return rc;
+    if (host_cb) {
+        head.resize(hbits / 8 + 8);
+        if ((rc = hz_header_write(cb.get(), n, last_byte, head.data(), head.size(), &hb, &pend_bits, &pend))) return rc;
+    } else {
+        hb = dinfo_h[0];
+        pend_bits = (uint32_t)dinfo_h[1];
+        pend = (uint8_t)dinfo_h[2];
+        if (dinfo_h[3] != hbits) return HZ_EFORMAT;  // the device writer disagrees with the header length
+    }
     g_timing.host_ms += ms_since(th);
     FileWriter fout;
     if ((rc = fout.open(out_path))) return rc;
