@@ -2400,7 +2400,11 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             uint32_t g[C];
 #pragma unroll
             for (int c = 0; c < C; ++c)
+#ifdef HZ_EXP_NOESC  // timing experiment only (wrong lengths): the walk without the escape gathers
+                if (pk[c]) g[c] = 18u + (pW[c] & 3u);
+#else
                 if (pk[c]) g[c] = a.esc[pW[c] >> (32 - a.m)];
+#endif
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (!pk[c]) continue;
