@@ -848,9 +848,9 @@ struct EventPair {
         for (auto x : e)
             if (x) (void)hipEventDestroy(x);
     }
-    int create() {
+    int create(bool timing = false) {
         for (auto& x : e)
-            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return HZ_EHIP;
+            if (hipEventCreateWithFlags(&x, timing ? hipEventDefault : hipEventDisableTiming) != hipSuccess) return HZ_EHIP;
         return HZ_OK;
     }
 };
@@ -903,6 +903,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     if (!fp) return HZ_EIO;
     std::unique_ptr<FILE, int (*)(FILE*)> fin(fp, fclose);
     // ---- pass 1: histogram (resident: the chunks stay in dall)
+    const auto t_hist = Clock::now();  // "Histograming took" (Compressor.cu:395-399): read + upload + histogram
     HZ_TRY(hipMemsetAsync(dhist.p, 0, HZ_NSYM * 8, c->stream));
     EventPair done;
     if ((rc = done.create())) return rc;
@@ -933,11 +934,15 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     std::vector<uint8_t> head;
     uint64_t dinfo_h[4] = {0, 0, 0, 0};
     DevBuf dcb, dhead, dinfo;
+    EventPair cbt;  // "construction time" (gpuHuffmanConstruction.h:776-782): the device codebook
+    if ((rc = cbt.create(true))) return rc;
     if (!host_cb) {
         if ((rc = dcb.alloc(sizeof(hz_codebook))) || (rc = dhead.alloc(kHeadCap)) || (rc = dinfo.alloc(4 * 8))) return rc;
         head.resize(kHeadCap);
         hipEvent_t t0 = spans.mark(c->stream);
+        HZ_TRY(hipEventRecord(cbt.e[0], c->stream));
         if ((rc = hz_codebook_build_device(c, (const uint64_t*)dhist.p, (hz_codebook*)dcb.p))) return rc;
+        HZ_TRY(hipEventRecord(cbt.e[1], c->stream));
         if ((rc = hz_header_write_device(c, (const hz_codebook*)dcb.p, n, last_byte, (uint8_t*)dhead.p, kHeadCap,
                                          (uint64_t*)dinfo.p)))
             return rc;
@@ -954,15 +959,24 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
         spans.add(t0, spans.mark(c->stream), &g_timing.d2h_ms);
     }
     if ((rc = hz_ctx_sync(c))) return rc;
+    const double hist_ms = ms_since(t_hist);
     const auto th = Clock::now();
     if (host_cb && (rc = hz_codebook_build(hist.data(), cb.get()))) return rc;
+    float cb_ms = 0.0f;
+    if (host_cb) cb_ms = (float)ms_since(th);
+    else HZ_TRY(hipEventElapsedTime(&cb_ms, cbt.e[0], cbt.e[1]));
     uint64_t hbits = 0, pbits = 0;
     hz_header_bits(cb.get(), n, &hbits);
     hz_payload_bits(cb.get(), hist.data(), &pbits);
-    if (verbose) {
+    if (verbose) {  // the reference's stdout lines, its stage timers included
         std::cout << "The size of the sum of ORIGINAL files is: " << n << " bytes" << std::endl;
         std::cout << "Unique symbols count: " << cb->nsym << std::endl;
+        std::cout << "Histograming took " << hist_ms << " ms" << std::endl;
+        printf("construction time: %.3f ms, symbols/s: %.3f\n", cb_ms,
+               cb_ms > 0 ? (float)cb->nsym / (cb_ms * 1e-3f) : 0.0f);
+        fflush(stdout);
     }
+    const auto t_enc = Clock::now();  // "Encoding took" (Compressor.cu:588-593): header, pack, payload out
     // ---- header
     uint64_t hb;
     uint32_t pend_bits;
@@ -1112,6 +1126,7 @@ static int hz_archive_stream_impl(const char* in_path, const char* out_path, uin
     spans.fold();
     if (written != (hbits + pbits + 7) / 8) return HZ_EFORMAT;
     if (verbose) {
+        std::cout << "Encoding took " << ms_since(t_enc) << " ms" << std::endl;
         std::cout << "The size of the COMPRESSED file is: " << written << " bytes" << std::endl;
         const float ratio = 100.0f * (float)written / (float)(n ? n : 1);
         std::cout << "Compressed file's size is [" << ratio << "%] of the original files." << std::endl;

@@ -364,21 +364,31 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
         const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
         xe = (T)xx;
-        // Every lane issues all 33 escape loads (lanes without a miss read
-        // esc[0], one coalesced address): a fixed load count keeps the waits
-        // of later loads and stores static. The escape table holds entries in
-        // the register format, so each load lands in its e[k] directly.
+        // The escape table holds entries in the register format. Every lane loads
+        // (lanes without a miss read esc[0], one coalesced address) and the blend is
+        // a v_bfi the compiler cannot turn back into a select: written as
+        // `miss ? esc[s] : e` the loads become 33 exec-masked branches (12.73-12.87
+        // vs 12.61-12.67 ms at 16 GiB Zipf, round 3 A/B); an empty asm forcing each
+        // loaded value at its load serialises the loads (18.9 ms).
         (void)any;
+        uint32_t v[kSPT], mk[kSPT];
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
-            const bool miss = (uint32_t)e[k] >> 31;
-            const uint32_t v = a.esc[miss ? (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu : 0u];
-            e[k] = miss ? (T)v : e[k];
+            mk[k] = 0u - ((uint32_t)e[k] >> 31);
+            v[k] = a.esc[((raw[k >> 1] >> (16 * (k & 1))) & 0xffffu) & mk[k]];
+        }
+        const uint32_t xmk = 0u - (xx >> 31);
+        const uint32_t xv = a.esc[xs & xmk];
+#pragma unroll
+        for (int k = 0; k < kSPT; ++k) {
+            uint32_t r;
+            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"((uint32_t)e[k]));
+            e[k] = (T)r;
         }
         {
-            const bool miss = xx >> 31;
-            const uint32_t v = a.esc[miss ? xs : 0u];
-            xe = miss ? (T)v : xe;
+            uint32_t r;
+            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(xmk), "v"(xv), "v"(xx));
+            xe = (T)r;
         }
     } else {
 #pragma unroll

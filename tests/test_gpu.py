@@ -122,6 +122,9 @@ def test_cli_archive_extract(hz, tmp_path):
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Compression is complete" in r.stdout and "Unique symbols count: 1268" in r.stdout
+    # the reference's stage timers (Compressor.cu:399, 593; gpuHuffmanConstruction.h:780-782)
+    for line in ("Histograming took ", "construction time: ", "Encoding took "):
+        assert line in r.stdout, r.stdout
     assert (tmp_path / "romeo.txt.compressed").read_bytes() == read("romeo.txt.compressed")
     r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "romeo.txt.compressed"], cwd=tmp_path,
                        capture_output=True, text=True, timeout=300)
@@ -185,6 +188,29 @@ def test_cli_archive_resident(hz, tmp_path, name, chunk):
     assert blob == (read(name + ".compressed") if name != "zipf" else oracle_lib.encode(data))
     r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "in.bin.compressed"], cwd=tmp_path,
                        capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
+
+
+@pytest.mark.parametrize("name", ["romeo.txt", "zipf", "odd"])
+@pytest.mark.parametrize("host", [False, True])
+def test_cli_device_and_host_codebook_paths(hz, tmp_path, name, host):
+    """`archive` builds the codebook and header on the device (k_cb_*, k_hw_*) unless
+    HZ_HOST_CODEBOOK=1; `extract` parses the header on the device (k_hdr_*) unless
+    HZ_HOST_HEADER=1, here with a 1 MiB payload window: both paths write the oracle's
+    archive and restore the input."""
+    data = {"romeo.txt": read("romeo.txt"), "zipf": _zipf_bytes((12 << 20) + 1, 21),
+            "odd": _skewed_bytes(6 << 20, 2) + b"\x07"}[name]
+    (tmp_path / "in.bin").write_bytes(data)
+    env = dict(os.environ, HZ_EXTRACT_WINDOW=str(1 << 20))
+    if host:
+        env.update(HZ_HOST_CODEBOOK="1", HZ_HOST_HEADER="1")
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "archive"), "in.bin"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "in.bin.compressed").read_bytes() == oracle_lib.encode(data)
+    r = subprocess.run([os.path.join(hz.BIN_DIR, "extract"), "in.bin.compressed"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
 
