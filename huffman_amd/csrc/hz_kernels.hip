@@ -1532,10 +1532,14 @@ HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte
 
 // Global table l2 as a buffer whose byte 0 lies kLutGlobal words before l2[0]:
 // the byte offset of a global link's entry is (raw + index bits) * 4, one
-// v_add_lshl_u32, and a chain resolved in LDS reads offset 4 * kLutGlobal = l2[0].
+// v_add_lshl_u32; num_records covers the largest table (kLutMaxL2 entries).
+// Lanes resolved in LDS read past num_records (0, no memory access) instead of l2[0]:
+// 12.27-12.29 vs 12.33-12.37 ms at 16 GiB Zipf (round 3, A/B in one run).
+constexpr uint32_t kL2Dummy = 0xfffffff0u;
 HZ_DEV __amdgpu_buffer_rsrc_t lut_l2_rsrc(const uint32_t* l2) {
     return __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(l2) - 4ull * kLutGlobal), 0, 0xffffffffu, 0x00020000);
+        reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(l2) - 4ull * kLutGlobal), 0,
+        4u * (kLutGlobal + kLutMaxL2), 0x00020000);
 }
 
 // The LDS steps of NC chains at once: all window reads, then all level-1
@@ -1570,7 +1574,7 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
         const uint32_t ee = h[c] ? x[c] : e[c];
         const uint32_t byte = ((ee >> 10) + __builtin_amdgcn_ubfe(W[c], ee, ee >> 5)) << 2;
         r[c].e = ee;
-        r[c].gi = lut_leaf(ee) ? 4u * kLutGlobal : byte;
+        r[c].gi = lut_leaf(ee) ? kL2Dummy : byte;
     }
 }
 

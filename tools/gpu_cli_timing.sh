@@ -1,4 +1,4 @@
-# GPU tests (archive/extract with reserved output files), then the 16 GiB CLI stage split
+# GPU tests of test_gpu.py (the CLIs among them), then the 16 GiB CLI stage split (tools/cli_timing.py)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests/test_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t10_tests.log 2>&1; rc=$?

@@ -1,4 +1,5 @@
-# device codebook tests, its phase profile (variant), the latency comparison and a kernel trace
+# device codebook / header GPU tests, the codebook phase profile (lib_cbprof variant), the device-vs-host latency
+# comparison (tools/cb_latency.py) and its kernel trace (needs: python huffman_amd/build.py --variant cbprof -DHZ_CB_PROF)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_codebook.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t8_tests.log 2>&1; rc=$?
