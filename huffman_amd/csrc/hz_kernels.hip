@@ -46,6 +46,14 @@ HZ_DEV uint64_t splitmix64(uint64_t x) {
 
 HZ_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+// One 16-byte non-temporal store (global_store_dwordx4 ... nt).
+HZ_DEV void store_nt16(uint4* p, uint4 v) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    __builtin_nontemporal_store(v.x, q);
+    __builtin_nontemporal_store(v.y, q + 1);
+    __builtin_nontemporal_store(v.z, q + 2);
+    __builtin_nontemporal_store(v.w, q + 3);
+}
 HZ_DEV uint32_t shfl_up_u32(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d, 64); }
 HZ_DEV uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
 HZ_DEV uint32_t shfl_xor_u32(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
@@ -322,9 +330,15 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
 // (bit 31) equals bit 15 of the symbol, i.e. when bit 31 of entry ^ tag is 0.
 // Misses (the slot holds the partner symbol) come from the escape table, all
 // issued before one wait. FULL: all 32 symbols valid (no per-symbol masking).
-template <int MODE, bool FULL>
+// mid() runs once the lookups' global loads are in flight and before any is
+// waited on (k_pack_write issues the previous block's stores there).
+struct NoMid {
+    HZ_DEV void operator()() const {}
+};
+template <int MODE, bool FULL, typename Mid = NoMid>
 HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, int nvalid, uint32_t (&raw)[kSPT / 2],
-                        typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe) {
+                        typename PackEnt<MODE>::T (&e)[kSPT], uint32_t xs, typename PackEnt<MODE>::T& xe,
+                        Mid mid = Mid()) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     if (!FULL) {
@@ -349,6 +363,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             e[k] = ((FULL || k < nvalid) && f) ? (T)((L << SH) | (f >> (17u - L))) : (T)0;
         }
         xe = pack_dense_one<T, SH>(lds, xs);
+        mid();
     } else if constexpr (MODE == ENC_HOT) {
         const uint32_t m = a.hot_mask;
         uint32_t any = 0;
@@ -379,6 +394,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         }
         const uint32_t xmk = 0u - (xx >> 31);
         const uint32_t xv = a.esc[xs & xmk];
+        mid();
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             uint32_t r;
@@ -397,6 +413,7 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
             e[k] = (FULL || k < nvalid) ? (T)a.wide[s] : (T)0;
         }
         xe = (T)a.wide[xs];
+        mid();
     }
 }
 
@@ -541,13 +558,63 @@ struct PackBlk {
     int nvalid;
 };
 
-template <int MODE>
+template <int MODE, typename Mid = NoMid>
 HZ_DEV void pack_block_lookup(const PackArgs& a, const uint32_t* lds, uint64_t blk, int lane, PackIn& in,
-                              PackBlk<MODE>& b) {
+                              PackBlk<MODE>& b, Mid mid = Mid()) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     b.nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
-    if (b.nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe);
-    else pack_lookup<MODE, false>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe);
+    if (b.nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
+    else pack_lookup<MODE, false>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
+}
+
+// A block whose words wait in the wave's LDS slot: its global stores (payload
+// copy-out and index entries) are issued during the NEXT block's lookup, after
+// that block's escape loads. On gfx9 stores count in vmcnt and loads wait in
+// order behind them, so stores issued just before a load wait stall the wave for
+// their write latency; deferred, they complete under a whole block of work.
+struct PackOut {
+    bool pending, fits;
+    uint64_t base4, blk, bstart, sub;
+    uint32_t sh4, nwords;
+};
+
+HZ_DEV void pack_copyout(const PackArgs& a, const uint32_t* slot, int lane, const PackOut& p) {
+    if (!p.pending) return;
+    if (p.fits) {
+        // Output words [wfirst, wfirst + nwords): a partial first 16-byte chunk
+        // (its words before wfirst are the previous block's), whole chunks,
+        // a partial last chunk. A fixed count of stores (1 + 4 + 1; lanes with
+        // nothing to write rewrite the block's first word with its own value),
+        // so later load waits count them statically. nwords >= 64.
+        const uint32_t sh4 = p.sh4;
+        const uint32_t wend = sh4 + p.nwords;                // slot index past the block
+        const uint32_t cf = sh4 ? 1u : 0u, cl = wend >> 2;  // whole chunks [cf, cl)
+        const uint32_t nhead = sh4 ? 4u - sh4 : 0u, ntail = wend & 3u;
+        {
+            const uint32_t i = (uint32_t)lane < nhead ? sh4 + (uint32_t)lane : sh4;
+            a.out[p.base4 + i] = bswap32(slot[i]);
+        }
+#pragma unroll
+        for (int it = 0; it < kPackCopyIters / 4; ++it) {
+            uint32_t c = cf + (uint32_t)lane + (uint32_t)it * kWave;
+            c = c < cl ? c : cl - 1;
+            const uint4 v = reinterpret_cast<const uint4*>(slot)[c];
+#ifdef HZ_EXP_PACK_NT
+            store_nt16(reinterpret_cast<uint4*>(a.out + p.base4) + c, make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)));
+#else
+            reinterpret_cast<uint4*>(a.out + p.base4)[c] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+#endif
+        }
+        {
+            const uint32_t i = (uint32_t)lane < ntail ? 4u * cl + (uint32_t)lane : sh4;
+            a.out[p.base4 + i] = bswap32(slot[i]);
+        }
+    }
+    if (a.index) {
+        a.index_sub[p.blk * kWave + lane] = p.sub;
+        if (lane == 0) a.index[p.blk] = p.bstart;
+    }
+    __builtin_amdgcn_wave_barrier();  // the slot's reads complete before the next emit rewrites it
 }
 
 // Lane bits, decode-chain offsets, wave scan of the bit counts.
@@ -569,7 +636,7 @@ HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
 // Writes block `blk` starting at absolute bit `bstart`, plus its index entries.
 template <int MODE>
 HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int lane, const PackBlk<MODE>& b,
-                            uint64_t bstart, uint64_t& max_bits) {
+                            uint64_t bstart, uint64_t& max_bits, PackOut* defer = nullptr) {
     using T = typename PackEnt<MODE>::T;
     constexpr int SH = PackEnt<MODE>::kShift;
     constexpr T CMASK = (T(1) << SH) - 1;
@@ -621,7 +688,27 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
         const uint32_t h = (uint32_t)(o & 31);
         if (h) sl[(uint32_t)((o >> 5) - wfirst)] |= prev << (32 - h);
         __builtin_amdgcn_wave_barrier();
+        if (MODE != ENC_WIDE && defer) {
+            defer->pending = true;
+            defer->fits = fits;
+            defer->base4 = wfirst & ~3ull;
+            defer->sh4 = sh4;
+            defer->nwords = nwords;
+            defer->blk = blk;
+            defer->bstart = bstart;
+            uint64_t sub = 0;
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c)
+                sub |= (uint64_t)(((uint32_t)bstart + ex_n + b.nc[c]) & 0xffffu) << (16 * c);
+            defer->sub = sub;
+            max_bits = b.bits > max_bits ? b.bits : max_bits;
+            return;
+        }
+#ifdef HZ_EXP_PACK_NOSTORE  // timing experiment only: no payload stores on the slot path
+        if (fits && a.nsym == 3) {
+#else
         if (fits) {
+#endif
             if constexpr (MODE != ENC_WIDE) {  // host: slot_words <= kPackCopyIters * kWave
                 // Output words [wfirst, wfirst + nwords): a partial first 16-byte chunk
                 // (its words before wfirst are the previous block's), whole chunks,
@@ -696,6 +783,10 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     }
 }
 
+#ifndef HZ_PACK_DEFER
+#define HZ_PACK_DEFER 1
+#endif
+constexpr bool kPackDefer = HZ_PACK_DEFER;
 // Three-pass pack (after k_pack_count + k_scan_*): block starts are known.
 template <int MODE>
 __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
@@ -711,15 +802,20 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     PackIn nx;  // the next block's inputs, in flight while this block is packed
     if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
+    PackOut po;
+    po.pending = false;
     for (; blk < a.nblocks; blk += W) {
         PackIn cur = nx;
         PackBlk<MODE> b;
-        pack_block_lookup<MODE>(a, lds, blk, lane, cur, b);
+        // the previous block's stores go out behind this block's escape loads
+        pack_block_lookup<MODE>(a, lds, blk, lane, cur, b, [&]() { pack_copyout(a, slot, lane, po); });
+        po.pending = false;
         // next block's loads: after this block's escapes, so no wait covers them early
         pack_prefetch(a, blk + W < a.nblocks ? blk + W : blk, lane, nx);
         pack_block_count<MODE>(lane, b);
-        pack_block_emit<MODE>(a, slot, blk, lane, b, cur.bstart, max_bits);
+        pack_block_emit<MODE>(a, slot, blk, lane, b, cur.bstart, max_bits, kPackDefer ? &po : nullptr);
     }
+    pack_copyout(a, slot, lane, po);
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
@@ -1323,43 +1419,74 @@ HZ_DEV void dec_stage(const DecArgs& a, uint64_t b0, uint64_t b1, uint32_t npc_m
     }
 }
 
-// Chain start bits of the lane relative to the block start: index sub[] holds
-// the low 16 bits of each chain's stream bit, bs the block's start bit; the
-// offsets are mod 2^16, rebuilt from deltas when the block is that long.
-HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bs, uint64_t bits, int lane, uint32_t (&off)[kChainsPerLane]) {
+// Chain slot c of lane l decodes the block's chain 64 c + l (its symbols 8 (64 c + l) .. + 7), so the
+// lane's chain-c symbols are the 16 output bytes at 1024 c + 16 l and each of a block's four output stores
+// covers 1 KiB (lane-major chains -- the lane's 32 symbols as 64 contiguous bytes -- left every store
+// touching 64 separate 64-byte pieces: 12.3 vs 11.15 ms at 16 GiB Zipf, round 3 A/B). The index keeps
+// its layout (sub[b * 64 + l] = chains 4 l .. 4 l + 3), so a lane reads its four chain starts as u16s.
+HZ_DEV uint64_t dec_sub_load(const DecArgs& a, uint64_t b, int lane) {
+#ifdef HZ_EXP_DEC_SUB1  // timing experiment only (wrong chain starts): one u64 load per lane
+    return a.subs[b * kWave + lane];
+#endif
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(a.subs) + b * kChainsPerBlock + (uint32_t)lane;
+    return (uint64_t)s16[0] | ((uint64_t)s16[64] << 16) | ((uint64_t)s16[128] << 32) | ((uint64_t)s16[192] << 48);
+}
+
+// Chain start bits relative to the block start (chain 64 c + l in slot c of lane l): sub holds the
+// low 16 bits of each chain's stream bit, bs the block's start bit; offsets are mod 2^16, rebuilt from
+// deltas when the block is that long.
+HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bs, uint64_t bits, int lane,
+                                   uint32_t (&off)[kChainsPerLane]) {
     constexpr int C = kChainsPerLane;
 #pragma unroll
     for (int c = 0; c < C; ++c) off[c] = ((uint32_t)(sub >> (16 * c)) - (uint32_t)bs) & 0xffffu;
-    if (bits >= 65536) {
-        uint32_t pv = shfl_up_u32(off[C - 1], 1);
-        if (lane == 0) pv = 0;
-        uint32_t d[C], sc = 0;
+    if (bits >= 65536) {  // rebuild from deltas in chain order: (c, l - 1) precedes (c, l), (c - 1, 63) (c, 0)
+        uint32_t carry = 0, last = 0;
 #pragma unroll
-        for (int c = 0; c < C; ++c) { d[c] = (off[c] - pv) & 0xffffu; pv = off[c]; sc += d[c]; }
+        for (int c = 0; c < C; ++c) {
+            uint32_t pv = shfl_up_u32(off[c], 1);
+            if (lane == 0) pv = last;
+            last = __builtin_amdgcn_readlane(off[c], 63);
+            uint32_t sc = (off[c] - pv) & 0xffffu;
 #pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-            const uint32_t o = shfl_up_u32(sc, dd);
-            if (lane >= dd) sc += o;
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t o = shfl_up_u32(sc, dd);
+                if (lane >= dd) sc += o;
+            }
+            off[c] = carry + sc;
+            carry = __builtin_amdgcn_readlane(off[c], 63);
         }
-#pragma unroll
-        for (int c = C - 1; c >= 0; --c) { off[c] = sc; sc -= d[c]; }
     }
 }
 
-// 32 symbols = 64 contiguous output bytes of the lane in block b.
 HZ_DEV void dec_store(const DecArgs& a, uint64_t b, int lane, const uint32_t* pk) {
-    const uint64_t sym0 = b * kBlockSyms + (uint64_t)lane * kSPT;
-    if (sym0 + kSPT <= a.nsym) {
-        uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0);
+    const uint64_t sym0 = b * kBlockSyms;
+#ifdef HZ_EXP_DEC_NOSTORE  // timing experiment only: no output
+    uint32_t x = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
-    } else if (sym0 < a.nsym) {
-        uint8_t* ob = a.out + 2 * sym0;
-        const uint32_t cnt = (uint32_t)(a.nsym - sym0);
-        for (uint32_t q = 0; q < cnt; ++q) {
-            const uint32_t v = (pk[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-            ob[2 * q] = (uint8_t)v;
-            ob[2 * q + 1] = (uint8_t)(v >> 8);
+    for (int i = 0; i < kSPT / 2; ++i) x ^= pk[i];
+    if (x == 0x9e3779b9u && a.nsym == 3) a.out[0] = 1;
+    return;
+#endif
+    if (sym0 + kBlockSyms <= a.nsym) {
+        // non-temporal (streaming) stores: the output is not read again by this kernel
+        // (10.70 vs 11.15-11.37 ms at 16 GiB Zipf, round 3 A/B)
+        uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0) + lane;
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c)
+            store_nt16(o + c * kWave, make_uint4(pk[4 * c], pk[4 * c + 1], pk[4 * c + 2], pk[4 * c + 3]));
+    } else {
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) {
+            const uint64_t s0 = sym0 + (uint64_t)kChainSyms * (uint32_t)(c * kWave + lane);
+            if (s0 >= a.nsym) continue;
+            uint8_t* ob = a.out + 2 * s0;
+            const uint32_t cnt = a.nsym - s0 < (uint64_t)kChainSyms ? (uint32_t)(a.nsym - s0) : kChainSyms;
+            for (uint32_t q = 0; q < cnt; ++q) {
+                const uint32_t v = (pk[4 * c + (q >> 1)] >> (16 * (q & 1))) & 0xffffu;
+                ob[2 * q] = (uint8_t)v;
+                ob[2 * q + 1] = (uint8_t)(v >> 8);
+            }
         }
     }
 }
@@ -1378,7 +1505,7 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
     for (int g = 0; g < NB; ++g) {
         const uint64_t b = bfirst + g < a.nblocks ? bfirst + g : a.nblocks - 1;  // duplicates decode, never store
         const uint64_t b0 = a.starts[b] + a.bit_adj, b1 = a.starts[b + 1] + a.bit_adj;
-        const uint64_t sub = a.subs[b * kWave + lane];
+        const uint64_t sub = dec_sub_load(a, b, lane);
         uint64_t w0;
         dec_stage<WIDE>(a, b0, b1, npc_max, stg0 + g * slot, lane, w0);
         uint32_t off[C1];
@@ -1587,7 +1714,7 @@ HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
     const uint64_t bb = b < a.nblocks ? b : a.nblocks - 1;  // past the end: any block, never used
     m.b0 = a.starts[bb];
     m.b1 = a.starts[bb + 1];
-    m.sub = a.subs[bb * kWave + lane];
+    m.sub = dec_sub_load(a, bb, lane);
 }
 
 // The first kStageUnroll 16-byte chunks of a block's staging window, always
@@ -1725,6 +1852,11 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mc[j], lane, sc[j]);
+#ifdef HZ_EXP_DEC_STDLY
+    uint32_t pkp[2][kSPT / 2];
+    uint64_t bprev = 0;
+    bool have_prev = false;
+#endif
     for (; b < a.nblocks; b += stride) {
         uint32_t p1[C];
 #pragma unroll
@@ -1759,6 +1891,13 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
             issue4(4);
+#ifdef HZ_EXP_DEC_STDLY  // the previous pair's stores issued behind this pair's first 8 gathers
+            if (q == 0 && have_prev) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    if (bprev + j < a.nblocks) dec_store(a, bprev + j, lane, pkp[j]);
+            }
+#endif
             if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
@@ -1772,6 +1911,15 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             for (int c = 4; c < 8; ++c) finish(c, q);
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef HZ_EXP_DEC_STDLY
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < kSPT / 2; ++i) pkp[j][i] = pk[j][i];
+        bprev = b;
+        have_prev = true;
+        if (false)
+#endif
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             if (b + j < a.nblocks) dec_store(a, b + j, lane, pk[j]);
@@ -1783,6 +1931,13 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             for (int u = 0; u < kStageUnroll; ++u) sc[j][u] = sn[j][u];
         }
     }
+#ifdef HZ_EXP_DEC_STDLY
+    if (have_prev) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (bprev + j < a.nblocks) dec_store(a, bprev + j, lane, pkp[j]);
+    }
+#endif
 }
 
 constexpr int kDecPipe2Threads = 512;  // two staging slots per wave (1024 with smaller hot heads: 15.2 ms vs 13.1)
