@@ -599,11 +599,7 @@ HZ_DEV void pack_copyout(const PackArgs& a, const uint32_t* slot, int lane, cons
             uint32_t c = cf + (uint32_t)lane + (uint32_t)it * kWave;
             c = c < cl ? c : cl - 1;
             const uint4 v = reinterpret_cast<const uint4*>(slot)[c];
-#ifdef HZ_EXP_PACK_NT
-            store_nt16(reinterpret_cast<uint4*>(a.out + p.base4) + c, make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w)));
-#else
             reinterpret_cast<uint4*>(a.out + p.base4)[c] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
-#endif
         }
         {
             const uint32_t i = (uint32_t)lane < ntail ? 4u * cl + (uint32_t)lane : sh4;
@@ -1425,9 +1421,6 @@ HZ_DEV void dec_stage(const DecArgs& a, uint64_t b0, uint64_t b1, uint32_t npc_m
 // touching 64 separate 64-byte pieces: 12.3 vs 11.15 ms at 16 GiB Zipf, round 3 A/B). The index keeps
 // its layout (sub[b * 64 + l] = chains 4 l .. 4 l + 3), so a lane reads its four chain starts as u16s.
 HZ_DEV uint64_t dec_sub_load(const DecArgs& a, uint64_t b, int lane) {
-#ifdef HZ_EXP_DEC_SUB1  // timing experiment only (wrong chain starts): one u64 load per lane
-    return a.subs[b * kWave + lane];
-#endif
     const uint16_t* s16 = reinterpret_cast<const uint16_t*>(a.subs) + b * kChainsPerBlock + (uint32_t)lane;
     return (uint64_t)s16[0] | ((uint64_t)s16[64] << 16) | ((uint64_t)s16[128] << 32) | ((uint64_t)s16[192] << 48);
 }
@@ -1852,11 +1845,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mc[j], lane, sc[j]);
-#ifdef HZ_EXP_DEC_STDLY
-    uint32_t pkp[2][kSPT / 2];
-    uint64_t bprev = 0;
-    bool have_prev = false;
-#endif
     for (; b < a.nblocks; b += stride) {
         uint32_t p1[C];
 #pragma unroll
@@ -1891,13 +1879,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
             issue4(4);
-#ifdef HZ_EXP_DEC_STDLY  // the previous pair's stores issued behind this pair's first 8 gathers
-            if (q == 0 && have_prev) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    if (bprev + j < a.nblocks) dec_store(a, bprev + j, lane, pkp[j]);
-            }
-#endif
             if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
@@ -1911,15 +1892,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             for (int c = 4; c < 8; ++c) finish(c, q);
         }
         __builtin_amdgcn_wave_barrier();
-#ifdef HZ_EXP_DEC_STDLY
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < kSPT / 2; ++i) pkp[j][i] = pk[j][i];
-        bprev = b;
-        have_prev = true;
-        if (false)
-#endif
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             if (b + j < a.nblocks) dec_store(a, b + j, lane, pk[j]);
@@ -1931,13 +1903,6 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             for (int u = 0; u < kStageUnroll; ++u) sc[j][u] = sn[j][u];
         }
     }
-#ifdef HZ_EXP_DEC_STDLY
-    if (have_prev) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (bprev + j < a.nblocks) dec_store(a, bprev + j, lane, pkp[j]);
-    }
-#endif
 }
 
 constexpr int kDecPipe2Threads = 512;  // two staging slots per wave (1024 with smaller hot heads: 15.2 ms vs 13.1)
@@ -2683,10 +2648,15 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         for (int c = 0; c < C; ++c) {
             if (!fl[c]) continue;
             const uint64_t j = seg0[c] * (kSegBits / 128) + mcount[c];
+#ifdef HZ_EXP_WALK_NOSTORE  // timing experiment only: no bitmap stores
+            if ((mcount[c] & (GM - 1)) == GM - 1 && a.nseg == 3) {
+#else
             if ((mcount[c] & (GM - 1)) == GM - 1) {
+#endif
                 uint4* dst = reinterpret_cast<uint4*>(a.bmp) + (j - (GM - 1));
 #pragma unroll
-                for (uint32_t i = 0; i < GM; ++i) dst[i] = mk[c][i];
+                for (uint32_t i = 0; i < GM; ++i)
+                    store_nt16(dst + i, mk[c][i]);  // read back by k_sync_select only (16.0 vs 16.3 ms walk, round 3)
             }
             if ((mcount[c] & 31) == 31) a.cnt[j >> 5] = rc[c];
             ++mcount[c];
@@ -2931,6 +2901,9 @@ static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long*
         if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         if (*h_changed == 0 || it > (int)y.nseg) break;
+#ifdef HZ_EXP_WALK_NOSTORE  // the experiment's bitmap is garbage: no fixed point to reach
+        if (it >= 1) break;
+#endif
     }
     const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
