@@ -389,16 +389,27 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         uint32_t v[kSPT], mk[kSPT];
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
+#ifdef HZ_EXP_PACK_NOESC  // timing experiment only (wrong codes): no escape loads
+            mk[k] = 0u;
+#else
             mk[k] = 0u - ((uint32_t)e[k] >> 31);
+#endif
             v[k] = a.esc[((raw[k >> 1] >> (16 * (k & 1))) & 0xffffu) & mk[k]];
         }
+#ifdef HZ_EXP_PACK_NOESC
+        const uint32_t xmk = 0u;
+#else
         const uint32_t xmk = 0u - (xx >> 31);
+#endif
         const uint32_t xv = a.esc[xs & xmk];
         mid();
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             uint32_t r;
             asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"((uint32_t)e[k]));
+#ifdef HZ_EXP_PACK_NOESC
+            r &= 0x7fffffffu;
+#endif
             e[k] = (T)r;
         }
         {
@@ -563,8 +574,13 @@ HZ_DEV void pack_block_lookup(const PackArgs& a, const uint32_t* lds, uint64_t b
                               PackBlk<MODE>& b, Mid mid = Mid()) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     b.nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
-    if (b.nvalid == kSPT) pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
-    else pack_lookup<MODE, false>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
+    // a wave-uniform choice: mid() may run wave-wide code (DPP scans of the pipelined emit), so it
+    // must not run once per branch of a divergent split (the stream's last block mixes full and
+    // partial lanes; the partial path handles full lanes too)
+    if (__ballot(b.nvalid != kSPT) == 0)
+        pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
+    else
+        pack_lookup<MODE, false>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
 }
 
 // A block whose words wait in the wave's LDS slot: its global stores (payload
@@ -783,6 +799,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
 #define HZ_PACK_DEFER 1
 #endif
 constexpr bool kPackDefer = HZ_PACK_DEFER;
+
 // Three-pass pack (after k_pack_count + k_scan_*): block starts are known.
 template <int MODE>
 __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
@@ -1295,6 +1312,9 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 // Every code 16 bits (FIXED16): symbol i sits at bit start + 16 i, so that
 // decoder needs no index and no staging (k_decode_fixed16).
 // ===========================================================================
+#ifndef HZ_DEC_PERM
+#define HZ_DEC_PERM 1  // pipelined decoder: two symbols packed by one v_perm (A/B switch)
+#endif
 struct DecArgs {
     const uint32_t* words;   // payload view, 64-byte aligned
     uint64_t nwords;
@@ -1864,16 +1884,26 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         auto finish = [&](int c, int q) {
             const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
             p1[c] += (ee >> 16) & 63u;
-            const uint32_t sym = ee & 0xffffu;
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
-            if (q & 1) pk[c / kChainsPerLane][i] |= sym << 16;
-            else pk[c / kChainsPerLane][i] = sym;
+            // an even step keeps the whole entry; the odd step packs both symbols (low halves) by one v_perm
+#if HZ_DEC_PERM
+            if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x05040100u);
+            else pk[c / kChainsPerLane][i] = ee;
+#else
+            if (q & 1) pk[c / kChainsPerLane][i] |= ee << 16;
+            else pk[c / kChainsPerLane][i] = ee & 0xffffu;
+#endif
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
         auto issue4 = [&](int c) {
             dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
+            for (int t = 0; t < 4; ++t)
+#ifdef HZ_EXP_DEC_NOGATHER  // timing experiment only (wrong symbols): no level-2 gathers
+                g[c + t] = st[c + t].gi ^ 0x80000000u;
+#else
+                g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
+#endif
         };
         issue4(0);
 #pragma unroll
@@ -2744,6 +2774,10 @@ constexpr int kSelectThreads = 256;
 constexpr uint32_t kSelTileSegs = 16;
 constexpr uint32_t kSelTileWords = kSelTileSegs * kBmpWords;  // 2048 = 8 words per thread
 constexpr uint32_t kSelMaxChains = kSelTileWords * 32 / kChainSyms + 2;
+#ifndef HZ_SEL_AHEAD
+#define HZ_SEL_AHEAD 1
+#endif
+constexpr int kSelAhead = HZ_SEL_AHEAD;
 __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint64_t nsym, uint64_t nblocks,
                                                                 const unsigned long long* first,
                                                                 unsigned long long* starts, uint16_t* subs) {
@@ -2766,16 +2800,26 @@ __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint
             for (int i = 0; i < 8; ++i) mm[i] = w0 + i < nw ? y.bmp[w0 + i] : 0u;
         }
     };
-    uint64_t fn = 0;
-    uint32_t mn[8];
-    if (blockIdx.x < ntile) load(blockIdx.x, fn, mn);
+    // kSelAhead tiles in flight per thread (16 GiB Zipf: 1 / 3 / 5 ahead 4.61 / 4.89 / 5.03 ms, round 3)
+    uint64_t fn[kSelAhead] = {};
+    uint32_t mn[kSelAhead][8];
+#pragma unroll
+    for (int d = 0; d < kSelAhead; ++d)
+        if (blockIdx.x + d * (uint64_t)gridDim.x < ntile) load(blockIdx.x + d * (uint64_t)gridDim.x, fn[d], mn[d]);
     for (uint64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
         const uint64_t seg0 = tile * kSelTileSegs;
-        const uint64_t f0 = fn;
+        const uint64_t f0 = fn[0];
         uint32_t m[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = mn[i];
-        if (tile + gridDim.x < ntile) load(tile + gridDim.x, fn, mn);
+        for (int i = 0; i < 8; ++i) m[i] = mn[0][i];
+#pragma unroll
+        for (int d = 0; d + 1 < kSelAhead; ++d) {
+            fn[d] = fn[d + 1];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mn[d][i] = mn[d + 1][i];
+        }
+        if (tile + kSelAhead * (uint64_t)gridDim.x < ntile)
+            load(tile + kSelAhead * (uint64_t)gridDim.x, fn[kSelAhead - 1], mn[kSelAhead - 1]);
         if (f0 > nsym) break;  // workgroup-uniform; later tiles start later still
         const uint64_t w0 = seg0 * kBmpWords + 8u * threadIdx.x;
         uint32_t c[8], tot = 0;
