@@ -1312,6 +1312,12 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 // Every code 16 bits (FIXED16): symbol i sits at bit start + 16 i, so that
 // decoder needs no index and no staging (k_decode_fixed16).
 // ===========================================================================
+#ifndef HZ_DEC_LEAF_OOB
+#define HZ_DEC_LEAF_OOB 1
+#endif
+#ifndef HZ_DEC_DESC
+#define HZ_DEC_DESC 1
+#endif
 #ifndef HZ_DEC_PERM
 #define HZ_DEC_PERM 1  // pipelined decoder: two symbols packed by one v_perm (A/B switch)
 #endif
@@ -1676,6 +1682,7 @@ HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte
 // Lanes resolved in LDS read past num_records (0, no memory access) instead of l2[0]:
 // 12.27-12.29 vs 12.33-12.37 ms at 16 GiB Zipf (round 3, A/B in one run).
 constexpr uint32_t kL2Dummy = 0xfffffff0u;
+static_assert(kLutGlobal + kLutMaxL2 == (1u << 21), "a leaf (bit 31) read as a link lands past num_records");
 HZ_DEV __amdgpu_buffer_rsrc_t lut_l2_rsrc(const uint32_t* l2) {
     return __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(l2) - 4ull * kLutGlobal), 0,
@@ -1695,8 +1702,15 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
     bool h[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+#if HZ_DEC_DESC
+        // descending slot (dec_stage_commit<true>): p1 holds m, stream word t + 1 at byte (m >> 3) & ~3,
+        // word t just above it, and m & 31 is the funnel shift (no v_not per step)
+        const uint32_t wb = (p1[c] >> 3) & ~3u;
+        W[c] = __builtin_amdgcn_alignbit(lds_at(wb + 4), lds_at(wb), p1[c]);
+#else
         const uint32_t wb = (p1[c] >> 3) & ~3u;
         W[c] = __builtin_amdgcn_alignbit(lds_at(wb), lds_at(wb + 4), ~p1[c]);
+#endif
     }
     HZ_WALK_FENCE();
 #pragma unroll
@@ -1714,7 +1728,13 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
         const uint32_t ee = h[c] ? x[c] : e[c];
         const uint32_t byte = ((ee >> 10) + __builtin_amdgcn_ubfe(W[c], ee, ee >> 5)) << 2;
         r[c].e = ee;
+#if HZ_DEC_LEAF_OOB
+        // a leaf's byte offset is >= 4 (2^31 >> 10) = num_records of lut_l2_rsrc: the load returns 0
+        // without a memory access, as kL2Dummy did, with no select
+        r[c].gi = byte;
+#else
         r[c].gi = lut_leaf(ee) ? kL2Dummy : byte;
+#endif
     }
 }
 
@@ -1751,6 +1771,8 @@ HZ_DEV uint32_t pick4(const uint4& v, uint32_t i) {
 
 // Writes the prefetched chunks (fixed up for the payload's end) and any
 // further chunks of an oversized window into the slot.
+// DESC: the slot holds the words in descending order (stream word t at slot word 4 npc_max - 1 - t).
+template <bool DESC = false>
 HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_max, uint32_t* stg, int lane,
                              const uint4 (&v)[kStageUnroll], uint64_t& w0) {
     const uint64_t b0 = m.b0 + a.bit_adj, b1 = m.b1 + a.bit_adj;
@@ -1774,12 +1796,18 @@ HZ_DEV void dec_stage_commit(const DecArgs& a, const PipeMeta& m, uint32_t npc_m
                 }
                 x = make_uint4(q[0], q[1], q[2], q[3]);
             }
-            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+            if (DESC)
+                reinterpret_cast<uint4*>(stg)[npc_max - 1 - p] = make_uint4(bswap32(x.w), bswap32(x.z), bswap32(x.y), bswap32(x.x));
+            else
+                reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
         }
     }
     for (uint32_t p = (uint32_t)lane + kStageUnroll * kWave; p < npc; p += kWave) {  // oversized block: rare
         const uint4 x = dec_stage_load(a, w0 + 4ull * p);
-        reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+        if (DESC)
+            reinterpret_cast<uint4*>(stg)[npc_max - 1 - p] = make_uint4(bswap32(x.w), bswap32(x.z), bswap32(x.y), bswap32(x.x));
+        else
+            reinterpret_cast<uint4*>(stg)[p] = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
     }
 }
 
@@ -1855,7 +1883,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
     constexpr int C = 2 * kChainsPerLane;
     static_assert(kChainsPerLane == 4, "four pairs of chains over two blocks");
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(a.l2);
-    const uint32_t stg_bit = (uint32_t)(stg - lds) * 32u - 1u;  // LDS bit address of the slots, minus 1
+    [[maybe_unused]] const uint32_t stg_bit = (uint32_t)(stg - lds) * 32u - 1u;  // LDS bit address of the slots, minus 1
     PipeMeta mc[2], mn[2], mn2[2];
     uint4 sc[2][kStageUnroll], sn[2][kStageUnroll];
 #pragma unroll
@@ -1870,12 +1898,21 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint64_t w0;
-            dec_stage_commit(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
+            dec_stage_commit<HZ_DEC_DESC>(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
             uint32_t off[kChainsPerLane];
             dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
+#if HZ_DEC_DESC
+            // m = (E - 1) * 32 + 31 - r for the slot's top word E and r = the chain's next bit - 1,
+            // relative to stream word w0; a step of L bits subtracts L
+            const uint32_t top = (uint32_t)(stg - lds) + (uint32_t)(j + 1) * slot - 1u;
+            const uint32_t base = top * 32u - (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5));
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base - off[c];
+#else
             const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u + stg_bit;
 #pragma unroll
             for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base + off[c];
+#endif
         }
         __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
         uint32_t pk[2][kSPT / 2];
@@ -1883,7 +1920,11 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         uint32_t g[C];
         auto finish = [&](int c, int q) {
             const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
+#if HZ_DEC_DESC
+            p1[c] -= (ee >> 16) & 63u;
+#else
             p1[c] += (ee >> 16) & 63u;
+#endif
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
             // an even step keeps the whole entry; the odd step packs both symbols (low halves) by one v_perm
 #if HZ_DEC_PERM
