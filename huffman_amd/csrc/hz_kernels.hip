@@ -46,6 +46,10 @@ HZ_DEV uint64_t splitmix64(uint64_t x) {
 
 HZ_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+// 16 bytes at a 4-byte aligned address (global_load/store_dwordx4 need only dword alignment): the
+// FIXED16 block kernels move a stream that starts at any word behind the header.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
 // One 16-byte non-temporal store (global_store_dwordx4 ... nt).
 HZ_DEV void store_nt16(uint4* p, uint4 v) {
     uint32_t* q = reinterpret_cast<uint32_t*>(p);
@@ -64,7 +68,11 @@ HZ_DEV uint32_t dpp0(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
 }
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
-constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
+#ifndef HZ_FIXED16_BLK
+#define HZ_FIXED16_BLK 1
+#endif
+constexpr bool kFixed16Blk = HZ_FIXED16_BLK;  // FIXED16 streams: the 1 KiB-coalesced full-block kernels
 
 // Inclusive prefix sum over the 64 lanes.
 HZ_DEV uint32_t wave_incl_sum(uint32_t v) {
@@ -1022,7 +1030,73 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_lb(PackArgs a, LbArg
 // Symbol i starts at bit start_bit + 16 i: no count pass and no scan. Lane j
 // packs symbols [32 j, 32 j + 32) into the 16 words whose last bit lies in its
 // run; word t is a funnel shift of code pairs t-1 and t by start_bit % 32.
-__global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint64_t start_bit) {
+// Full blocks [0, nb) of a FIXED16 stream: one wave per block; lane l's sub-run c is the block's symbols 8 (64 c + l) .. + 7, i.e. 16 input bytes and 4
+// output words at 1 KiB-coalesced offsets (the lane-run kernel below moves 64 contiguous bytes per
+// lane, so each of its 16-byte accesses touches 64 separate pieces). Word t of a sub-run is a funnel
+// shift of code pairs t - 1 and t; pair -1 is lane l - 1's last (DPP), sub-run c - 1's lane 63 for
+// lane 0, or, for the block's first, the pair before the block (loaded) or the header's pending bits.
+__global__ __launch_bounds__(kPackThreads) void k_pack_fixed16_blk(PackArgs a, uint64_t start_bit, uint64_t nb) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    load_lds_table<ENC_FIXED16>(lds, a.lds_img, a.lds_words);
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(lds);
+    const uint32_t sb = (uint32_t)(start_bit & 31);
+    const int lane = threadIdx.x & 63;
+    const uint4* in4 = reinterpret_cast<const uint4*>(a.in);
+    u32x4a4* out4 = reinterpret_cast<u32x4a4*>(a.out + (start_bit >> 5));  // any word of the stream
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    auto load = [&](uint64_t bb, uint4 (&x)[kChainsPerLane]) {
+        bb = bb < nb ? bb : 0;
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) x[c] = in4[bb * (kBlockSyms / 8) + c * kWave + lane];
+    };
+    uint4 nx[kChainsPerLane];
+    if (b < nb) load(b, nx);
+    for (; b < nb; b += W) {
+        uint4 x[kChainsPerLane];
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) x[c] = nx[c];
+        load(b + W, nx);
+        uint32_t p0 = a.lead;  // the pair before the block (same address on every lane)
+        if (b > 0) {
+            const uint32_t pr = *reinterpret_cast<const uint32_t*>(a.in + 2 * (b * kBlockSyms - 2));
+            p0 = ((uint32_t)c16[pr & 0xffffu] << 16) | c16[pr >> 16];
+        }
+        uint32_t last = p0;  // sub-run c - 1's last pair on lane 63 (wave-uniform)
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) {
+            const uint32_t raw[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+            uint32_t v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = ((uint32_t)c16[raw[t] & 0xffffu] << 16) | c16[raw[t] >> 16];
+            uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[3], kDppWaveShr1, 0xf, 0xf, false);
+            if (lane == 0) prev = last;
+            last = readlane(v[3], 63);
+            uint32_t o[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t pp = t ? v[t - 1] : prev;
+                o[t] = sb ? __builtin_amdgcn_alignbit(pp, v[t], sb) : v[t];
+            }
+            u32x4a4 ov;
+            ov.x = bswap32(o[0]); ov.y = bswap32(o[1]); ov.z = bswap32(o[2]); ov.w = bswap32(o[3]);
+            out4[b * (kBlockSyms / 8) + c * kWave + lane] = ov;
+        }
+        if (a.index) {
+            const uint32_t bs = (uint32_t)(start_bit + (uint64_t)b * kBlockSyms * 16);
+            uint64_t sub = 0;
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c)
+                sub |= (uint64_t)((bs + 16u * (kSPT * (uint32_t)lane + kChainSyms * c)) & 0xffffu) << (16 * c);
+            a.index_sub[b * kWave + lane] = sub;
+            if (lane == 0) a.index[b] = start_bit + (uint64_t)b * kBlockSyms * 16;
+            if (b == 0 && lane == 0) a.index[a.nblocks + 1] = 16ull * kBlockSyms;
+        }
+    }
+}
+
+// Lane runs [j_begin, ...) of 32 symbols (the stream's tail after k_pack_fixed16_blk, or all of it).
+__global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint64_t start_bit, uint64_t j_begin) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     load_lds_table<ENC_FIXED16>(lds, a.lds_img, a.lds_words);
     const uint16_t* c16 = reinterpret_cast<const uint16_t*>(lds);
@@ -1046,7 +1120,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_fixed16(PackArgs a, uint6
         }
     };
     uint32_t nraw[kSPT / 2];
-    const uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t j0 = j_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     load_run(j0, nraw);
     for (uint64_t j = j0; j < nl; j += stride) {  // the loop is uniform except in the last round
         const uint64_t sym0 = j * kSPT;
@@ -1227,10 +1301,22 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     if (t.enc_mode == ENC_FIXED16) {
         hipError_t e = ensure_lds_limit((const void*)k_pack_fixed16, kFixed16LdsBytes);
         if (e != hipSuccess) return e;
+        if ((e = ensure_lds_limit((const void*)k_pack_fixed16_blk, kFixed16LdsBytes)) != hipSuccess) return e;
         const uint64_t nl = (nsym + kSPT - 1) / kSPT;
-        uint64_t wgs = (nl + kPackThreads - 1) / kPackThreads;
+        // every block but the last through the coalesced kernel when it fits; the lane-run kernel
+        // takes the rest (the stream's end, the index end)
+        const uint64_t nb = nblocks - 1;
+        const bool blk = kFixed16Blk && nb > 0 && (start_bit >> 5) + nb * (kBlockSyms / 2) <= out_words;
+        uint64_t jb = 0;
+        if (blk) {
+            uint64_t wgs = (nb + kPackThreads / 64 - 1) / (kPackThreads / 64);
+            if (wgs > (uint64_t)ncu) wgs = ncu;  // 128 KiB table: one workgroup per CU
+            hipLaunchKernelGGL(k_pack_fixed16_blk, dim3(wgs), dim3(kPackThreads), kFixed16LdsBytes, s, a, start_bit, nb);
+            jb = nb * kWave;
+        }
+        uint64_t wgs = (nl - jb + kPackThreads - 1) / kPackThreads;
         if (wgs > (uint64_t)ncu) wgs = ncu;  // 128 KiB table: one workgroup per CU
-        hipLaunchKernelGGL(k_pack_fixed16, dim3(wgs), dim3(kPackThreads), kFixed16LdsBytes, s, a, start_bit);
+        hipLaunchKernelGGL(k_pack_fixed16, dim3(wgs), dim3(kPackThreads), kFixed16LdsBytes, s, a, start_bit, jb);
         return hipGetLastError();
     }
     // Waves per workgroup: as many output slots of the expected block size
@@ -2011,7 +2097,57 @@ __global__ __launch_bounds__(PIPE == 2 ? kDecPipe2Threads : 1024) void k_decode(
 
 // Every code 16 bits: lane j decodes symbols [32 j, 32 j + 32) from the 17
 // words starting at stream word (p0 >> 5) + 16 j.
-__global__ __launch_bounds__(1024) void k_decode_fixed16(DecArgs a) {
+// Full blocks [0, nb) of a FIXED16 stream (k_pack_fixed16_blk's mapping): lane l's sub-run c decodes the block's symbols 8 (64 c + l) .. + 7 from 4 words at a
+// 1 KiB-coalesced offset plus the next sub-run's first word (lane l + 1 by DPP, sub-run c + 1's lane 0,
+// or the next block's first word), and stores 16 bytes at a 1 KiB-coalesced offset.
+__global__ __launch_bounds__(1024) void k_decode_fixed16_blk(DecArgs a, uint64_t nb) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
+    const uint64_t p0 = a.starts[0] + a.bit_adj;
+    const uint32_t sh = (uint32_t)(p0 & 31);
+    const uint32_t* w = a.words + (p0 >> 5);  // any word of the payload view
+    const u32x4a4* w4 = reinterpret_cast<const u32x4a4*>(w);
+    uint4* o4 = reinterpret_cast<uint4*>(a.out);
+    const int lane = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    constexpr uint32_t kBW = kBlockSyms / 2;  // words per block
+    auto load = [&](uint64_t bb, u32x4a4 (&x)[kChainsPerLane], uint32_t& nw) {
+        bb = bb < nb ? bb : 0;
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) x[c] = w4[bb * (kBW / 4) + c * kWave + lane];
+        nw = w[(bb + 1) * kBW];  // the next block's first word (the stream's last block follows block nb - 1)
+    };
+    u32x4a4 nx[kChainsPerLane];
+    uint32_t nn = 0;
+    if (b < nb) load(b, nx, nn);
+    for (; b < nb; b += W) {
+        u32x4a4 x[kChainsPerLane];
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) x[c] = nx[c];
+        const uint32_t after = nn;
+        load(b + W, nx, nn);
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) {
+            uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[c].x, kDppWaveShl1, 0xf, 0xf, false);
+            const uint32_t first_next = c + 1 < kChainsPerLane ? readlane(x[c + 1 < kChainsPerLane ? c + 1 : c].x, 0) : after;
+            if (lane == 63) nxt = first_next;
+            const uint32_t ww[5] = {bswap32(x[c].x), bswap32(x[c].y), bswap32(x[c].z), bswap32(x[c].w), bswap32(nxt)};
+            uint32_t o[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t cw = sh ? __builtin_amdgcn_alignbit(ww[t], ww[t + 1], 32u - sh) : ww[t];
+                o[t] = (uint32_t)t16[cw >> 16] | ((uint32_t)t16[cw & 0xffffu] << 16);
+            }
+            store_nt16(o4 + b * (kBlockSyms / 8) + c * kWave + lane, make_uint4(o[0], o[1], o[2], o[3]));
+        }
+    }
+}
+
+// Lane runs of 32 symbols: those after the nb blocks k_decode_fixed16_blk decodes, or all of them.
+__global__ __launch_bounds__(1024) void k_decode_fixed16(DecArgs a, uint64_t nb) {
+    const uint64_t j_begin = nb * kWave;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const uint64_t p0 = a.starts[0] + a.bit_adj;  // the stream's first bit (the index holds nothing else we need)
@@ -2021,7 +2157,7 @@ __global__ __launch_bounds__(1024) void k_decode_fixed16(DecArgs a) {
     const bool vec = (W0 & 3) == 0;
     const uint64_t nl = (a.nsym + kSPT - 1) / kSPT;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += stride) {
+    for (uint64_t j = j_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += stride) {
         const uint64_t ws = W0 + 16 * j;
         uint32_t w[17];
         if (vec && ws + 17 <= a.nwords) {
@@ -2138,10 +2274,18 @@ hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t pay
     if (t.dec_mode == DEC_FIXED16) {
         hipError_t e = ensure_lds_limit((const void*)k_decode_fixed16, kFixed16LdsBytes);
         if (e != hipSuccess) return e;
+        if ((e = ensure_lds_limit((const void*)k_decode_fixed16_blk, kFixed16LdsBytes)) != hipSuccess) return e;
         const uint64_t nl = (nsym + kSPT - 1) / kSPT;
+        // every block but the last through the coalesced kernel; the lane-run kernel takes the last
+        const uint64_t nb = kFixed16Blk && a.nblocks > 1 ? a.nblocks - 1 : 0;
+        if (nb) {
+            uint64_t wgs = (nb + 15) / 16;
+            if (wgs > (uint64_t)ncu) wgs = ncu;
+            hipLaunchKernelGGL(k_decode_fixed16_blk, dim3(wgs), dim3(1024), kFixed16LdsBytes, s, a, nb);
+        }
         uint64_t wgs = (nl + 1023) / 1024;
         if (wgs > (uint64_t)ncu) wgs = ncu;
-        hipLaunchKernelGGL(k_decode_fixed16, dim3(wgs), dim3(1024), kFixed16LdsBytes, s, a);
+        hipLaunchKernelGGL(k_decode_fixed16, dim3(wgs), dim3(1024), kFixed16LdsBytes, s, a, nb);
         return hipGetLastError();
     }
     const uint64_t pbits = payload_bytes * 8;
