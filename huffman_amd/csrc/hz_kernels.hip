@@ -69,6 +69,12 @@ HZ_DEV uint32_t dpp0(uint32_t v) {
 }
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
 constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
+#ifndef HZ_DEC_SMEM
+#define HZ_DEC_SMEM 1  // decode: block bounds through the scalar cache (10.04-10.23 vs 10.27-10.33 ms, round 3)
+#endif
+#ifndef HZ_UNIFORM_WID
+#define HZ_UNIFORM_WID 1
+#endif
 #ifndef HZ_FIXED16_BLK
 #define HZ_FIXED16_BLK 1
 #endif
@@ -86,6 +92,15 @@ HZ_DEV uint32_t wave_incl_sum(uint32_t v) {
 }
 
 HZ_DEV uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// The wave's index in its workgroup as a wave-uniform (SGPR) value: block numbers derived from it,
+// and the index / start loads they address, stay on the scalar unit.
+HZ_DEV uint32_t wave_id() {
+#if HZ_UNIFORM_WID
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#else
+    return threadIdx.x >> 6;
+#endif
+}
 
 HZ_DEV uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
@@ -817,6 +832,7 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     // Output slot of this wave: the block's words are assembled in LDS and
     // leave as contiguous 256-byte stores (a block that does not fit, and the
     // stream's last block, store straight from the lanes).
+    // (the wave index stays a VGPR value here: as a scalar, 12.4-12.7 vs 11.8-12.2 ms pack stage)
     uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t max_bits = 0;  // largest block of this wave (index max_bits: one atomic per wave)
@@ -1831,8 +1847,18 @@ struct PipeMeta {
 
 HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
     const uint64_t bb = b < a.nblocks ? b : a.nblocks - 1;  // past the end: any block, never used
+#if HZ_DEC_SMEM
+    // the block's bounds through the scalar cache (the index is read-only here): the window
+    // arithmetic that follows stays on the scalar unit
+    typedef const __attribute__((address_space(4))) unsigned long long* cu64p;
+    const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bb >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bb);
+    m.b0 = ((cu64p)a.starts)[bu];
+    m.b1 = ((cu64p)a.starts)[bu + 1];
+#else
     m.b0 = a.starts[bb];
     m.b1 = a.starts[bb + 1];
+#endif
     m.sub = dec_sub_load(a, bb, lane);
 }
 
@@ -2069,9 +2095,9 @@ __global__ __launch_bounds__(PIPE == 2 ? kDecPipe2Threads : 1024) void k_decode(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
-    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t wid = wave_id();
     // slots fit the stream's largest block; waves without a slot have nothing to do
-    const uint32_t slot = dec_slot_words(a.starts[a.nblocks + 1], a.max_len);
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)dec_slot_words(a.starts[a.nblocks + 1], a.max_len));
     const uint32_t nwave = blockDim.x >> 6;
     if constexpr (PIPE == 2) {
         uint32_t nw2 = a.region_words / (2 * slot);
