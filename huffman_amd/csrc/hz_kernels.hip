@@ -576,7 +576,15 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
     }
 }
 
-constexpr int kPackWriteThreads = 512;  // <= 8 waves: room for a block of registers in flight per lane
+#ifndef HZ_PACK_MAXW
+#define HZ_PACK_MAXW 8
+#endif
+#ifndef HZ_PACK_MARGIN
+#define HZ_PACK_MARGIN 1.12
+#endif
+// <= 8 waves: room for a block of registers in flight per lane (16 GiB Zipf, round 3: 9 / 10 waves under a
+// 168-VGPR cap 11.7 / 11.0 ms vs 8 waves 9.6 ms for k_pack_write)
+constexpr int kPackWriteThreads = 64 * HZ_PACK_MAXW;
 constexpr int kPackCopyIters = 16;       // slot copy-out covers 16 x 64 words: a 1024-word slot
 
 // One block of a wave between its lookup and its emit: the lane's 32 entries,
@@ -1340,7 +1348,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
     a.lds_words = table_words;
     const uint32_t free_words = kLdsBytes / 4 - table_words;
-    const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * 1.12 / 32.0) + 4;
+    const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * HZ_PACK_MARGIN / 32.0) + 4;
     constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
     uint32_t waves = free_words / est_words;
     waves = waves > kMaxWaves ? kMaxWaves : waves;
