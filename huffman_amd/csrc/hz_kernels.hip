@@ -1599,7 +1599,8 @@ HZ_DEV void dec_store(const DecArgs& a, uint64_t b, int lane, const uint32_t* pk
 #endif
     if (sym0 + kBlockSyms <= a.nsym) {
         // non-temporal (streaming) stores: the output is not read again by this kernel
-        // (10.70 vs 11.15-11.37 ms at 16 GiB Zipf, round 3 A/B)
+        // (10.70 vs 11.15-11.37 ms at 16 GiB Zipf, round 3 A/B; buffer stores with nt / sc0 nt /
+        // nt sc1 / sc0 nt sc1 10.13-10.48 vs 10.01-10.02 ms)
         uint4* o = reinterpret_cast<uint4*>(a.out + 2 * sym0) + lane;
 #pragma unroll
         for (int c = 0; c < kChainsPerLane; ++c)
