@@ -69,6 +69,9 @@ HZ_DEV uint32_t dpp0(uint32_t v) {
 }
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
 constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
+#ifndef HZ_DEC_HOT_OOB
+#define HZ_DEC_HOT_OOB 1  // 10.30-10.32 vs 10.38-10.43 ms at 16 GiB Zipf (round 3 A/B)
+#endif
 #ifndef HZ_DEC_SMEM
 #define HZ_DEC_SMEM 1  // decode: block bounds through the scalar cache (10.04-10.23 vs 10.27-10.33 ms, round 3)
 #endif
@@ -1831,7 +1834,13 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
     for (int c = 0; c < NC; ++c) {
         h[c] = lut_lds_link(e[c]);
         const uint32_t byte = ((e[c] >> 10) + __builtin_amdgcn_ubfe(W[c], e[c], e[c] >> 5)) << 2;
+#if HZ_DEC_HOT_OOB
+        // a leaf's or a global link's byte address is >= 256 KiB, past the workgroup's LDS: that
+        // read returns nothing anyone uses (the select below keeps e), so no address select
+        x[c] = lds_at(byte);
+#else
         x[c] = lds_at(h[c] ? byte : 0u);
+#endif
     }
     HZ_WALK_FENCE();
 #pragma unroll
