@@ -605,3 +605,36 @@ def test_product_equals_literal_writer_except_b1_b2(hz):
             for p in diff:
                 hits[allowed[p]] += 1
     assert hits["B1"] > 0 and hits["B2"] > 0, hits
+
+
+@pytest.mark.parametrize("start_bit", [0, 7, 32, 45, 64, 96, 127, 145, 671])
+def test_fixed16_block_kernels_any_start(hz, start_bit):
+    """FIXED16 streams (every code 16 bits): every block but the last goes through the 1 KiB-coalesced
+    block kernels (k_pack_fixed16_blk / k_decode_fixed16_blk) at any word and bit of the output; the
+    stream equals the oracle's packer and decodes bit-exact through the index hz_pack wrote."""
+    import torch
+    from huffman_amd.codec import Device, build_codebook
+    rng = np.random.default_rng(start_bit)
+    sym = np.concatenate([rng.permutation(65536), rng.permutation(65536),
+                          rng.permutation(65536)[:9000]]).astype(np.uint16)
+    data = sym.view(np.uint8).copy()   # every symbol 2 or 3 times: all codes 16 bits, a partial last block
+    nsym = sym.size
+    h = oracle_lib.hist16(data)
+    _, ln, code = oracle_lib.codebook(h)
+    assert (ln == 16).all()
+    dev = Device()
+    dev.upload(build_codebook(h))
+    d_in = torch.from_numpy(data).cuda()
+    cap = (start_bit + 16 * nsym) // 8 + 64
+    d_out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    idx = torch.zeros(hz.index_bytes(nsym) // 8 + 8, dtype=torch.int64, device="cuda")
+    dev.pack(d_in.data_ptr(), data.size, start_bit, 0, d_out.data_ptr(), cap, idx.data_ptr())
+    dec = torch.empty(data.size + 16, dtype=torch.uint8, device="cuda")
+    dev.decode(d_out.data_ptr(), cap, nsym, idx.data_ptr(), dec.data_ptr())
+    dev.sync()
+    b0 = start_bit // 8
+    ref = oracle_lib.pack_range(data, 0, nsym, ln, code, start_bit - 8 * b0, (16 * nsym + 7) // 8 + 2)
+    got = d_out.cpu().numpy()[b0:b0 + ref.size]
+    assert np.array_equal(got[:(start_bit % 8 + 16 * nsym) // 8], ref[:(start_bit % 8 + 16 * nsym) // 8])
+    assert np.array_equal(dec[:data.size].cpu().numpy(), data)
+    dev.close()

@@ -30,9 +30,10 @@ from collections import defaultdict
 # stage -> (kernels of the stage, kernels that mark one launch of the stage)
 STAGES = {
     "hist": (("k_hist16",), ("k_hist16",)),
-    "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16"),
+    "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16",
+              "k_pack_fixed16_blk"),
              ("k_pack_write", "k_pack_fixed16")),
-    "decode": (("k_decode", "k_decode_fixed16"), ("k_decode", "k_decode_fixed16")),
+    "decode": (("k_decode", "k_decode_fixed16", "k_decode_fixed16_blk"), ("k_decode", "k_decode_fixed16")),
     "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
                "k_sync_subs"),
               ("k_sync_subs", "k_idx_fixed16")),
@@ -40,8 +41,8 @@ STAGES = {
 
 
 # kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
-WIDE_READ = ("k_hist16", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16", "k_decode",
-             "k_decode_fixed16", "k_idx_walk")
+WIDE_READ = ("k_hist16", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16", "k_pack_fixed16_blk",
+             "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk")
 
 
 def _is(name, k):
