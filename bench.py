@@ -391,7 +391,10 @@ def main():
         enc_ms = avg["hist"] + avg["pack"]
         enc_algo = 2 * N + C  # hist reads N; pack reads N and writes C
         enc_traffic = [pmc_traffic("hist"), pmc_traffic("pack")]
-        idx_algo = C + index_bytes(nsym)  # payload read + block index written
+        # payload read + block index written; a FIXED16 stream's index is arithmetic (k_idx_fixed16 reads
+        # no payload), so there only the index bytes written count
+        fixed16 = int(plan.cb.min_len) == 16 and int(plan.cb.max_len) == 16
+        idx_algo = index_bytes(nsym) + (0 if fixed16 else C)
         idx_traffic = pmc_traffic("index")
         line = {
             "metric": "encode + decode throughput GB/s and % HBM3E peak, 16 GiB Zipf(1.1), 1/2/4/8 GPU",

@@ -91,6 +91,10 @@ PROTOTYPES = [
     ("hz_index_bytes", _U64, [_U64]),
     ("hz_scratch_bytes", _U64, [_U64]),
     ("hz_pack", _I, [_P, _P, _U64, _U64, _U32, _P, _U64, _P]),
+    ("hz_ranges_bytes", _U64, [_U64]),
+    ("hz_hist16_ranges", _I, [_P, _P, _U64, _P, _I, _P]),
+    ("hz_pack_ranges", _I, [_P, _P, _U64, _U64, _U32, _P, _U64, _P, _P]),
+    ("hz_last_pack_ranges", _I, [_P]),
     ("hz_decode", _I, [_P, _P, _U64, _U64, _P, _P]),
     ("hz_index_build", _I, [_P, _P, _U64, _U64, _U64, _P]),
     ("hz_last_kernel_ms", _I, [_P, _I, ctypes.POINTER(ctypes.c_float)]),

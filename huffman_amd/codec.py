@@ -199,6 +199,22 @@ class Device:
     def pack(self, d_in, n, start_bit, lead, d_out, out_cap, d_index=None):
         check(self.lib.hz_pack(self.h, d_in, n, start_bit, lead, d_out, out_cap, d_index), "hz_pack")
 
+    # -- two-pass encode (range plan): hist16_ranges then pack_ranges on the same input ----------
+    def ranges_bytes(self, n):
+        """Bytes of the range plan buffer for an n-byte input (0: too small, plain passes)."""
+        return self.lib.hz_ranges_bytes(n)
+
+    def hist16_ranges(self, d_in, n, d_hist, d_ranges, accumulate=False):
+        check(self.lib.hz_hist16_ranges(self.h, d_in, n, d_hist, int(accumulate), d_ranges), "hz_hist16_ranges")
+
+    def pack_ranges(self, d_in, n, start_bit, lead, d_out, out_cap, d_index, d_ranges):
+        check(self.lib.hz_pack_ranges(self.h, d_in, n, start_bit, lead, d_out, out_cap, d_index, d_ranges),
+              "hz_pack_ranges")
+
+    def last_pack_ranges(self):
+        """1 when the last pack_ranges took the range plan (no count pass), 0 for count + scan + write."""
+        return self.lib.hz_last_pack_ranges(self.h)
+
     def decode(self, d_payload, payload_bytes, nsym, d_index, d_out):
         check(self.lib.hz_decode(self.h, d_payload, payload_bytes, nsym, d_index, d_out), "hz_decode")
 

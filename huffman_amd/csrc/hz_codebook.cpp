@@ -346,6 +346,18 @@ std::vector<uint32_t> build_len8(const hz_codebook* cb) {
     return img;
 }
 
+// Range plan (k_range_dot): the code lengths of both symbols a histogram LDS word counts,
+// in hist_word order: u16 = len[2 s'] | len[2 s' + 1] << 8, two per u32.
+std::vector<uint32_t> build_lenpair(const hz_codebook* cb) {
+    std::vector<uint32_t> img(16384, 0u);
+    uint16_t* lp = reinterpret_cast<uint16_t*>(img.data());
+    for (uint32_t w = 0; w < 32768; ++w) {
+        const uint32_t s2 = hist_word_inv(w) << 1;
+        lp[w] = (uint16_t)(cb->len[s2] | ((uint32_t)cb->len[s2 + 1] << 8));
+    }
+    return img;
+}
+
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb) {
     std::vector<uint64_t> t(HZ_NSYM, 0ull);
     for (uint32_t s = 0; s < HZ_NSYM; ++s)
@@ -403,7 +415,7 @@ int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K) {
 
 namespace {
 constexpr uint32_t kLeafBit = 1u << 31;
-inline uint32_t leaf(uint32_t L, uint32_t sym) { return kLeafBit | (L << 16) | sym; }
+inline uint32_t leaf(uint32_t L, uint32_t sym) { return lut_leaf_entry(L, sym); }
 }  // namespace
 
 // Fill one table level. `syms` are the symbols whose codes pass through this
@@ -482,7 +494,7 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
         for (uint32_t t = 0; t < (1u << nb); ++t) {
             const uint32_t x = l2[off + t];
             if (!(x & kLeafBit)) continue;
-            const uint32_t rem = ((x >> 16) & 63u) - (uint32_t)K1;
+            const uint32_t rem = lut_leaf_len(x) - (uint32_t)K1;
             for (uint32_t c = rem; c <= nb; ++c) r[c]++;
         }
         heads.push_back({q, nb, off, 0});
@@ -521,7 +533,7 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
         for (uint32_t j = 0; j < (1u << hd.c); ++j) {
             const uint32_t t0 = hd.off + (j << rest);
             const uint32_t x = l2[t0];
-            const bool done = (x & kLeafBit) && ((x >> 16) & 63u) - (uint32_t)K1 <= hd.c;
+            const bool done = (x & kLeafBit) && lut_leaf_len(x) - (uint32_t)K1 <= hd.c;
             img.push_back(done ? x : (rest ? lut_link(t0 + kLutGlobal, rest, (uint32_t)K1 + hd.c) : x));
         }
         img[hd.q] = lut_link(o, hd.c, (uint32_t)K1);

@@ -32,6 +32,7 @@ std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m);
 uint32_t choose_hot_mask(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_esc(const hz_codebook* cb);
 std::vector<uint32_t> build_len8(const hz_codebook* cb);
+std::vector<uint32_t> build_lenpair(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
@@ -80,8 +81,9 @@ struct hz_ctx {
     hipEvent_t ev[4][2] = {};
     bool ev_used[4] = {false, false, false, false};
     Staging stage_enc, stage_dec;
-    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_dec_lds = 0, cap_dec_l2 = 0,
-           cap_walk_lds = 0, cap_walk_esc = 0;
+    size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
+           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0;
+    int last_pack_ranges = 0;       // the last hz_pack_ranges call took the range plan
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -108,6 +110,7 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_enc_wide);
     (void)hipFree(t.d_enc_esc);
     (void)hipFree(t.d_len8);
+    (void)hipFree(t.d_lenpair);
     (void)hipFree(t.d_dec_lds);
     (void)hipFree(t.d_dec_l2);
     (void)hipFree(t.d_walk_lds);
@@ -208,6 +211,23 @@ extern "C" int hz_hist16(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
     c->ev_used[HZ_STAGE_HIST] = true;
     return HZ_OK;
+}
+
+extern "C" uint64_t hz_ranges_bytes(uint64_t n) { return range_geom(n / 2).bytes; }
+
+extern "C" int hz_hist16_ranges(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d_hist, int accumulate,
+                                void* d_ranges) {
+    if (!c || !d_hist || (n && !d_in)) return HZ_EINVAL;
+    if (!range_geom(n / 2).bytes) return hz_hist16(c, d_in, n, d_hist, accumulate);  // too small for a plan
+    if (!d_ranges || (((uintptr_t)d_in) & 15) || (((uintptr_t)d_ranges) & 15)) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    if (!accumulate) HZ_TRY(hipMemsetAsync(d_hist, 0, HZ_NSYM * sizeof(uint64_t), c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][0], c->stream));
+    HZ_TRY(launch_hist16_ranges(d_in, n, reinterpret_cast<unsigned long long*>(d_hist), d_ranges, c->d_err,
+                                c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
+    c->ev_used[HZ_STAGE_HIST] = true;
+    return arm_err_check(c);
 }
 
 extern "C" int hz_codebook_build_device(hz_ctx* c, const uint64_t* d_hist, hz_codebook* d_cb) {
@@ -326,6 +346,9 @@ static int hz_codebook_upload_encode_impl(hz_ctx* c, const hz_codebook* cb) {
         return rc;
     if (mode != ENC_FIXED16 && (rc = stage_copy(c, c->stage_enc, &t.d_len8, &c->cap_len8, build_len8(cb))))
         return rc;
+    if (mode != ENC_FIXED16 &&
+        (rc = stage_copy(c, c->stage_enc, &t.d_lenpair, &c->cap_lenpair, build_lenpair(cb))))
+        return rc;
     HZ_TRY(hipEventRecord(c->stage_enc.done, c->stream));
     t.enc_mode = mode;
     return HZ_OK;
@@ -357,7 +380,7 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (mode != DEC_FIXED16 && t.dec_lds_bytes + 4 * dec_slot_words_max(t.dec_max_len) > kLdsBytes)
         return HZ_ENOMEM;  // cannot happen for K1 <= 14 and codes <= 56 bits
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_lds, &c->cap_dec_lds, dimg))) return rc;
-    if (l2.empty()) l2.push_back(0x80010000u);
+    if (l2.empty()) l2.push_back(lut_leaf_entry(1, 0));
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
     // the index walker's length tables (FIXED16 streams have an arithmetic index)
@@ -401,8 +424,8 @@ static int ensure_scratch(hz_ctx* c, uint64_t words) {
     return HZ_OK;
 }
 
-extern "C" int hz_pack(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_bit, uint32_t lead, uint8_t* d_out,
-                       uint64_t out_cap, uint64_t* d_index) {
+static int pack_impl(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_bit, uint32_t lead, uint8_t* d_out,
+                     uint64_t out_cap, uint64_t* d_index, void* d_ranges) {
     if (!c || !d_out) return HZ_EINVAL;
     if (((uintptr_t)d_out) & 3) return HZ_EINVAL;
     const uint64_t nsym = n / 2;
@@ -417,11 +440,26 @@ extern "C" int hz_pack(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t star
     if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][0], c->stream));
     HZ_TRY(launch_pack(c->t, d_in, nsym, start_bit, lead, reinterpret_cast<uint32_t*>(d_out), out_cap / 4, c->d_desc,
-                       reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->ncu, c->stream));
+                       reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->ncu, c->stream, d_ranges,
+                       &c->last_pack_ranges));
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][1], c->stream));
     c->ev_used[HZ_STAGE_PACK] = true;
     return arm_err_check(c);
 }
+
+extern "C" int hz_pack(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_bit, uint32_t lead, uint8_t* d_out,
+                       uint64_t out_cap, uint64_t* d_index) {
+    return pack_impl(c, d_in, n, start_bit, lead, d_out, out_cap, d_index, nullptr);
+}
+
+extern "C" int hz_pack_ranges(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_bit, uint32_t lead,
+                              uint8_t* d_out, uint64_t out_cap, uint64_t* d_index, void* d_ranges) {
+    if (c) c->last_pack_ranges = 0;
+    if (range_geom(n / 2).bytes && (!d_ranges || (((uintptr_t)d_ranges) & 15))) return HZ_EINVAL;
+    return pack_impl(c, d_in, n, start_bit, lead, d_out, out_cap, d_index, range_geom(n / 2).bytes ? d_ranges : nullptr);
+}
+
+extern "C" int hz_last_pack_ranges(hz_ctx* c) { return c ? c->last_pack_ranges : 0; }
 
 extern "C" int hz_decode(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
                          const uint64_t* d_index, uint8_t* d_out) {
@@ -725,6 +763,12 @@ int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
         const uint64_t piece = ((n + kReaders - 1) / kReaders + 4095) & ~(uint64_t)4095;
         std::atomic<bool> bad{pos < 0};
         std::vector<std::thread> th;
+        // joins every started reader on every exit, a failed thread spawn (std::system_error,
+        // turned into an HZ_ status by guarded()) included
+        struct Joiner {
+            std::vector<std::thread>& v;
+            ~Joiner() { for (auto& t : v) if (t.joinable()) t.join(); }
+        } joiner{th};
         for (uint64_t a = 0; a < n && !bad; a += piece) {
             const uint64_t len = std::min(piece, n - a);
             th.emplace_back([&bad, fd, p, a, len, pos] {
@@ -737,6 +781,7 @@ int read_exact(FILE* fp, uint8_t* p, uint64_t n) {
             });
         }
         for (auto& t : th) t.join();
+        th.clear();
         ok = !bad && fseeko(fp, pos + (off_t)n, SEEK_SET) == 0;
     }
     g_timing.fread_ms += ms_since(t0);
@@ -1216,7 +1261,15 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
     if ((rc = parse_header_for_extract(head, cb.get(), &info))) return rc;
     FileWriter fout;
     if ((rc = fout.open(out_path))) return rc;
-    fout.reserve(info.n);
+    {
+        // Reserve no more than the payload can decode to: a header whose N overstates it (corrupt or
+        // crafted) must not allocate disk before the decode rejects it. nsym codewords need at least
+        // nsym * min_len payload bits.
+        const uint64_t pay_bits = fsize > info.payload_byte ? (fsize - info.payload_byte) * 8 - info.payload_bit : 0;
+        const uint64_t min_len = std::max<uint32_t>(cb->min_len, 1);
+        const uint64_t most = 2 * (pay_bits / min_len) + (info.is_odd ? 1 : 0);
+        fout.reserve(std::min<uint64_t>(info.n, most));
+    }
     uint64_t out_off = 0;
     const uint64_t nsym = info.n / 2;
     if (nsym > 0) {

@@ -34,6 +34,56 @@ __host__ __device__ inline uint64_t index_bytes(uint64_t nsym) {
 }
 __host__ __device__ inline uint64_t index_sub_offset(uint64_t nblocks) { return nblocks + 2; }  // in u64 words
 
+// ---- range plan: the two-pass encode (DESIGN.md "Ranges") -------------------
+// The input is cut into nranges RANGES of bpr whole blocks. The histogram kernel
+// sweeps them with `groups` workgroups (range j by workgroup j % groups, in
+// order) and snapshots its cumulative LDS histogram at the end of every range;
+// with the codebook known, a dot product of each snapshot with the code
+// lengths gives every range's payload bits, a scan gives its start bit, and
+// one pack wave per range writes its blocks in order from there: no count
+// pass over the input. Buffer (hz_ranges_bytes), in order:
+//   u32 snap[nranges][32768]            LDS image at the range's end (u16 pairs, hist_word order)
+//   u32 list[groups][1 + list_cap]      count, then every +-65536 carry the workgroup
+//                                       made: local range << 17 | negative << 16 | bin
+//   u64 dot[nranges]                    sum of len * cumulative count (k_range_dot)
+//   u64 start[nranges + 1]              start bit of every range, then the stream's end
+constexpr uint64_t kRangeTarget = 2048;     // ranges (= pack waves: 256 CUs x 8)
+constexpr uint64_t kRangeMinBlocks = 64;    // a snapshot (128 KiB) per >= 256 KiB of input
+constexpr uint64_t kRangeMinRanges = 1024;  // smaller inputs keep count + scan + write
+constexpr uint32_t kRangeGroups = 256;
+struct RangeGeom {
+    uint64_t nsym, nblocks, bpr, nranges, per_group;
+    uint32_t groups, list_cap;
+    uint64_t off_list, off_dot, off_start, bytes;  // byte offsets in the range buffer
+};
+__host__ __device__ inline RangeGeom range_geom(uint64_t nsym) {
+    RangeGeom g{};
+    g.nsym = nsym;
+    g.nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
+    const uint64_t want = (g.nblocks + kRangeTarget - 1) / kRangeTarget;
+    g.bpr = want > kRangeMinBlocks ? want : kRangeMinBlocks;
+    g.nranges = (g.nblocks + g.bpr - 1) / g.bpr;
+    if (g.nranges < kRangeMinRanges) return RangeGeom{};  // bytes = 0: no range plan
+    g.groups = (uint32_t)(g.nranges < kRangeGroups ? g.nranges : kRangeGroups);
+    g.per_group = (g.nranges + g.groups - 1) / g.groups;
+    // a low-half wrap needs 65 536 adds and makes at most three records (its own, a high-half
+    // wrap of its transient carry and the carry's undo); a high-half wrap one. Bound x4 + 16.
+    g.list_cap = (uint32_t)(4 * (g.per_group * g.bpr * kBlockSyms / 65536) + 16);
+    g.off_list = g.nranges * 32768ull * 4;
+    g.off_dot = (g.off_list + 4ull * g.groups * (1 + g.list_cap) + 15) & ~15ull;
+    g.off_start = g.off_dot + 8 * g.nranges;
+    g.bytes = g.off_start + 8 * (g.nranges + 1);
+    return g;
+}
+
+// Histogram LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data
+// share their low bits (the first byte), which alone would pick the LDS bank:
+// the second byte times 13 (odd: distinct small bytes land on distinct, spread
+// banks) is XORed into word bits 0-5; it depends only on word bits 7-14, which
+// the XOR leaves alone, so the map is a bijection.
+__host__ __device__ inline uint32_t hist_word(uint32_t s) { return (s >> 1) ^ (((s >> 8) * 13u) & 0x3fu); }
+__host__ __device__ inline uint32_t hist_word_inv(uint32_t w) { return w ^ (((w >> 7) * 13u) & 0x3fu); }
+
 // Encode table modes (selected on the host per codebook, DESIGN.md "Pack").
 enum EncMode : int {
     ENC_DENSE = 0,  // max_len <= 16: 65536 x 17-bit sentinel entries, 139 264 B LDS
@@ -57,7 +107,7 @@ enum DecMode : int {
 constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-bit codes
 constexpr int kDecLevelBits = 9;  // bits per global subtable level (fewer when the table would exceed kLutMaxL2)
 // LUT entries (DEC_LUT; hz_codebook.cpp build_dec_lut):
-//   leaf  1 << 31 | L << 16 | sym
+//   leaf  1 << 31 | L << 24 | sym << 8   (bits 7..0 zero)
 //   link  raw << 10 | nb << 5 | pos   (bit 31 clear). raw < kLutGlobal: the subtable starts at word raw of
 //         the LDS image; else at l2[raw - kLutGlobal]. nb (<= 15) index bits follow the D code bits
 //         already consumed; pos = 32 - D - nb (0 when D + nb > 32): the index is bits [pos, pos + nb) of
@@ -68,6 +118,16 @@ constexpr uint32_t kLutMaxL2 = (1u << 21) - kLutGlobal;     // global entries a 
 __host__ __device__ inline uint32_t lut_link(uint32_t raw, uint32_t nb, uint32_t D) {
     return (raw << 10) | (nb << 5) | (D + nb <= 32 ? 32 - D - nb : 0u);
 }
+// A leaf read as a link (the pipelined decoder does so unconditionally) has pos = 0 and a width of
+// (sym & 3) * 8 <= 24 bits, so its index (e >> 10) + bfe(W, 0, width) lies in [2^21, 2^21 + 2^20 + 2^24):
+// past every LDS word and past the global table's num_records (2^21 entries), and its byte offset
+// (index * 4 < 2^27) never wraps a 32-bit register back into a table. Symbol bits on a byte
+// boundary: one v_perm packs two symbols.
+__host__ __device__ inline uint32_t lut_leaf_entry(uint32_t L, uint32_t sym) {
+    return (1u << 31) | (L << 24) | (sym << 8);
+}
+__host__ __device__ inline uint32_t lut_leaf_len(uint32_t e) { return (e >> 24) & 63u; }
+__host__ __device__ inline uint32_t lut_leaf_sym(uint32_t e) { return (e >> 8) & 0xffffu; }
 constexpr int kDecMaxWaves = 16;
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
@@ -117,6 +177,7 @@ struct Tables {
     uint64_t* d_enc_wide = nullptr;// 65536 x u64: len << 56 | code
     uint32_t* d_enc_esc = nullptr; // 65536 x u32: len << 26 | code (HOT escapes, len <= 26)
     uint32_t* d_len8 = nullptr;    // LDS image: u8 length at len8_index(s)
+    uint32_t* d_lenpair = nullptr; // range plan: u8 lengths of both symbols of every histogram word (u16 each)
     uint32_t hot_mask = 0x8000;    // HOT pairing: s and s ^ hot_mask share slot
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
@@ -140,9 +201,14 @@ __host__ __device__ inline uint32_t hot_word(uint32_t slot) { return slot ^ ((sl
 // Launchers (hz_kernels.hip). All stream ordered; return hipError_t.
 hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu,
                          hipStream_t s);
+hipError_t launch_hist16_ranges(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, void* d_ranges,
+                                uint32_t* d_err, hipStream_t s);  // range plan (RangeGeom)
+// d_ranges (nullable): the range plan of d_in from launch_hist16_ranges; *used_ranges = 1 when the
+// pack took it (else count + scan + write)
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit,
                        uint32_t lead, uint32_t* d_out, uint64_t out_words, unsigned long long* d_scratch,
-                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s);
+                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s,
+                       void* d_ranges = nullptr, int* used_ranges = nullptr);
 uint64_t pack_scratch_words(uint64_t nsym);  // u64 words of d_scratch hz_pack needs
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                          uint64_t nsym, const unsigned long long* d_index, uint8_t* d_out,

@@ -163,23 +163,28 @@ hipError_t launch_generate(uint8_t* d_out, uint64_t n, uint64_t offset, int kind
 // ===========================================================================
 constexpr int kHistThreads = 1024;
 
-// LDS word of symbol pair s >> 1. Byte-pair symbols of skewed data share
-// their low bits (the first byte), which alone would pick the LDS bank: the
-// second byte's low bits are XORed into the bank bits (a bijection).
-// The second byte times 13 (odd: distinct small bytes land on distinct, spread
-// banks) XORed into word bits 0-5; it depends only on word bits 7-14, which
-// the XOR leaves alone, so the map is a bijection.
-HZ_DEV uint32_t hist_word(uint32_t s) { return (s >> 1) ^ (((s >> 8) * 13u) & 0x3fu); }
-HZ_DEV uint32_t hist_word_inv(uint32_t w) { return w ^ (((w >> 7) * 13u) & 0x3fu); }
+// (LDS word of a symbol pair: hist_word, hz_internal.h)
 
 // Fix-up after `old = atomicAdd(&lds[hist_word(s)], inc)`; rare (once per 65 536 adds of a bin).
-HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old) {
+// rec(bin, negative) sees every +-65 536 the global histogram receives (range snapshots).
+struct NoRec {
+    HZ_DEV void operator()(uint32_t, uint32_t) const {}
+};
+template <typename Rec = NoRec>
+HZ_DEV void hist_fix(uint32_t* lds, unsigned long long* hist, uint32_t s, uint32_t old, Rec rec = Rec()) {
     const uint32_t inc = (s & 1) ? 0x10000u : 1u;
-    if (old + inc < old) atomicAdd(&hist[s | 1], 65536ull);  // the dword (high half) wrapped
-    if (!(s & 1) && (old & 0xffffu) == 0xffffu) {            // low half crossed 65 536: undo its carry
+    if (old + inc < old) {  // the dword (high half) wrapped
+        atomicAdd(&hist[s | 1], 65536ull);
+        rec(s | 1, 0u);
+    }
+    if (!(s & 1) && (old & 0xffffu) == 0xffffu) {  // low half crossed 65 536: undo its carry
         atomicAdd(&hist[s], 65536ull);
+        rec(s, 0u);
         uint32_t o2 = atomicSub(&lds[hist_word(s)], 0x10000u);
-        if (o2 < 0x10000u) atomicAdd(&hist[s | 1], (unsigned long long)(-65536ll));
+        if (o2 < 0x10000u) {
+            atomicAdd(&hist[s | 1], (unsigned long long)(-65536ll));
+            rec(s | 1, 1u);
+        }
     }
 }
 
@@ -188,9 +193,59 @@ HZ_DEV bool hist_needs_fix(uint32_t s, uint32_t old) {
     return (old + inc < old) | (!(s & 1) & ((old & 0xffffu) == 0xffffu));
 }
 
-HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s) {
+template <typename Rec = NoRec>
+HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s, Rec rec = Rec()) {
     uint32_t old = atomicAdd(&lds[hist_word(s)], (s & 1) ? 0x10000u : 1u);
-    if (hist_needs_fix(s, old)) hist_fix(lds, hist, s, old);
+    if (hist_needs_fix(s, old)) hist_fix(lds, hist, s, old, rec);
+}
+
+// The 8 symbols of a 16-byte vector: 8 LDS atomics; a fix-up is due exactly when the
+// incremented half was 0xffff (the half a symbol counts in is its bit 0, the shift 16 * bit 0).
+template <typename Rec = NoRec>
+HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v, Rec rec = Rec()) {
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    uint32_t old[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        sh[k] = (s << 4) & 16u;
+        old[k] = atomicAdd(&lds[hist_word(s)], 1u << sh[k]);
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
+    if (__builtin_expect(any, 0)) {
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            if (hist_needs_fix(s, old[k])) hist_fix(lds, hist, s, old[k], rec);
+        }
+    }
+}
+
+// Vectors [i0, end) of in4 with stride `step` from this thread's i0: software pipelined over
+// two register buffers (no copies), the next vector's load in flight while this one's LDS
+// atomics run (loads and LDS ops use separate counters).
+template <typename Rec = NoRec>
+HZ_DEV void hist_sweep(uint32_t* lds, unsigned long long* hist, const uint4* in4, uint64_t i, uint64_t end,
+                       uint64_t step, Rec rec = Rec()) {
+    uint4 va = i < end ? in4[i] : make_uint4(0, 0, 0, 0), vb;
+    for (; i < end; i += 2 * step) {
+        if (i + step < end) vb = in4[i + step];
+        hist_count8(lds, hist, va, rec);
+        if (i + step >= end) break;
+        if (i + 2 * step < end) va = in4[i + 2 * step];
+        hist_count8(lds, hist, vb, rec);
+    }
+}
+
+// Adds the workgroup's LDS histogram to the global one.
+HZ_DEV void hist_flush(const uint32_t* lds, unsigned long long* hist) {
+    for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
+        const uint32_t v = lds[i];
+        const uint32_t s2 = hist_word_inv((uint32_t)i) << 1;  // the symbol pair this word counts
+        if (v & 0xffffu) atomicAdd(&hist[s2], (unsigned long long)(v & 0xffffu));
+        if (v >> 16) atomicAdd(&hist[s2 + 1], (unsigned long long)(v >> 16));
+    }
 }
 
 template <bool VEC>
@@ -201,45 +256,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
     __syncthreads();
     uint64_t tail_begin = 0;
     if (VEC) {
-        const uint4* in4 = reinterpret_cast<const uint4*>(in);
-        const uint64_t nvec = nsym / 8;
         // the whole chip sweeps the input together (neighbouring 16 KiB pieces),
         // one vector (8 symbols) per lane per step
-        const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-        const uint64_t end = nvec;
-        // 8 LDS atomics; a fix-up is due exactly when the incremented half was
-        // 0xffff (the half a symbol counts in is its bit 0, the shift 16 * bit 0)
-        auto count8 = [&](const uint4& v) {
-            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-            uint32_t old[8], sh[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                sh[k] = (s << 4) & 16u;
-                old[k] = atomicAdd(&lds[hist_word(s)], 1u << sh[k]);
-            }
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
-            if (__builtin_expect(any, 0)) {
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                    if (hist_needs_fix(s, old[k])) hist_fix(lds, hist, s, old[k]);
-                }
-            }
-        };
-        // software pipelined over two register buffers (no copies): the next
-        // vector's load is in flight while this one's LDS atomics run (loads
-        // and LDS ops use separate counters)
-        uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        uint4 va = i < end ? in4[i] : make_uint4(0, 0, 0, 0), vb;
-        for (; i < end; i += 2 * step) {
-            if (i + step < end) vb = in4[i + step];
-            count8(va);
-            if (i + step >= end) break;
-            if (i + 2 * step < end) va = in4[i + 2 * step];
-            count8(vb);
-        }
+        const uint64_t nvec = nsym / 8;
+        hist_sweep(lds, hist, reinterpret_cast<const uint4*>(in), (uint64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                   nvec, (uint64_t)gridDim.x * blockDim.x);
         tail_begin = nvec * 8;
     }
     // Scalar symbols: the < 8-symbol tail (VEC) or everything (unaligned input).
@@ -252,12 +273,66 @@ __global__ __launch_bounds__(kHistThreads) void k_hist16(const uint8_t* __restri
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
-        const uint32_t v = lds[i];
-        const uint32_t s2 = hist_word_inv((uint32_t)i) << 1;  // the symbol pair this word counts
-        if (v & 0xffffu) atomicAdd(&hist[s2], (unsigned long long)(v & 0xffffu));
-        if (v >> 16) atomicAdd(&hist[s2 + 1], (unsigned long long)(v >> 16));
+    hist_flush(lds, hist);
+}
+
+// ---- range plan histogram (hz_internal.h RangeGeom) -------------------------
+struct RangeArgs {
+    uint32_t* snap;              // [nranges][32768] LDS images
+    uint32_t* list;              // [groups][1 + list_cap] carry records
+    unsigned long long* dot;     // [nranges]
+    unsigned long long* start;   // [nranges + 1]
+    uint64_t nsym, nblocks, bpr, nranges;
+    uint32_t groups, list_cap;
+    uint32_t* err;
+};
+
+static RangeArgs range_args(void* buf, const RangeGeom& g, uint32_t* err) {
+    RangeArgs r;
+    uint8_t* b = reinterpret_cast<uint8_t*>(buf);
+    r.snap = reinterpret_cast<uint32_t*>(b);
+    r.list = reinterpret_cast<uint32_t*>(b + g.off_list);
+    r.dot = reinterpret_cast<unsigned long long*>(b + g.off_dot);
+    r.start = reinterpret_cast<unsigned long long*>(b + g.off_start);
+    r.nsym = g.nsym; r.nblocks = g.nblocks; r.bpr = g.bpr; r.nranges = g.nranges;
+    r.groups = g.groups; r.list_cap = g.list_cap; r.err = err;
+    return r;
+}
+
+// Workgroup g sweeps ranges g, g + groups, ... (each a contiguous stretch of whole
+// blocks; the last one ends at the stream's end) and stores its CUMULATIVE LDS
+// image after each: range j's bits are then dot(j) - dot(j - groups), the
+// difference of two snapshots weighted by the code lengths plus the carries the
+// workgroup made in between (k_range_dot). The global histogram equals k_hist16's.
+// Input 16-byte aligned (ranges start on block boundaries: whole vectors).
+__global__ __launch_bounds__(kHistThreads) void k_hist16_rng(const uint8_t* __restrict__ in,
+                                                             unsigned long long* __restrict__ hist, RangeArgs r) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    for (int i = threadIdx.x; i < 32768; i += blockDim.x) lds[i] = 0;
+    if (threadIdx.x == 0) r.list[(uint64_t)blockIdx.x * (1 + r.list_cap)] = 0u;
+    __syncthreads();
+    const uint4* in4 = reinterpret_cast<const uint4*>(in);
+    uint32_t* list = r.list + (uint64_t)blockIdx.x * (1 + r.list_cap);
+    uint32_t k = 0;  // the range's index among this workgroup's (< 2^15)
+    for (uint64_t j = blockIdx.x; j < r.nranges; j += r.groups, ++k) {
+        const uint64_t s0 = j * r.bpr * kBlockSyms;
+        const uint64_t s1 = s0 + r.bpr * kBlockSyms < r.nsym ? s0 + r.bpr * kBlockSyms : r.nsym;
+        auto rec = [&](uint32_t bin, uint32_t neg) {
+            const uint32_t i = atomicAdd(list, 1u);
+            if (i < r.list_cap) list[1 + i] = (k << 17) | (neg << 16) | bin;
+            else atomicOr(r.err, 16u);  // cannot happen (RangeGeom bound): flagged, never silent
+        };
+        const uint64_t v1 = s1 / 8;
+        hist_sweep(lds, hist, in4, s0 / 8 + threadIdx.x, v1, blockDim.x, rec);
+        for (uint64_t q = v1 * 8 + threadIdx.x; q < s1; q += blockDim.x)  // the stream's < 8-symbol tail
+            hist_one(lds, hist, (uint32_t)in[2 * q] | ((uint32_t)in[2 * q + 1] << 8), rec);
+        __syncthreads();
+        uint4* dst = reinterpret_cast<uint4*>(r.snap) + j * 8192;
+        const uint4* src = reinterpret_cast<const uint4*>(lds);
+        for (int q = threadIdx.x; q < 8192; q += blockDim.x) dst[q] = src[q];
+        __syncthreads();
     }
+    hist_flush(lds, hist);
 }
 
 hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, int ncu, hipStream_t s) {
@@ -274,6 +349,17 @@ hipError_t launch_hist16(const uint8_t* d_in, uint64_t n, unsigned long long* d_
         hipLaunchKernelGGL(k_hist16<true>, dim3(grid), dim3(kHistThreads), 131072, s, d_in, nsym, d_hist);
     else
         hipLaunchKernelGGL(k_hist16<false>, dim3(grid), dim3(kHistThreads), 131072, s, d_in, nsym, d_hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist16_ranges(const uint8_t* d_in, uint64_t n, unsigned long long* d_hist, void* d_ranges,
+                                uint32_t* d_err, hipStream_t s) {
+    const RangeGeom g = range_geom(n / 2);
+    if (!g.bytes || (((uintptr_t)d_in) & 15) || (((uintptr_t)d_ranges) & 15)) return hipErrorInvalidValue;
+    hipError_t e = ensure_lds_limit((const void*)k_hist16_rng, 131072);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hist16_rng, dim3(g.groups), dim3(kHistThreads), 131072, s, d_in, d_hist,
+                       range_args(d_ranges, g, d_err));
     return hipGetLastError();
 }
 
@@ -310,6 +396,8 @@ struct PackArgs {
     unsigned long long* index_sub;  // block index sub[] (four u16 chain start bits per lane, low 16 bits)
     uint32_t* err;
     uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
+    const unsigned long long* rstart;  // range plan: start bit of every range (k_range_scan)
+    uint64_t bpr, nranges;       // range plan: blocks per range, ranges
 };
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
@@ -346,7 +434,7 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
     x.psym = *reinterpret_cast<const uint16_t*>(a.in + 2 * ps);
-    x.bstart = a.blk_start ? a.blk_start[blk] : 0;  // one-pass pack (k_pack_lb): from the look-back
+    x.bstart = a.blk_start ? a.blk_start[blk] : 0;  // range pack: a running sum instead
 }
 
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
@@ -415,27 +503,16 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         uint32_t v[kSPT], mk[kSPT];
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
-#ifdef HZ_EXP_PACK_NOESC  // timing experiment only (wrong codes): no escape loads
-            mk[k] = 0u;
-#else
             mk[k] = 0u - ((uint32_t)e[k] >> 31);
-#endif
             v[k] = a.esc[((raw[k >> 1] >> (16 * (k & 1))) & 0xffffu) & mk[k]];
         }
-#ifdef HZ_EXP_PACK_NOESC
-        const uint32_t xmk = 0u;
-#else
         const uint32_t xmk = 0u - (xx >> 31);
-#endif
         const uint32_t xv = a.esc[xs & xmk];
         mid();
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             uint32_t r;
             asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"((uint32_t)e[k]));
-#ifdef HZ_EXP_PACK_NOESC
-            r &= 0x7fffffffu;
-#endif
             e[k] = (T)r;
         }
         {
@@ -750,11 +827,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
             max_bits = b.bits > max_bits ? b.bits : max_bits;
             return;
         }
-#ifdef HZ_EXP_PACK_NOSTORE  // timing experiment only: no payload stores on the slot path
-        if (fits && a.nsym == 3) {
-#else
         if (fits) {
-#endif
             if constexpr (MODE != ENC_WIDE) {  // host: slot_words <= kPackCopyIters * kWave
                 // Output words [wfirst, wfirst + nwords): a partial first 16-byte chunk
                 // (its words before wfirst are the previous block's), whole chunks,
@@ -834,8 +907,12 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
 #endif
 constexpr bool kPackDefer = HZ_PACK_DEFER;
 
-// Three-pass pack (after k_pack_count + k_scan_*): block starts are known.
-template <int MODE>
+// Pack of blocks whose start bits are known: the three-pass pack (after
+// k_pack_count + k_scan_*; wave w packs blocks w, w + W, ...) or, RNG, the
+// range plan (after k_range_dot + k_range_scan; wave w packs the blocks of
+// ranges w, w + W, ... in order, each block starting where the one before it
+// ended: a running sum, no count pass).
+template <int MODE, bool RNG>
 __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
@@ -846,210 +923,45 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     // (the wave index stays a VGPR value here: as a scalar, 12.4-12.7 vs 11.8-12.2 ms pack stage)
     uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     uint64_t max_bits = 0;  // largest block of this wave (index max_bits: one atomic per wave)
-    uint64_t blk = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint64_t blk = gw, r = gw, rend = 0, run = 0;
+    if (RNG) {
+        blk = r < a.nranges ? r * a.bpr : a.nblocks;
+        rend = blk + a.bpr < a.nblocks ? blk + a.bpr : a.nblocks;
+        run = r < a.nranges ? a.rstart[r] : 0;
+    }
     PackIn nx;  // the next block's inputs, in flight while this block is packed
     if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
     PackOut po;
     po.pending = false;
-    for (; blk < a.nblocks; blk += W) {
+    while (blk < a.nblocks) {
+        uint64_t nb = blk + W, nrun = 0;
+        bool newr = false;
+        if (RNG) {
+            if (blk + 1 < rend) {
+                nb = blk + 1;
+            } else {  // the wave's next range: its start bit lands during this block
+                r += W;
+                newr = true;
+                nb = r < a.nranges ? r * a.bpr : a.nblocks;
+                rend = nb + a.bpr < a.nblocks ? nb + a.bpr : a.nblocks;
+                nrun = r < a.nranges ? a.rstart[r] : 0;
+            }
+        }
         PackIn cur = nx;
         PackBlk<MODE> b;
         // the previous block's stores go out behind this block's escape loads
         pack_block_lookup<MODE>(a, lds, blk, lane, cur, b, [&]() { pack_copyout(a, slot, lane, po); });
         po.pending = false;
         // next block's loads: after this block's escapes, so no wait covers them early
-        pack_prefetch(a, blk + W < a.nblocks ? blk + W : blk, lane, nx);
+        pack_prefetch(a, nb < a.nblocks ? nb : blk, lane, nx);
         pack_block_count<MODE>(lane, b);
-        pack_block_emit<MODE>(a, slot, blk, lane, b, cur.bstart, max_bits, kPackDefer ? &po : nullptr);
+        pack_block_emit<MODE>(a, slot, blk, lane, b, RNG ? run : cur.bstart, max_bits, kPackDefer ? &po : nullptr);
+        if (RNG) run = newr ? nrun : run + b.bits;
+        blk = nb;
     }
     pack_copyout(a, slot, lane, po);
-    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
-}
-
-// ---- one-pass pack: block starts by a resolver wave ------------------------
-// Replaces k_pack_count + the scan kernels for HOT and DENSE tables, so pack
-// reads its input once (Compressor.cu:543-576 computes the same start bits
-// with populateCWLength + transform_inclusive_scan). Wave 0 of workgroup 0 is
-// the RESOLVER; every other wave is a packer, and packer w of W packs blocks
-// w, w + W, w + 2W, ... (the grid is sized to be co-resident, as
-// k_pack_write's). A packer looks the codes of a block up, counts its bits and
-// publishes the count, then looks up and publishes its NEXT block, and only
-// then takes the first block's start bit and emits it. The resolver walks the
-// blocks in order, kRsvBatch x 64 counts in flight per round trip, and
-// publishes every block's start as a running sum -- an exclusive scan with no
-// look-back and no contention. No workgroup barrier.
-//   - counts and starts are self-validating granules (a flag bit in the word,
-//     written and read with agent-scope relaxed atomics = sc1), so no fence
-//     orders them against anything else;
-//   - a wave that finds an unpublished count or start sleeps and re-reads it
-//     (its producer publishes without waiting); the spins are bounded
-//     (HZ_ETIMEOUT), so the kernel never hangs.
-constexpr uint32_t kAggValid = 1u << 31;
-constexpr uint64_t kStartValid = 1ull << 63;
-constexpr uint32_t kLbMaxSpins = 1u << 24;  // then flag HZ_ETIMEOUT (err bit 8) and go on: never a hang
-constexpr int kRsvBatch = 16;               // 64-block groups per resolver round trip
-
-struct LbArgs {
-    uint32_t* blk_agg;              // per block: kAggValid | bits
-    unsigned long long* blk_start;  // per block: kStartValid | start bit
-    uint64_t start_bit;
-};
-
-HZ_DEV uint32_t lb_ld32(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-HZ_DEV uint64_t lb_ld64(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-HZ_DEV void lb_st32(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-HZ_DEV void lb_st64(unsigned long long* p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The resolver: block starts in order, kRsvPer blocks per lane and kRsvPer * 64
-// per batch (lane i: blocks [base + kRsvPer i, + kRsvPer)); the next batch's
-// counts are in flight while this batch's starts are summed and stored. The
-// counts and starts move as 16-byte sc1 buffer accesses (every u32 count and
-// u64 start validates itself, so a torn 16-byte access is harmless).
-constexpr int kRsvPer = 16;
-constexpr uint32_t kRsvBatchBlocks = kRsvPer * kWave;
-
-HZ_DEV void rsv_load(__amdgpu_buffer_rsrc_t r, uint64_t base, int lane, uint32_t (&c)[kRsvPer]) {
-    const uint32_t off = (uint32_t)((base + (uint64_t)kRsvPer * lane) * 4);
-#pragma unroll
-    for (int q = 0; q < kRsvPer / 4; ++q) {
-        const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * q, 0, 16));
-        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
-    }
-}
-
-constexpr int kRsvRing = 4;  // batches whose counts are in flight
-
-HZ_DEV void lb_resolver(const PackArgs& a, const LbArgs& l, int lane) {
-    // reads past the last block fall outside the buffers' ranges: they return 0 and stores are dropped
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(l.blk_agg, 0, (uint32_t)(a.nblocks * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(l.blk_start, 0, (uint32_t)(a.nblocks * 8), 0x00020000);
-    uint64_t run = l.start_bit;
-    uint32_t c[kRsvRing][kRsvPer];
-#pragma unroll
-    for (int r = 0; r < kRsvRing - 1; ++r) rsv_load(ra, (uint64_t)r * kRsvBatchBlocks, lane, c[r]);
-    // one batch: wait for its counts, publish its starts; then issue the loads kRsvRing - 1 batches ahead
-    auto batch = [&](uint32_t (&cur)[kRsvPer], uint32_t (&ahead)[kRsvPer], uint64_t base) {
-        const uint64_t b0 = base + (uint64_t)kRsvPer * lane;
-        for (uint32_t n = 0;; ++n) {  // every count published (blocks past the end count as published zeros)
-            bool ok = true;
-#pragma unroll
-            for (int k = 0; k < kRsvPer; ++k) ok &= (cur[k] & kAggValid) || b0 + k >= a.nblocks;
-            if (!__ballot(!ok)) break;
-            if (n == kLbMaxSpins) {
-                if (lane == 0) atomicOr(a.err, 8u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            if (!ok) {
-#pragma unroll
-                for (int k = 0; k < kRsvPer; ++k)
-                    if (!(cur[k] & kAggValid) && b0 + k < a.nblocks) cur[k] = lb_ld32(l.blk_agg + b0 + k);
-            }
-        }
-        rsv_load(ra, base + (uint64_t)(kRsvRing - 1) * kRsvBatchBlocks, lane, ahead);  // harmless past the end
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < kRsvPer; ++k) sum += cur[k] & ~kAggValid;  // < 16 * 2^17
-        const uint32_t incl = wave_incl_sum(sum);                        // < 2^27
-        uint64_t st = run + (incl - sum);
-        const uint32_t off = (uint32_t)(b0 * 8);
-#pragma unroll
-        for (int q = 0; q < kRsvPer / 2; ++q) {
-            const uint64_t s0 = st, s1 = st + (cur[2 * q] & ~kAggValid);
-            st = s1 + (cur[2 * q + 1] & ~kAggValid);
-            const uint4 v = make_uint4((uint32_t)s0, (uint32_t)(s0 >> 32) | 0x80000000u, (uint32_t)s1,
-                                       (uint32_t)(s1 >> 32) | 0x80000000u);  // kStartValid
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                                   rs, off + 16 * q, 0, 16);
-        }
-        run += readlane(incl, 63);
-    };
-    static_assert(kRsvRing == 4, "ring of four");
-    for (uint64_t base = 0; base < a.nblocks; base += kRsvRing * kRsvBatchBlocks) {  // unrolled: no copies
-        batch(c[0], c[3], base);
-        if (base + kRsvBatchBlocks >= a.nblocks) break;
-        batch(c[1], c[0], base + kRsvBatchBlocks);
-        if (base + 2 * kRsvBatchBlocks >= a.nblocks) break;
-        batch(c[2], c[1], base + 2 * kRsvBatchBlocks);
-        if (base + 3 * kRsvBatchBlocks >= a.nblocks) break;
-        batch(c[3], c[2], base + 3 * kRsvBatchBlocks);
-    }
-}
-
-// Block b's start bit; `v` is a poll issued earlier (its latency hidden behind
-// a block's lookup), re-polled only while the start is unpublished.
-HZ_DEV uint64_t lb_wait_start(const PackArgs& a, const LbArgs& l, uint64_t b, uint64_t v, int lane) {
-    for (uint32_t n = 0; !(v & kStartValid); ++n) {
-        if (n == kLbMaxSpins) {
-            if (lane == 0) atomicOr(a.err, 8u);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        v = lb_ld64(l.blk_start + b);
-    }
-    return v & ~kStartValid;
-}
-
-// Blocks a packer has counted and published ahead of the one it emits: the
-// resolver's two hops (packer -> resolver -> packer, ~1-2 us each under load)
-// hide behind that many blocks of lookup work (one block ahead measured
-// 16.0 ms at 16 GiB Zipf with 45 % of the packers' time in the wait).
-#ifndef HZ_LB_AHEAD
-#define HZ_LB_AHEAD 2
-#endif
-constexpr int kLbAhead = HZ_LB_AHEAD;
-
-template <int MODE>
-__global__ __launch_bounds__(kPackWriteThreads) void k_pack_lb(PackArgs a, LbArgs l) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);  // the kernel's only workgroup barrier
-    const int lane = threadIdx.x & 63;
-    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (gw == 0) {
-        lb_resolver(a, l, lane);
-        return;
-    }
-    uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
-    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6) - 1;  // packers
-    uint64_t max_bits = 0;
-    const uint64_t first = gw - 1;
-    if (first < a.nblocks) {
-        // ring of kLbAhead + 1 counted blocks; block j of this packer (first + j W) sits in p[j % 3]
-        PackBlk<MODE> p[kLbAhead + 1];
-        PackIn in;
-        pack_prefetch(a, first, lane, in);
-        // steps j = 0, 1, ...: count + publish block j + kLbAhead (input prefetched), then emit block j
-        auto count = [&](PackBlk<MODE>& q, uint64_t b) {
-            pack_block_lookup<MODE>(a, lds, b, lane, in, q);
-            pack_prefetch(a, b + W < a.nblocks ? b + W : b, lane, in);
-            pack_block_count<MODE>(lane, q);
-            if (lane == 0) lb_st32(l.blk_agg + b, kAggValid | q.bits);
-        };
-#pragma unroll
-        for (int j = 0; j < kLbAhead; ++j)
-            if (first + j * W < a.nblocks) count(p[j], first + j * W);
-        // one step: emit block b (slot pe) after counting block b + 2W into slot pc
-        auto step = [&](PackBlk<MODE>& pe, PackBlk<MODE>& pc, uint64_t b) -> bool {
-            const uint64_t poll = lb_ld64(l.blk_start + b);  // lands during the lookup below
-            const uint64_t bc = b + kLbAhead * W;
-            if (bc < a.nblocks) count(pc, bc);
-            const uint64_t bst = lb_wait_start(a, l, b, poll, lane);
-            pack_block_emit<MODE>(a, slot, b, lane, pe, bst, max_bits);
-            return b + W < a.nblocks;
-        };
-        for (uint64_t b = first;; b += (kLbAhead + 1) * W) {  // unrolled by the ring size: no register rotation
-            bool more = true;
-#pragma unroll
-            for (int j = 0; j <= kLbAhead && more; ++j)
-                more = step(p[j], p[(j + kLbAhead) % (kLbAhead + 1)], b + j * W);
-            if (!more) break;
-        }
-    }
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
@@ -1294,19 +1206,75 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long
     }
 }
 
-// k_pack_lb's scratch (u64 words): block starts, then u32 block counts.
-static uint64_t lb_scratch_words(uint64_t nblocks) { return nblocks + (nblocks + 1) / 2; }
+// ---- range plan: bits and start of every range ------------------------------
+// dot[j] = sum over bins of len * (the cumulative count of workgroup j % groups
+// after its range j): the snapshot's u16 halves plus 65 536 x its carry records
+// up to range j. lenpair: the two code lengths of every histogram word (u8 each,
+// hist_word order, hz_codebook_upload_encode).
+constexpr int kDotThreads = 256;
+__global__ __launch_bounds__(kDotThreads) void k_range_dot(RangeArgs r, const uint32_t* __restrict__ lenpair) {
+    __shared__ unsigned long long red[kDotThreads / 64];
+    const uint16_t* lp16 = reinterpret_cast<const uint16_t*>(lenpair);
+    for (uint64_t j = blockIdx.x; j < r.nranges; j += gridDim.x) {
+        const uint4* sp = reinterpret_cast<const uint4*>(r.snap) + j * 8192;
+        const uint2* lp = reinterpret_cast<const uint2*>(lenpair);  // 4 length pairs per 16 snapshot bytes
+        auto mac = [](uint32_t v, uint32_t l) { return (v & 0xffffu) * (l & 0xffu) + (v >> 16) * ((l >> 8) & 0xffu); };
+        uint32_t acc = 0;  // <= 32 x 4 x 2 x 65535 x 56 < 2^32
+        for (uint32_t q = threadIdx.x; q < 8192; q += kDotThreads) {
+            const uint4 v = sp[q];
+            const uint2 l = lp[q];
+            acc += mac(v.x, l.x) + mac(v.y, l.x >> 16) + mac(v.z, l.y) + mac(v.w, l.y >> 16);
+        }
+        uint64_t sum = acc;
+        const uint32_t g = (uint32_t)(j % r.groups), k = (uint32_t)(j / r.groups);
+        const uint32_t* list = r.list + (uint64_t)g * (1 + r.list_cap);
+        const uint32_t n = list[0] < r.list_cap ? list[0] : r.list_cap;
+        for (uint32_t t = threadIdx.x; t < n; t += kDotThreads) {
+            const uint32_t e = list[1 + t];
+            if ((e >> 17) > k) continue;
+            const uint32_t bin = e & 0xffffu;
+            const uint64_t L = (lp16[hist_word(bin)] >> (8 * (bin & 1))) & 0xffu;
+            sum += (e >> 16) & 1u ? (uint64_t)0 - (L << 16) : L << 16;  // mod 2^64: the total is >= 0
+        }
+        sum = wave_sum_u64(sum);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t t = 0;
+            for (int w = 0; w < kDotThreads / 64; ++w) t += red[w];
+            r.dot[j] = t;
+        }
+        __syncthreads();
+    }
+}
+
+// start[j] = start_bit + sum of bits of ranges < j; bits_j = dot[j] - dot[j - groups]
+// (the same workgroup's previous snapshot); start[nranges] = the stream's end.
+__global__ __launch_bounds__(kScanThreads) void k_range_scan(RangeArgs r, uint64_t start_bit) {
+    __shared__ uint64_t sh[17];
+    uint64_t carry = start_bit;
+    for (uint64_t b = 0; b < r.nranges; b += kScanThreads) {
+        const uint64_t j = b + threadIdx.x;
+        const uint64_t v = j < r.nranges ? r.dot[j] - (j >= r.groups ? r.dot[j - r.groups] : 0ull) : 0ull;
+        uint64_t total;
+        const uint64_t ex = block_exclusive_scan(v, sh, total);
+        if (j < r.nranges) r.start[j] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) r.start[r.nranges] = carry;
+}
 
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
-    const uint64_t three = 2 * nblocks + ntiles, one = lb_scratch_words(nblocks);
-    return three > one ? three : one;
+    return 2 * nblocks + ntiles;
 }
 
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
                        uint32_t* d_out, uint64_t out_words, unsigned long long* d_scratch,
-                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s) {
+                       unsigned long long* d_index, uint32_t* d_err, int ncu, hipStream_t s, void* d_ranges,
+                       int* used_ranges) {
+    if (used_ranges) *used_ranges = 0;
     if (nsym == 0) return hipSuccess;
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
@@ -1321,6 +1289,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     unsigned long long* tiles = d_scratch + 2 * nblocks;
     a.blk_start = blk_start; a.index = d_index; a.err = d_err;
     a.index_sub = d_index ? d_index + index_sub_offset(nblocks) : nullptr;
+    a.rstart = nullptr; a.bpr = 0; a.nranges = 0;
     if (d_index && t.enc_mode != ENC_FIXED16) {
         hipError_t e = hipMemsetAsync(d_index + nblocks + 1, 0, 8, s);  // max_bits, raised per block
         if (e != hipSuccess) return e;
@@ -1365,29 +1334,37 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t lds = 4 * (table_words + waves * a.slot_words);
     const uint64_t cap = (uint64_t)ncu * (lds ? kLdsBytes / lds : 4);
     if (wgs > cap) wgs = cap;
-    // one pass (k_pack_lb) on request: HZ_PACK_LB=1 (slower on MI355X than count + scan + write)
-    static const bool one_pass = [] { const char* v = getenv("HZ_PACK_LB"); return v && v[0] == '1'; }();
-    if (one_pass && t.enc_mode != ENC_WIDE && (wgs > 1 || waves > 1)) {  // a packer beside the resolver
-        LbArgs l;
-        l.blk_start = d_scratch;
-        l.blk_agg = reinterpret_cast<uint32_t*>(d_scratch + nblocks);
-        l.start_bit = start_bit;
-        a.blk_start = nullptr;
-        hipError_t e = hipMemsetAsync(d_scratch, 0, lb_scratch_words(nblocks) * 8, s);
-        if (e != hipSuccess) return e;
-        const void* fn = t.enc_mode == ENC_HOT ? (const void*)k_pack_lb<ENC_HOT> : (const void*)k_pack_lb<ENC_DENSE>;
-        if ((e = ensure_lds_limit(fn, kLdsBytes)) != hipSuccess) return e;
-        if (t.enc_mode == ENC_HOT)
-            hipLaunchKernelGGL(k_pack_lb<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a, l);
-        else
-            hipLaunchKernelGGL(k_pack_lb<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a, l);
-        return hipGetLastError();
+    // Range plan (the histogram's snapshots, hz_hist16_ranges): every pack wave takes whole ranges,
+    // so the plan is used when the waves cover the ranges evenly; else count + scan + write.
+    const RangeGeom g = d_ranges ? range_geom(nsym) : RangeGeom{};
+    if (g.bytes && t.d_lenpair) {
+        uint64_t rw = (g.nranges + waves - 1) / waves;
+        if (rw > cap) rw = cap;
+        const uint64_t W = rw * waves;
+        if (W >= g.nranges || g.nranges % W == 0) {
+            const void* fr[3] = {(const void*)k_pack_write<ENC_DENSE, true>, (const void*)k_pack_write<ENC_HOT, true>,
+                                 (const void*)k_pack_write<ENC_WIDE, true>};
+            hipError_t e = ensure_lds_limit(fr[t.enc_mode], kLdsBytes);
+            if (e != hipSuccess) return e;
+            const RangeArgs r = range_args(d_ranges, g, d_err);
+            uint64_t dg = g.nranges < (uint64_t)ncu * 4 ? g.nranges : (uint64_t)ncu * 4;
+            hipLaunchKernelGGL(k_range_dot, dim3(dg), dim3(kDotThreads), 0, s, r, (const uint32_t*)t.d_lenpair);
+            hipLaunchKernelGGL(k_range_scan, dim3(1), dim3(kScanThreads), 0, s, r, start_bit);
+            a.rstart = r.start; a.bpr = g.bpr; a.nranges = g.nranges; a.blk_start = nullptr;
+            switch (t.enc_mode) {
+                case ENC_DENSE: hipLaunchKernelGGL((k_pack_write<ENC_DENSE, true>), dim3(rw), dim3(threads), lds, s, a); break;
+                case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, true>), dim3(rw), dim3(threads), lds, s, a); break;
+                default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, true>), dim3(rw), dim3(threads), lds, s, a); break;
+            }
+            if (used_ranges) *used_ranges = 1;
+            return hipGetLastError();
+        }
     }
     {
         hipError_t e = ensure_lds_limit((const void*)k_pack_count, kLen8LdsBytes);
         if (e != hipSuccess) return e;
-        const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE>, (const void*)k_pack_write<ENC_HOT>,
-                             (const void*)k_pack_write<ENC_WIDE>};
+        const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE, false>, (const void*)k_pack_write<ENC_HOT, false>,
+                             (const void*)k_pack_write<ENC_WIDE, false>};
         if ((e = ensure_lds_limit(fw[t.enc_mode], kLdsBytes)) != hipSuccess) return e;
     }
     {
@@ -1402,9 +1379,9 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
                        nblocks, (const unsigned long long*)tiles, blk_start);
     switch (t.enc_mode) {
-        case ENC_DENSE: hipLaunchKernelGGL(k_pack_write<ENC_DENSE>, dim3(wgs), dim3(threads), lds, s, a); break;
-        case ENC_HOT: hipLaunchKernelGGL(k_pack_write<ENC_HOT>, dim3(wgs), dim3(threads), lds, s, a); break;
-        default: hipLaunchKernelGGL(k_pack_write<ENC_WIDE>, dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_DENSE: hipLaunchKernelGGL((k_pack_write<ENC_DENSE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, false>), dim3(wgs), dim3(threads), lds, s, a); break;
+        default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
     }
     return hipGetLastError();
 }
@@ -1420,14 +1397,11 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 // is no per-lane refill state, so a symbol costs a window read, a table
 // lookup and an add. Tables (LDS, one copy per workgroup):
 //   DENSE: 2^K u16 symbols + 2-bit (len - min_len), K = max_len;
-//   LUT:   2^K1 u32 level-1 entries (leaf: 1<<31 | len<<16 | sym;
-//          link: nbits<<26 | offset), deeper levels in global memory.
+//   LUT:   2^K1 u32 level-1 entries (leaf / link, hz_internal.h),
+//          deeper levels in global memory.
 // Every code 16 bits (FIXED16): symbol i sits at bit start + 16 i, so that
 // decoder needs no index and no staging (k_decode_fixed16).
 // ===========================================================================
-#ifndef HZ_DEC_LEAF_OOB
-#define HZ_DEC_LEAF_OOB 1
-#endif
 #ifndef HZ_DEC_DESC
 #define HZ_DEC_DESC 1
 #endif
@@ -1489,8 +1463,8 @@ HZ_DEV void dec_lookup(const DecArgs& a, const uint32_t* lds, uint64_t win, uint
             e = lut_at(lds, a.l2, (e >> 10) + (uint32_t)((win << D) >> (64 - nb)));
             D += nb;
         }
-        L = (e >> 16) & 63u;
-        sym = e & 0xffffu;
+        L = lut_leaf_len(e);
+        sym = lut_leaf_sym(e);
     }
 }
 
@@ -1593,13 +1567,6 @@ HZ_DEV void dec_chain_offsets(uint64_t sub, uint64_t bs, uint64_t bits, int lane
 
 HZ_DEV void dec_store(const DecArgs& a, uint64_t b, int lane, const uint32_t* pk) {
     const uint64_t sym0 = b * kBlockSyms;
-#ifdef HZ_EXP_DEC_NOSTORE  // timing experiment only: no output
-    uint32_t x = 0;
-#pragma unroll
-    for (int i = 0; i < kSPT / 2; ++i) x ^= pk[i];
-    if (x == 0x9e3779b9u && a.nsym == 3) a.out[0] = 1;
-    return;
-#endif
     if (sym0 + kBlockSyms <= a.nsym) {
         // non-temporal (streaming) stores: the output is not read again by this kernel
         // (10.70 vs 11.15-11.37 ms at 16 GiB Zipf, round 3 A/B; buffer stores with nt / sc0 nt /
@@ -1706,8 +1673,8 @@ HZ_DEV void dec_group(const DecArgs& a, const uint32_t* lds, uint32_t* stg0, uin
                         Dd += nb;
                     }
                 }
-                L[c] = (ee >> 16) & 63u;
-                sym[c] = ee & 0xffffu;
+                L[c] = lut_leaf_len(ee);
+                sym[c] = lut_leaf_sym(ee);
             }
         }
 #pragma unroll
@@ -1794,8 +1761,8 @@ HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte
 // the byte offset of a global link's entry is (raw + index bits) * 4, one
 // v_add_lshl_u32; num_records covers the largest table (kLutMaxL2 entries).
 // Lanes resolved in LDS read past num_records (0, no memory access) instead of l2[0]:
-// 12.27-12.29 vs 12.33-12.37 ms at 16 GiB Zipf (round 3, A/B in one run).
-constexpr uint32_t kL2Dummy = 0xfffffff0u;
+// 12.27-12.29 vs 12.33-12.37 ms at 16 GiB Zipf (round 3, A/B in one run). A leaf's offset
+// computed as a link's is >= 4 * 2^21 and < 2^27 (hz_internal.h lut_leaf_entry): no wrap.
 static_assert(kLutGlobal + kLutMaxL2 == (1u << 21), "a leaf (bit 31) read as a link lands past num_records");
 HZ_DEV __amdgpu_buffer_rsrc_t lut_l2_rsrc(const uint32_t* l2) {
     return __builtin_amdgcn_make_buffer_rsrc(
@@ -1848,13 +1815,9 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
         const uint32_t ee = h[c] ? x[c] : e[c];
         const uint32_t byte = ((ee >> 10) + __builtin_amdgcn_ubfe(W[c], ee, ee >> 5)) << 2;
         r[c].e = ee;
-#if HZ_DEC_LEAF_OOB
-        // a leaf's byte offset is >= 4 (2^31 >> 10) = num_records of lut_l2_rsrc: the load returns 0
-        // without a memory access, as kL2Dummy did, with no select
+        // a leaf's byte offset lies in [4 * 2^21, 2^27): past num_records of lut_l2_rsrc, so the
+        // load returns 0 without a memory access, with no select (lut_leaf_entry)
         r[c].gi = byte;
-#else
-        r[c].gi = lut_leaf(ee) ? kL2Dummy : byte;
-#endif
     }
 }
 
@@ -1970,8 +1933,8 @@ HZ_DEV void dec_wave_pipe(const DecArgs& a, const uint32_t* lds, uint32_t* stg, 
         uint32_t g[C];
         auto finish = [&](int c, int q) {
             const uint32_t ee = (st[c].e >> 31) ? st[c].e : g[c];
-            pos[c] += (ee >> 16) & 63u;
-            const uint32_t sym = ee & 0xffffu;
+            pos[c] += lut_leaf_len(ee);
+            const uint32_t sym = lut_leaf_sym(ee);
             const int i = (c * kChainSyms + q) >> 1;
             if (q & 1) pk[i] |= sym << 16;
             else pk[i] = sym;
@@ -2051,18 +2014,18 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         auto finish = [&](int c, int q) {
             const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
 #if HZ_DEC_DESC
-            p1[c] -= (ee >> 16) & 63u;
+            p1[c] -= lut_leaf_len(ee);
 #else
-            p1[c] += (ee >> 16) & 63u;
+            p1[c] += lut_leaf_len(ee);
 #endif
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
-            // an even step keeps the whole entry; the odd step packs both symbols (low halves) by one v_perm
+            // an even step keeps the whole entry; the odd step packs both symbols (leaf bytes 1-2) by one v_perm
 #if HZ_DEC_PERM
-            if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x05040100u);
+            if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x06050201u);
             else pk[c / kChainsPerLane][i] = ee;
 #else
-            if (q & 1) pk[c / kChainsPerLane][i] |= ee << 16;
-            else pk[c / kChainsPerLane][i] = ee & 0xffffu;
+            if (q & 1) pk[c / kChainsPerLane][i] |= lut_leaf_sym(ee) << 16;
+            else pk[c / kChainsPerLane][i] = lut_leaf_sym(ee);
 #endif
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
@@ -2070,11 +2033,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-#ifdef HZ_EXP_DEC_NOGATHER  // timing experiment only (wrong symbols): no level-2 gathers
-                g[c + t] = st[c + t].gi ^ 0x80000000u;
-#else
                 g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
-#endif
         };
         issue4(0);
 #pragma unroll
@@ -2529,8 +2488,8 @@ HZ_DEV void lut_len2(const DecArgs& a, const uint32_t* lds, const BitReader (&r)
         gi[c] = lut_leaf(e[c]) ? 0u : lut_gnext32(e[c], W[c]);
     }
     const uint32_t g0 = a.l2[gi[0]], g1 = a.l2[gi[1]];
-    L[0] = (((e[0] >> 31) ? e[0] : g0) >> 16) & 63u;
-    L[1] = (((e[1] >> 31) ? e[1] : g1) >> 16) & 63u;
+    L[0] = lut_leaf_len((e[0] >> 31) ? e[0] : g0);
+    L[1] = lut_leaf_len((e[1] >> 31) ? e[1] : g1);
 }
 
 __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs y) {
@@ -2797,11 +2756,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
             uint32_t g[C];
 #pragma unroll
             for (int c = 0; c < C; ++c)
-#ifdef HZ_EXP_NOESC  // timing experiment only (wrong lengths): the walk without the escape gathers
-                if (pk[c]) g[c] = 18u + (pW[c] & 3u);
-#else
                 if (pk[c]) g[c] = a.esc[pW[c] >> (32 - a.m)];
-#endif
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (!pk[c]) continue;
@@ -2907,11 +2862,7 @@ __global__ __launch_bounds__(kWalkWaves * 64) void k_idx_walk(WalkArgs a) {
         for (int c = 0; c < C; ++c) {
             if (!fl[c]) continue;
             const uint64_t j = seg0[c] * (kSegBits / 128) + mcount[c];
-#ifdef HZ_EXP_WALK_NOSTORE  // timing experiment only: no bitmap stores
-            if ((mcount[c] & (GM - 1)) == GM - 1 && a.nseg == 3) {
-#else
             if ((mcount[c] & (GM - 1)) == GM - 1) {
-#endif
                 uint4* dst = reinterpret_cast<uint4*>(a.bmp) + (j - (GM - 1));
 #pragma unroll
                 for (uint32_t i = 0; i < GM; ++i)
@@ -3174,9 +3125,6 @@ static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long*
         if ((e = hipMemcpyAsync(h_changed, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         if (*h_changed == 0 || it > (int)y.nseg) break;
-#ifdef HZ_EXP_WALK_NOSTORE  // the experiment's bitmap is garbage: no fixed point to reach
-        if (it >= 1) break;
-#endif
     }
     const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,

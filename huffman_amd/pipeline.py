@@ -4,9 +4,10 @@ This is the flow `archive` runs, kept on the device end to end so it can be
 timed with inputs already resident in HBM (bench.py) and sharded across ranks
 (huffman_amd/dist.py):
 
-    hist16 (GPU) -> host codebook + header (reference semantics) -> encode
-    table upload -> pack (GPU, one bit stream + decode-unit index) -> decode
-    table upload (host build overlaps the pack kernel) -> decode (GPU)
+    hist16 (GPU, + the range plan) -> host codebook + header (reference
+    semantics) -> encode table upload -> pack (GPU, one bit stream + decode-unit
+    index; range starts from the plan, one pass over the input) -> decode table
+    upload (host build overlaps the pack kernel) -> decode (GPU)
 
 PyTorch provides device memory and the stream; every compute stage is a
 gfx950 kernel of libhuffman_amd.so.
@@ -54,7 +55,7 @@ class Plan:
 
 
 class StreamCodec:
-    def __init__(self, device_index=0):
+    def __init__(self, device_index=0, use_ranges=True):
         self.device = torch.device("cuda", device_index)
         torch.cuda.set_device(self.device)
         # A real (non-null) stream shared by torch and the library, so torch
@@ -64,10 +65,23 @@ class StreamCodec:
         self.dev = Device(device_index, stream=self.stream.cuda_stream)
         self.hist = torch.zeros(_lib.HZ_NSYM, dtype=torch.int64, device=self.device)
         self.timings = {}
+        # two-pass encode (hz_hist16_ranges / hz_pack_ranges): the plan of the last histogram's input
+        self.use_ranges = use_ranges
+        self.ranges = None
+        self._ranges_of = None
 
     # -- stages ---------------------------------------------------------------
     def histogram(self, x, accumulate=False):
-        self.dev.hist16(x.data_ptr(), x.numel(), self.hist.data_ptr(), accumulate)
+        n = x.numel()
+        rb = self.dev.ranges_bytes(n) if self.use_ranges and not accumulate else 0
+        if rb:
+            if self.ranges is None or self.ranges.numel() < rb:
+                self.ranges = torch.empty(rb, dtype=torch.uint8, device=self.device)
+            self.dev.hist16_ranges(x.data_ptr(), n, self.hist.data_ptr(), self.ranges.data_ptr(), accumulate)
+            self._ranges_of = (x.data_ptr(), n)
+        else:
+            self.dev.hist16(x.data_ptr(), n, self.hist.data_ptr(), accumulate)
+            self._ranges_of = None
         return self.hist
 
     def make_plan(self, hist_host, n_total, hist_local=None, first_shard=True, shard_bit_offset=0, last_byte=0,
@@ -95,8 +109,14 @@ class StreamCodec:
         return out, index
 
     def pack(self, x, plan, out, index):
-        self.dev.pack(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
-                      index.data_ptr())
+        """Pack x; with the range plan of x's histogram (the last histogram() call, same tensor,
+        unchanged since: stream order) in one pass over x, else count + scan + write."""
+        if self._ranges_of == (x.data_ptr(), x.numel()):
+            self.dev.pack_ranges(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
+                                 index.data_ptr(), self.ranges.data_ptr())
+        else:
+            self.dev.pack(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
+                          index.data_ptr())
         return out
 
     def decode(self, payload, nsym, index, out):

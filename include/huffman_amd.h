@@ -173,6 +173,31 @@ uint64_t hz_scratch_bytes(uint64_t nsym);
 int hz_pack(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t start_bit, uint32_t lead,
             uint8_t *d_out, uint64_t out_cap, uint64_t *d_index);
 
+/* ---- two-pass encode: the range plan ------------------------------------
+ * The reference reads its input three times on the device: the histogram
+ * (Compressor.cu:369-372), populateCWLength + the length scan (:543-553) and
+ * encodeFromCW (:573-576). hz_hist16 + hz_pack do the same (count pass, scan,
+ * write). The range plan removes the middle pass: hz_hist16_ranges computes the
+ * same histogram and also leaves, in d_ranges (hz_ranges_bytes(n) bytes,
+ * 16-byte aligned, caller-owned), the cumulative histogram of the input at the
+ * end of every range of whole blocks (about 2048 ranges); hz_pack_ranges turns
+ * them into every range's start bit with the codebook (a dot product with the
+ * code lengths and a scan, no input read) and packs each range in one pass.
+ * The output equals hz_pack's byte for byte.
+ *   - hz_ranges_bytes(n) is 0 for inputs too small for a plan (< 256 MiB);
+ *     both calls then behave as hz_hist16 / hz_pack and ignore d_ranges.
+ *   - d_in must be 16-byte aligned and must not change between the two calls
+ *     (stream order); d_ranges is overwritten by the next hz_hist16_ranges.
+ *   - hz_pack_ranges falls back to count + scan + write (same output) when the
+ *     codebook's packing waves cannot take the ranges evenly;
+ *     hz_last_pack_ranges(ctx) says which path the last hz_pack_ranges took. */
+uint64_t hz_ranges_bytes(uint64_t n);
+int hz_hist16_ranges(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, int accumulate,
+                     void *d_ranges);
+int hz_pack_ranges(hz_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t start_bit, uint32_t lead,
+                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_index, void *d_ranges);
+int hz_last_pack_ranges(hz_ctx *ctx);
+
 /* Decode nsym symbols from d_payload (bit stream as hz_pack writes it) into
  * d_out (2*nsym bytes, 16-byte aligned). d_index: the block index (from
  * hz_pack, or hz_index_build for an index-less stream). d_payload
@@ -209,7 +234,7 @@ int hz_archive_file(const char *path, int verbose);
 int hz_archive_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* Streaming extract of in_path into out_path through a device window of
  * chunk_bytes of payload (index-less: hz_index_build per window), bounded
- * host and device memory. hz_extract_file uses it with 512 MiB windows.
+ * host and device memory. hz_extract_file uses it with 256 MiB windows.
  * Replaces the whole-file buffers of Decompressor.cu:65-114,259-291. */
 int hz_extract_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* Stage split of the calling thread's last hz_archive_stream /

@@ -108,6 +108,102 @@ def test_long_codes_wide_tables(hz, depth, mode):
     assert hz.decode(blob) == data
 
 
+def _lut_global_entries(ln, code, k1, lvl):
+    """Entries of the decoder's global LUT levels (hz_codebook.cpp fill_level) at `lvl` index bits per level."""
+    syms = np.nonzero(ln)[0]
+
+    def level(sel, depth, nb):
+        # codes of `sel` with their first `depth` bits consumed; this table has nb index bits
+        rem = ln[sel].astype(np.int64) - depth
+        deep = sel[rem > nb]
+        if deep.size == 0:
+            return 0
+        r = ln[deep].astype(np.int64) - depth
+        q = (code[deep] >> (r - nb).astype(np.uint64)) & np.uint64((1 << nb) - 1)
+        total = 0
+        for qv in np.unique(q):
+            grp = deep[q == qv]
+            nb2 = int(min(int((ln[grp].astype(np.int64) - depth - nb).max()), lvl))
+            total += (1 << nb2) + level(grp, depth + nb, nb2)
+        return total
+    return level(syms, 0, k1)
+
+
+def test_lut_narrow_global_levels(hz):
+    """a codebook whose 9-bit global LUT levels would exceed kLutMaxL2 (2^21 - 65 536
+    entries) is built with narrower levels (hz_codebook.cpp build_dec_lut); pack, decode and the
+    index builder stay bit-exact on it. The prefix code (not a Huffman code of the input: the tables
+    take any prefix code) is 4096 caterpillars under 12-bit prefixes: lengths 13 .. 22, so every
+    level-1 (13-bit) prefix ending in 0 has a 9-bit-deep subtree."""
+    import ctypes
+    import torch
+    from huffman_amd import index_bytes
+    from huffman_amd._lib import Codebook
+    from huffman_amd.codec import Device
+    ln = np.zeros(65536, np.uint8)
+    code = np.zeros(65536, np.uint64)
+    for g in range(4096):
+        for j in range(11):
+            s = g * 11 + j
+            L = 13 + j if j < 10 else 22               # prefix g, then 0^j 1 (j < 10) or 0^10
+            ln[s] = L
+            code[s] = (g << (L - 12)) | (1 if j < 10 else 0)
+    assert _lut_global_entries(ln, code, 13, 9) > (1 << 21) - 65536     # 9-bit levels do not fit
+    assert _lut_global_entries(ln, code, 13, 8) <= (1 << 21) - 65536
+    cb = Codebook()
+    syms = np.nonzero(ln)[0]
+    cb.nsym, cb.max_len, cb.min_len = syms.size, int(ln.max()), int(ln[syms].min())
+    np.ctypeslib.as_array(cb.order)[:syms.size] = syms
+    np.ctypeslib.as_array(cb.len)[:] = ln
+    np.ctypeslib.as_array(cb.code)[:] = code
+    rng = np.random.default_rng(8)
+    sym = rng.choice(syms, size=(3 << 20) + 777).astype("<u2")
+    host = sym.view(np.uint8)
+    nsym = sym.size
+    dev = Device()
+    dev.upload(cb)
+    x = torch.from_numpy(host).cuda()
+    bits = int(ln[sym].astype(np.uint64).sum())
+    cap = (bits + 5) // 8 + 64
+    pay = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    idx = torch.full((index_bytes(nsym) // 8 + 4,), -1, dtype=torch.int64, device="cuda")
+    dev.pack(x.data_ptr(), x.numel(), 5, 0, pay.data_ptr(), cap, idx.data_ptr())
+    out = torch.empty(x.numel() + 16, dtype=torch.uint8, device="cuda")
+    dev.decode(pay.data_ptr(), cap, nsym, idx.data_ptr(), out.data_ptr())
+    rebuilt = torch.full_like(idx, -1)
+    dev.index_build(pay.data_ptr(), cap, 5, nsym, rebuilt.data_ptr())
+    dev.sync()
+    assert torch.equal(out[:x.numel()], x)
+    nb = index_bytes(nsym)
+    assert np.array_equal(idx.cpu().numpy().view(np.uint8)[:nb], rebuilt.cpu().numpy().view(np.uint8)[:nb])
+    ref = oracle_lib.pack_range(host, 0, nsym, ln, code, 5, cap)
+    assert np.array_equal(pay.cpu().numpy()[1:(5 + bits) // 8], ref[1:(5 + bits) // 8])
+
+
+def test_lut_leaf_symbols_with_high_bits(hz, codec):
+    """the pipelined decoder reads every LUT entry as a link, leaves included.
+    Symbols whose bits 9..5 are 30/31 (0x03C0 .. 0x03FF, the old leaf layout's widest bit-field)
+    given long all-ones codes decode bit-exact (the leaf layout keeps such reads past the table)."""
+    import torch
+    rng = np.random.default_rng(31)
+    hot = np.arange(0x03C0, 0x0400, dtype=np.uint16)                 # the rare, long-coded symbols
+    common = rng.integers(0x1000, 0x1400, size=1 << 21).astype(np.uint16)
+    rare = np.repeat(hot, np.arange(1, hot.size + 1))                 # ragged small counts: long codes
+    sym = np.concatenate([common, rare])
+    rng.shuffle(sym)
+    host = sym.astype("<u2").view(np.uint8)
+    x = torch.from_numpy(host).cuda()
+    plan, payload, index = codec.encode(x)
+    n = x.numel()
+    from huffman_amd import codebook_arrays
+    _, ln, _ = codebook_arrays(plan.cb)
+    assert int(ln[hot].max()) >= 18
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(payload, n // 2, index, out)
+    codec.sync()
+    assert torch.equal(out[:n], x)
+
+
 def test_uniform_dense_tables(hz):
     data = oracle_lib.generate(1 << 22, kind=0, seed=3).tobytes()   # all 65536 symbols, 16-bit codes
     blob = hz.encode(data)
@@ -213,20 +309,6 @@ def test_cli_device_and_host_codebook_paths(hz, tmp_path, name, host):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "DECOMPRESSED_FILE").read_bytes() == data
-
-
-@pytest.mark.parametrize("kind", ["zipf", "skewed"])
-def test_one_pass_pack_opt_in(hz, tmp_path, kind):
-    """The one-pass pack (HZ_PACK_LB=1: one resolver wave chains block starts while
-    packer waves count, wait and emit; DESIGN.md records why it is not the default)
-    writes the same archive as count + scan + write."""
-    data = _zipf_bytes((24 << 20) + 1, 17) if kind == "zipf" else _skewed_bytes(24 << 20, 9)
-    (tmp_path / "in.bin").write_bytes(data)
-    env = dict(os.environ, HZ_PACK_LB="1")
-    r = subprocess.run([os.path.join(hz.BIN_DIR, "archive"), "in.bin"], cwd=tmp_path, capture_output=True,
-                       text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr
-    assert (tmp_path / "in.bin.compressed").read_bytes() == oracle_lib.encode(data)
 
 
 def test_cli_exit_codes(hz, tmp_path):
