@@ -18,7 +18,7 @@ STATUS = {
     0: "HZ_OK", -1: "HZ_EINVAL", -2: "HZ_ENOMEM", -3: "HZ_EHIP", -4: "HZ_ETOOLONG",
     -5: "HZ_EFORMAT", -6: "HZ_ECAP", -7: "HZ_ETIMEOUT", -8: "HZ_EIO", -9: "HZ_ENODEV", -10: "HZ_ENOENT",
 }
-STAGE_HIST, STAGE_PACK, STAGE_DECODE, STAGE_INDEX = 0, 1, 2, 3
+STAGE_HIST, STAGE_PACK, STAGE_DECODE, STAGE_INDEX, STAGE_EXTRACT = 0, 1, 2, 3, 4
 
 
 class HZError(RuntimeError):
@@ -97,6 +97,7 @@ PROTOTYPES = [
     ("hz_last_pack_ranges", _I, [_P]),
     ("hz_decode", _I, [_P, _P, _U64, _U64, _P, _P]),
     ("hz_index_build", _I, [_P, _P, _U64, _U64, _U64, _P]),
+    ("hz_decode_indexless", _I, [_P, _P, _U64, _U64, _U64, _P, _P]),
     ("hz_last_kernel_ms", _I, [_P, _I, ctypes.POINTER(ctypes.c_float)]),
     ("hz_generate", _I, [_P, _P, _U64, _U64, _I, ctypes.c_double, _U64]),
     ("hz_archive_file", _I, [ctypes.c_char_p, _I]),

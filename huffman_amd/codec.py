@@ -221,6 +221,12 @@ class Device:
     def index_build(self, d_payload, payload_bytes, start_bit, nsym, d_index):
         check(self.lib.hz_index_build(self.h, d_payload, payload_bytes, start_bit, nsym, d_index), "hz_index_build")
 
+    def decode_indexless(self, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit=None):
+        """Decode an index-less stream (the `extract` path): no block index; d_end_bit (device u64) gets
+        the end bit of the last codeword (past payload_bytes * 8: too few codewords)."""
+        check(self.lib.hz_decode_indexless(self.h, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit),
+              "hz_decode_indexless")
+
     def generate(self, d_out, n, offset=0, kind=1, alpha=1.1, seed=42):
         check(self.lib.hz_generate(self.h, d_out, n, offset, kind, alpha, seed), "hz_generate")
 

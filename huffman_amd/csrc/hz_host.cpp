@@ -78,8 +78,10 @@ struct hz_ctx {
     unsigned long long* d_thr = nullptr;
     unsigned long long* d_cbws = nullptr;  // hz_codebook_build_device workspace
     double thr_alpha = -1.0;
-    hipEvent_t ev[4][2] = {};
-    bool ev_used[4] = {false, false, false, false};
+    hipEvent_t ev[5][2] = {};
+    bool ev_used[5] = {false, false, false, false, false};
+    unsigned long long* d_xidx = nullptr;  // hz_decode_indexless fallback: a block index
+    uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
            cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0;
@@ -139,7 +141,7 @@ extern "C" int hz_ctx_create(int device, void* stream, hz_ctx** out) {
     HZ_TRY(hipMemset(c->d_err, 0, 16));
     HZ_TRY(hipHostMalloc(&c->h_err, 16, hipHostMallocDefault));
     *c->h_err = 0;
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 5; ++i)
         for (int j = 0; j < 2; ++j) HZ_TRY(hipEventCreate(&c->ev[i][j]));
     *out = c.release();
     return HZ_OK;
@@ -159,8 +161,9 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
     (void)hipFree(c->d_thr);
     (void)hipFree(c->d_cbws);
     (void)hipHostFree(c->h_err);
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 5; ++i)
         for (int j = 0; j < 2; ++j) (void)hipEventDestroy(c->ev[i][j]);
+    (void)hipFree(c->d_xidx);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return HZ_OK;
@@ -196,7 +199,7 @@ static int arm_err_check(hz_ctx* c) {
 }
 
 extern "C" int hz_last_kernel_ms(hz_ctx* c, int stage, float* ms) {
-    if (!c || !ms || stage < 0 || stage > 3) return HZ_EINVAL;
+    if (!c || !ms || stage < 0 || stage > 4) return HZ_EINVAL;
     if (!c->ev_used[stage]) { *ms = 0.f; return HZ_OK; }
     HZ_TRY(hipEventElapsedTime(ms, c->ev[stage][0], c->ev[stage][1]));
     return HZ_OK;
@@ -497,6 +500,53 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     return arm_err_check(c);
 }
 
+extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                                   uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
+    if (!c) return HZ_EINVAL;
+    if (nsym == 0) return HZ_OK;
+    if (!d_payload || !d_out || (((uintptr_t)d_out) & 15)) return HZ_EINVAL;
+    if (c->t.dec_mode < 0) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    // nsym codewords end within nsym * max_len bits: the rest of a longer buffer is never walked
+    const uint64_t reach = (start_bit + nsym * (uint64_t)std::max(c->t.dec_max_len, 1) + 7) / 8 + 8;
+    if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
+    if (!seg_decode_supported(c->t) || payload_bytes < 16) {
+        // codebooks the two-pass decoder does not take: block index, then the block decoder
+        const uint64_t ib = hz_index_bytes(nsym);
+        if (c->xidx_cap < ib) {
+            HZ_TRY(hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_xidx);
+            c->d_xidx = nullptr;
+            c->xidx_cap = 0;
+            HZ_TRY(hipMalloc(&c->d_xidx, ib));
+            c->xidx_cap = ib;
+        }
+        HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
+        int rc = hz_index_build(c, d_payload, payload_bytes, start_bit, nsym, (uint64_t*)c->d_xidx);
+        if (rc) return rc;
+        const uint64_t* end = (const uint64_t*)c->d_xidx + index_blocks(nsym);
+        if (d_end_bit) HZ_TRY(hipMemcpyAsync(d_end_bit, end, 8, hipMemcpyDeviceToDevice, c->stream));
+        // a payload with fewer than nsym codewords (end bit all ones) must not reach the decoder
+        uint64_t eb = 0;
+        HZ_TRY(hipMemcpyAsync(&eb, end, 8, hipMemcpyDeviceToHost, c->stream));
+        if ((rc = hz_ctx_sync(c))) return rc;
+        if (eb > payload_bytes * 8) return HZ_OK;  // the caller sees the end bit past the payload
+        if ((rc = hz_decode(c, d_payload, payload_bytes, nsym, (const uint64_t*)c->d_xidx, d_out))) return rc;
+        HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
+        c->ev_used[HZ_STAGE_EXTRACT] = true;
+        return arm_err_check(c);
+    }
+    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit));
+    if (rc) return rc;
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
+    HZ_TRY(launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
+                                   reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err, c->h_err + 2,
+                                   c->ncu, c->stream));
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
+    c->ev_used[HZ_STAGE_EXTRACT] = true;
+    return arm_err_check(c);
+}
+
 // Zipf thresholds: thr[r-1] = floor(2^64 * sum_{j<=r} j^-alpha / H); thr[255] = max.
 static void zipf_thresholds(double alpha, unsigned long long* thr) {
     double H = 0.0;
@@ -639,17 +689,17 @@ int decode_image(const uint8_t* f, uint64_t len, std::vector<uint8_t>& out) {
         if ((rc = dpay.alloc(pay + 16))) return rc;
         HZ_TRY(hipMemsetAsync(dpay.p, 0, pay + 16, c->stream));
         HZ_TRY(hipMemcpyAsync(dpay.p, f + info.payload_byte, pay, hipMemcpyHostToDevice, c->stream));
-        if ((rc = didx.alloc(hz_index_bytes(nsym)))) return rc;
+        if ((rc = didx.alloc(16))) return rc;
         if ((rc = dout.alloc(2 * nsym + 16))) return rc;
-        if ((rc = hz_index_build(c, (const uint8_t*)dpay.p, pay, info.payload_bit, nsym, (uint64_t*)didx.p))) return rc;
-        // the index builder leaves the end bit at all ones when the payload holds
-        // fewer than nsym codewords (truncated or corrupt file): reject before decoding
+        // index-less decode (no block index); a payload with fewer than nsym codewords (truncated
+        // or corrupt file) ends past the payload: rejected
+        if ((rc = hz_decode_indexless(c, (const uint8_t*)dpay.p, pay, info.payload_bit, nsym, (uint8_t*)dout.p,
+                                      (uint64_t*)didx.p)))
+            return rc;
         uint64_t end_bit = 0;
-        HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(nsym), 8, hipMemcpyDeviceToHost,
-                              c->stream));
+        HZ_TRY(hipMemcpyAsync(&end_bit, didx.p, 8, hipMemcpyDeviceToHost, c->stream));
         if ((rc = hz_ctx_sync(c))) return rc;
         if (end_bit > pay * 8) return HZ_EFORMAT;
-        if ((rc = hz_decode(c, (const uint8_t*)dpay.p, (end_bit + 7) / 8, nsym, (const uint64_t*)didx.p, (uint8_t*)dout.p))) return rc;
         HZ_TRY(hipMemcpyAsync(out.data(), dout.p, 2 * nsym, hipMemcpyDeviceToHost, c->stream));
         if ((rc = hz_ctx_sync(c))) return rc;
     }
@@ -1242,7 +1292,7 @@ static int parse_header_for_extract(const std::vector<uint8_t>& head, hz_codeboo
 // redone at the max_len bound), and moves the unconsumed tail of the window to
 // the front of the other buffer before refilling it. The host's fread of the
 // next window overlaps the decode, and its fwrite of a round's output overlaps
-// the next round's upload and index build.
+// the next round's upload and index-less decode (hz_decode_indexless).
 static int hz_extract_stream_impl(const char* in_path, const char* out_path, uint64_t chunk_bytes, int verbose) {
     if (!in_path || !out_path || chunk_bytes < 4096) return HZ_EINVAL;
     chunk_bytes &= ~(uint64_t)15;
@@ -1295,7 +1345,7 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
         const auto ta = Clock::now();
         for (int i = 0; i < 2; ++i)
             if ((rc = dwin[i].alloc(W + 16))) return rc;
-        if ((rc = didx.alloc(hz_index_bytes(sym_cap)))) return rc;
+        if ((rc = didx.alloc(16))) return rc;  // the round's end bit
         if ((rc = dout.alloc(2 * sym_cap + 16))) return rc;
         if ((rc = hin.alloc(W))) return rc;
         for (int i = 0; i < 2; ++i)
@@ -1318,13 +1368,14 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
             return std::max<uint64_t>(k, 1);
         };
         uint64_t end_bit = 0;
+        // a round: the window's first kk codewords decoded index-less into dout, and their end bit
         auto launch_index = [&](uint64_t kk) -> int {
             hipEvent_t t0 = spans.mark(c->stream);
-            int r2 = hz_index_build(c, (const uint8_t*)dwin[cur].p, have, bit, kk, (uint64_t*)didx.p);
+            int r2 = hz_decode_indexless(c, (const uint8_t*)dwin[cur].p, have, bit, kk, (uint8_t*)dout.p,
+                                         (uint64_t*)didx.p);
             if (r2) return r2;
             spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
-            HZ_TRY(hipMemcpyAsync(&end_bit, (const uint64_t*)didx.p + index_blocks(kk), 8, hipMemcpyDeviceToHost,
-                                  c->stream));
+            HZ_TRY(hipMemcpyAsync(&end_bit, didx.p, 8, hipMemcpyDeviceToHost, c->stream));
             return HZ_OK;
         };
         // first fill
@@ -1347,10 +1398,6 @@ static int hz_extract_stream_impl(const char* in_path, const char* out_path, uin
                 if ((rc = launch_index(k)) || (rc = hz_ctx_sync(c))) return rc;
             }
             if (end_bit > have * 8) return HZ_EFORMAT;    // truncated file
-            hipEvent_t t0 = spans.mark(c->stream);
-            if ((rc = hz_decode(c, (const uint8_t*)dwin[cur].p, have, k, (const uint64_t*)didx.p, (uint8_t*)dout.p)))
-                return rc;
-            spans.add(t0, spans.mark(c->stream), &g_timing.kernel_ms);
             hipEvent_t t1 = spans.mark(c->stream);
             HZ_TRY(hipMemcpyAsync(hout[ob].p, dout.p, 2 * k, hipMemcpyDeviceToHost, c->stream));
             spans.add(t1, spans.mark(c->stream), &g_timing.d2h_ms);

@@ -218,6 +218,13 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
                               unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
                               hipStream_t s);  // synchronises the stream (iterates to a fixed point)
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
+// Index-less decode in two long-chain passes (no block index); d_end: the end bit of codeword nsym - 1.
+bool seg_decode_supported(const Tables& t);
+hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                                   uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
+                                   unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
+                                   hipStream_t s);  // synchronises the stream (fix-ups to a fixed point)
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit);
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -2603,6 +2603,7 @@ struct WalkArgs {
     unsigned long long* cnt;
     unsigned long long* ent;
     uint32_t* dirty;
+    uint32_t lead;            // k_seg_walk: lead-in bits before a chain's first segment
 };
 
 // 16 payload bytes at word w (4-aligned): zeros before word 0 / past the end.
@@ -3187,7 +3188,7 @@ static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int n
     w.nchains = (y.nseg + w.spc - 1) / w.spc;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
     w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
-    w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0];
+    w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0]; w.lead = kWalkLead;
     // chains tid and tid + T of every thread
     const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
     uint64_t wgs = (threads_needed + kWalkWaves * 64 - 1) / (kWalkWaves * 64);
@@ -3262,6 +3263,473 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
     if (e != hipSuccess) return e;
     if (t.dec_mode == DEC_DENSE) return finish_index<DEC_DENSE>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
     return finish_index<DEC_LUT>(a, y, first, tiles, d_index, h_scratch, lds, ncu, s);
+}
+
+// ===========================================================================
+// Index-less decode without a block index: the `extract` path of a reference
+// file (Decompressor.cu:259-291 decodes it serially). Two passes of LONG
+// chains over the payload, no boundary bitmap and no select:
+//   k_seg_walk   : lengths only (k_idx_walk's table, payload ring and escape
+//                  parking); per 4096-bit segment its ENTRY (absolute bit of
+//                  the first codeword starting at or after the segment's first
+//                  bit) and COUNT (codewords starting in it), per chain its EXIT
+//                  (the first codeword start at or after the chain's end)
+//   k_seg_fix    : a chain whose lead-in had not resynchronised disagrees with
+//                  the previous chain's exit at its first entry: walk the true
+//                  path from that exit, rewriting entries and counts, until it
+//                  lands on a recorded entry (from there both paths agree);
+//                  host loop to a fixed point (typically one pass)
+//   k_scan_*     : counts -> F[k], the number of the first codeword of segment k
+//   k_seg_decode : every chain decodes from its first segment's true entry and
+//                  emits the codewords [A_i, A_{i+1}), A = F rounded up to a
+//                  multiple of 8 (it decodes and drops the few before A_i, which
+//                  the previous chain emits): each lane's output is one
+//                  contiguous, 16-byte aligned run, stored 16 bytes at a time
+// ===========================================================================
+struct SegArgs {
+    uint64_t nseg, spc, nchains;
+    unsigned long long* ent;    // [nseg] entry bit of every segment
+    unsigned long long* cnt;    // [nseg] codewords starting in it
+    unsigned long long* xit;    // [nchains] exit bit of every walk chain
+    unsigned long long* first;  // [nseg] F (k_scan_apply of cnt)
+    uint32_t* dirty[2];         // k_seg_fix: chains to check, ping-pong
+    uint32_t* changed;
+    unsigned long long* end;    // k_seg_decode: end bit of codeword nsym - 1
+};
+
+constexpr int kSegWalkWaves = 16;
+constexpr uint32_t kSegRing = 16 + 1;  // payload ring words + pad (odd stride: lanes' rings start in distinct banks)
+
+__global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, SegArgs y) {
+    // the length table at LDS address 0 (k_idx_walk's layout), the rings after it
+    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 8];
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(wtab, a.lds_img, a.lds_words);
+    const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
+    constexpr uint32_t G = kWalkGroup;
+    const uint32_t k = (uint32_t)a.k, bias = (uint32_t)a.bias;
+    uint32_t* ring = lds + threadIdx.x * kSegRing;
+    const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = ch < y.nchains;
+    const uint64_t seg0 = (live ? ch : 0) * y.spc;
+    const uint64_t seg1 = seg0 + y.spc < y.nseg ? seg0 + y.spc : y.nseg;
+    const uint64_t cs = seg0 * kSegBits, ce = seg1 * kSegBits;
+    const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
+    const uint64_t P0 = a.start + a.bit_adj + x0;
+    const uint64_t bch = (P0 >> 7) - 1;  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
+    uint32_t off = (uint32_t)(P0 - 128 * bch);
+    const uint64_t abs0 = a.start + x0 - off;  // absolute stream bit of ring position p: abs0 + p
+    const uint32_t end = live ? off + (uint32_t)(ce - x0) : off;
+    uint32_t nb = off + (uint32_t)(cs - x0);   // the next segment start to cross
+    uint64_t sj = seg0;                        // the segment that starts at nb (seg1: the chain's end)
+    uint32_t cc = 0;                           // codewords since the last crossing
+    // off moved past nb: off is the first codeword start of segment sj (or the chain's exit)
+    auto cross = [&]() {
+        if (__builtin_expect(off >= nb, 0) && sj <= seg1 && live) {
+            if (sj > seg0) y.cnt[sj - 1] = cc;
+            if (sj < seg1) y.ent[sj] = abs0 + off;
+            else y.xit[ch] = abs0 + off;
+            cc = 0;
+            ++sj;
+            nb += kSegBits;
+        }
+    };
+    uint4 pre[G];
+    bool gin;
+    uint32_t w0, w1, sh, wn, nxt, f;
+    {
+        uint4 v[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch + g));
+        const uint64_t gb = (bch + 3) & ~(uint64_t)(G - 1);
+        gin = 4 * (gb + G) <= a.nwords && gb < a.nwords;
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) pre[g] = walk_load(a, 4 * (gb + g));
+#pragma unroll
+        for (int g = 0; g < 3; ++g) ring_put<1>(ring, (uint32_t)g, walk_fix(a, 4 * (bch + g), v[g]));
+        f = 3;
+        const uint32_t q0 = (off - 1) >> 5;
+        w0 = ring[q0];
+        w1 = ring[q0 + 1];
+        sh = (0u - off) & 31;
+        wn = q0 + 2;
+    }
+    cross();  // a chain at the stream's start begins on its first segment's entry
+    bool pk = false;
+    uint32_t pW = 0;
+    for (;;) {
+        if (!__any(off < end)) break;
+        const uint32_t lim = min(end, 128 * f - 96);  // filled data: w0, w1 and nxt lie below off + 96
+        nxt = ring[wn & 15];
+        auto shift = [&](uint32_t L) {
+            const int32_t r = (int32_t)sh - (int32_t)L;  // >= -32 (codes <= 32 bits)
+            const bool cr = r < 0;
+            w0 = cr ? w1 : w0;
+            w1 = cr ? nxt : w1;
+            sh = (uint32_t)(cr ? r + 32 : r);
+            wn += cr ? 1u : 0u;
+            nxt = ring[wn & 15];
+        };
+        // a parked chain (code longer than the table's k bits): one gather from the escape table
+        auto resolve = [&]() {
+            if (pk) {
+                const uint32_t L = a.esc[pW >> (32 - a.m)];
+                ++cc;
+                off += L;
+                shift(L);
+                pk = false;
+                cross();
+            }
+        };
+#pragma unroll
+        for (int half = 0; half < kWalkHalves; ++half) {
+#pragma unroll
+            for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
+                const bool ok = !pk & (off < lim);
+                const uint32_t W = __builtin_amdgcn_alignbit(w0, w1, sh);
+                uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
+                HZ_WALK_FENCE();
+                e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
+                const bool adv = ok & (e != 0u), park = ok ^ adv;
+                const uint32_t L = adv ? e + bias : 0u;
+                cc += adv ? 1u : 0u;
+                off += L;
+                shift(L);
+                pk |= park;
+                pW = park ? W : pW;
+                cross();
+            }
+            resolve();
+        }
+        // chunk f goes into the ring when the chain no longer needs chunk f - 4
+        bool ld = false;
+        if (f <= ((off - 1) >> 7) + 3) {
+            const uint64_t q = bch + f;
+            uint4 x = pick_group<G>(pre, (uint32_t)q & (G - 1));
+            if (!gin) x = walk_fix(a, 4 * q, x);
+            ring_put<1>(ring, f & 3, x);
+            ++f;
+            ld = ((q + 1) & (G - 1)) == 0;  // the group is in the ring: load the next one
+        }
+        if (ld) {
+            const uint64_t q = bch + f;
+            gin = 4 * (q + G) <= a.nwords;
+            if (gin) {
+                const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
+#pragma unroll
+                for (uint32_t i = 0; i < G; ++i) pre[i] = src[i];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < G; ++i) pre[i] = walk_load(a, 4 * (q + i));
+            }
+        }
+    }
+}
+
+// Chain i (>= 1) against chain i - 1's exit: the true path enters segment seg0(i) at xit[i - 1].
+// When that is not the recorded entry, walk the true path segment by segment (entries and counts
+// rewritten) until a segment's true entry equals its recorded one; a walk that leaves the chain
+// hands its exit to chain i + 1 for the next iteration. it == 0 checks every chain.
+template <int MODE>
+__global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, uint64_t start, int it) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint32_t* dr = y.dirty[it & 1];
+    uint32_t* dw = y.dirty[(it + 1) & 1];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < y.nchains; i += stride) {
+        if (it > 0 && !dr[i]) continue;
+        uint64_t s = i * y.spc;
+        const uint64_t s1 = s + y.spc < y.nseg ? s + y.spc : y.nseg;
+        uint64_t p = y.xit[i - 1];
+        if (p == y.ent[s]) continue;
+        BitReader r;
+        br_init(r, a, p + a.bit_adj);
+        bool met = false;
+        for (; s < s1; ++s) {
+            if (p == y.ent[s]) { met = true; break; }
+            y.ent[s] = p;
+            const uint64_t sb = start + (s + 1) * kSegBits;
+            uint64_t n = 0;
+            while (p < sb) {
+                uint32_t sym;
+                const uint32_t L = br_next<MODE>(r, a, lds, sym);
+                if (L == 0) { atomicOr(a.err, 2u); p = sb; break; }
+                p += L;
+                ++n;
+            }
+            y.cnt[s] = n;
+        }
+        if (!met) {  // the exit moved: chain i + 1 checks it next iteration
+            y.xit[i] = p;
+            if (i + 1 < y.nchains) dw[i + 1] = 1u;
+            atomicAdd(y.changed, 1u);
+        }
+    }
+}
+
+// Full decode of chains of segments (the pipelined decoder's LUT: level 1 + hot heads in
+// LDS, one global level). Lane chain i: segments [k0, k1) from ent[k0], codewords
+// [A0, A1) emitted (A = F rounded up to 8; A1 of the last chain = nsym). Per lane a
+// payload ring (k_seg_walk's) and a 32-symbol output ring in LDS; a code that needs the
+// global level parks its chain until the end of the half-round (one gather for all
+// parked chains), as the walk's escapes do. Full 16-byte groups leave as 16-byte stores
+// at 16-byte aligned output addresses.
+constexpr uint32_t kSegOutWords = 16 + 1;  // 32 u16 symbols + pad
+constexpr uint32_t kSegLaneWords = kSegRing + kSegOutWords;
+constexpr int kSegDecMaxWaves = 16;
+
+__global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a, DecArgs d, SegArgs y,
+                                                                     uint64_t nsym) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, d.lds_img, d.lds_words);
+    constexpr uint32_t G = kWalkGroup;
+    const uint32_t k = (uint32_t)d.k;
+    uint32_t* ring = lds + d.lds_words + threadIdx.x * kSegLaneWords;
+    uint16_t* obuf = reinterpret_cast<uint16_t*>(ring + kSegRing);
+    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
+    const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k0 = ch * y.spc;
+    const uint64_t k1 = k0 + y.spc < y.nseg ? k0 + y.spc : y.nseg;
+    uint64_t A0 = nsym, A1 = nsym;
+    uint32_t skip = 0;
+    uint64_t p0 = 0;
+    if (k0 < y.nseg) {
+        const uint64_t F0 = y.first[k0];
+        A0 = (F0 + 7) & ~7ull;
+        A0 = A0 < nsym ? A0 : nsym;
+        A1 = k1 < y.nseg ? ((y.first[k1] + 7) & ~7ull) : nsym;
+        A1 = A1 < nsym ? A1 : nsym;
+        skip = (uint32_t)(A0 - F0 < 8 ? A0 - F0 : 0);
+        p0 = y.ent[k0];
+    }
+    const bool live = A0 < A1;
+    uint64_t rem = live ? A1 - A0 : 0;     // codewords still to emit
+    uint64_t ob = A0;                      // output symbol of obuf slot fl
+    uint32_t oc = 0, fl = 0;               // symbols put / flushed (obuf slot = count & 31)
+    const uint64_t P0 = p0 + a.bit_adj;
+    const uint64_t bch = (P0 >> 7) - 1;
+    uint32_t off = (uint32_t)(P0 - 128 * bch);
+    const uint64_t abs0 = p0 - off;
+    uint4 pre[G];
+    bool gin;
+    uint32_t w0, w1, sh, wn, nxt, f;
+    {
+        uint4 v[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch + g));
+        const uint64_t gb = (bch + 3) & ~(uint64_t)(G - 1);
+        gin = 4 * (gb + G) <= a.nwords && gb < a.nwords;
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) pre[g] = walk_load(a, 4 * (gb + g));
+#pragma unroll
+        for (int g = 0; g < 3; ++g) ring_put<1>(ring, (uint32_t)g, walk_fix(a, 4 * (bch + g), v[g]));
+        f = 3;
+        const uint32_t q0 = (off - 1) >> 5;
+        w0 = ring[q0];
+        w1 = ring[q0 + 1];
+        sh = (0u - off) & 31;
+        wn = q0 + 2;
+    }
+    uint8_t* out = d.out;
+    bool pk = false;
+    uint32_t pgi = 0;
+    // one codeword (symbol s, length L) decoded: dropped while skip > 0, else put in obuf
+    auto put = [&](uint32_t sym, bool adv) {
+        const bool emit = adv & (skip == 0u);
+        skip -= (adv & (skip != 0u)) ? 1u : 0u;
+        obuf[oc & 31u] = (uint16_t)sym;  // slot oc is free (pending symbols: fl .. oc - 1, < 32)
+        oc += emit ? 1u : 0u;
+        rem -= emit ? 1u : 0u;
+    };
+    for (;;) {
+        if (!__any(rem > 0)) break;
+        const uint32_t lim = 128 * f - 96;
+        nxt = ring[wn & 15];
+        auto shift = [&](uint32_t L) {
+            const int32_t r = (int32_t)sh - (int32_t)L;
+            const bool cr = r < 0;
+            w0 = cr ? w1 : w0;
+            w1 = cr ? nxt : w1;
+            sh = (uint32_t)(cr ? r + 32 : r);
+            wn += cr ? 1u : 0u;
+            nxt = ring[wn & 15];
+        };
+        auto resolve = [&]() {
+            const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(l2r, pk ? pgi : 0xfffffff0u, 0, 0);
+            if (pk) {
+                const uint32_t L = lut_leaf_len(g);
+                put(lut_leaf_sym(g), true);
+                off += L;
+                shift(L);
+                pk = false;
+            }
+        };
+#pragma unroll
+        for (int half = 0; half < kWalkHalves; ++half) {
+#pragma unroll
+            for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
+                const bool ok = !pk & (rem > 0) & (off < lim);
+                const uint32_t W = __builtin_amdgcn_alignbit(w0, w1, sh);
+                uint32_t e = lds_at((W >> (32 - k)) << 2);
+                HZ_WALK_FENCE();
+                const bool h = lut_lds_link(e);
+                const uint32_t x = lds_at(((e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5)) << 2);  // past LDS unless h
+                HZ_WALK_FENCE();
+                e = h ? x : e;
+                const bool leaf = lut_leaf(e);
+                const bool adv = ok & leaf, park = ok & !leaf;
+                const uint32_t L = adv ? lut_leaf_len(e) : 0u;
+                put(lut_leaf_sym(e), adv);
+                off += L;
+                shift(L);
+                pk |= park;
+                pgi = park ? ((e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5)) << 2 : pgi;  // lut_l2_rsrc byte offset
+            }
+            resolve();
+        }
+        // whole 8-symbol groups leave as 16-byte stores (16-byte aligned: ob is a multiple of 8)
+        while (oc - fl >= 8u) {
+            const uint32_t b = fl & 31u;  // 8-aligned slot
+            const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + (b >> 1);
+            store_nt16(reinterpret_cast<uint4*>(out + 2 * ob), make_uint4(ow[0], ow[1], ow[2], ow[3]));
+            fl += 8;
+            ob += 8;
+        }
+        bool ld = false;
+        if (f <= ((off - 1) >> 7) + 3) {
+            const uint64_t q = bch + f;
+            uint4 xv = pick_group<G>(pre, (uint32_t)q & (G - 1));
+            if (!gin) xv = walk_fix(a, 4 * q, xv);
+            ring_put<1>(ring, f & 3, xv);
+            ++f;
+            ld = ((q + 1) & (G - 1)) == 0;
+        }
+        if (ld) {
+            const uint64_t q = bch + f;
+            gin = 4 * (q + G) <= a.nwords;
+            if (gin) {
+                const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
+#pragma unroll
+                for (uint32_t i = 0; i < G; ++i) pre[i] = src[i];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < G; ++i) pre[i] = walk_load(a, 4 * (q + i));
+            }
+        }
+    }
+    // the stream's last (partial) group: symbol by symbol
+    for (uint32_t j = fl; j < oc; ++j) {
+        const uint32_t v = obuf[j & 31u];
+        out[2 * (ob + (j - fl))] = (uint8_t)v;
+        out[2 * (ob + (j - fl)) + 1] = (uint8_t)(v >> 8);
+    }
+    if (live && A1 == nsym) *y.end = abs0 + off;  // past the payload: too few codewords (the caller checks)
+}
+
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
+    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
+    const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
+    // ent, cnt, first, xit (<= nseg chains) (u64); dirty[2] (u32); changed, end; tiles
+    return 4 * nseg + nseg + 4 + ntiles + 24;
+}
+
+bool seg_decode_supported(const Tables& t) {
+    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.dec_max_len <= 32 &&
+           t.dec_max_len <= t.dec_k + t.dec_level_bits;
+}
+
+hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                                   uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
+                                   unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
+                                   hipStream_t s) {
+    if (nsym == 0) return hipSuccess;
+    if (!seg_decode_supported(t)) return hipErrorInvalidValue;
+    DecArgs d;
+    fill_dec_args(d, t, d_payload, payload_bytes, nsym);
+    d.starts = nullptr; d.subs = nullptr; d.out = d_out; d.err = d_err;
+    if (d.nwords < 4) return hipErrorInvalidValue;
+    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    SegArgs y;
+    y.nseg = (bits + kSegBits - 1) / kSegBits;
+    if (y.nseg == 0) return hipErrorInvalidValue;
+    unsigned long long* p = d_scratch;
+    y.ent = p; p += y.nseg;
+    y.cnt = p; p += y.nseg;
+    y.first = p; p += y.nseg;
+    y.xit = p; p += y.nseg;
+    y.dirty[0] = reinterpret_cast<uint32_t*>(p);
+    y.dirty[1] = y.dirty[0] + y.nseg;
+    p += y.nseg;
+    y.changed = reinterpret_cast<uint32_t*>(p); p += 2;
+    y.end = p; p += 2;
+    unsigned long long* tiles = p;
+    WalkArgs w;
+    w.words = d.words; w.nwords = d.nwords; w.bit_adj = d.bit_adj;
+    w.start = start_bit; w.nseg = y.nseg;
+    w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
+    w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
+    w.bmp = nullptr; w.cnt = nullptr; w.ent = nullptr; w.dirty = nullptr;
+    // test hook: HZ_SEG_LEAD=<bits> (0: no lead-in, so nearly every chain takes the fix-up path)
+    static const uint32_t lead = [] { const char* v = getenv("HZ_SEG_LEAD"); return v ? (uint32_t)atoi(v) : kWalkLead; }();
+    w.lead = lead;
+    // 1. walk: chains of spc segments, one per lane
+    {
+        const uint32_t ring_bytes = kSegWalkWaves * 64 * kSegRing * 4;
+        hipError_t e = ensure_lds_limit((const void*)k_seg_walk, (int)ring_bytes);
+        if (e != hipSuccess) return e;
+        const uint64_t target = (uint64_t)kSegWalkWaves * 64 * (uint64_t)ncu;
+        y.spc = (y.nseg + target - 1) / target;
+        y.nchains = (y.nseg + y.spc - 1) / y.spc;
+        const uint64_t wgs = (y.nchains + kSegWalkWaves * 64 - 1) / (kSegWalkWaves * 64);
+        hipLaunchKernelGGL(k_seg_walk, dim3(wgs), dim3(kSegWalkWaves * 64), ring_bytes, s, w, y);
+    }
+    // 2. fix-ups to a fixed point (host loop)
+    {
+        hipError_t e = ensure_lds_limit((const void*)k_seg_fix<DEC_LUT>, kLdsBytes);
+        if (e != hipSuccess) return e;
+        uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
+        wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
+        for (int it = 0;; ++it) {
+            if ((e = hipMemsetAsync(y.changed, 0, 4, s)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nchains, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_seg_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y, start_bit,
+                               it);
+            if ((e = hipMemcpyAsync(h_scratch, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+            if (*h_scratch == 0 || it > (int)y.nchains) break;
+        }
+    }
+    // 3. F = exclusive scan of the counts
+    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
+    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
+                       (const unsigned long long*)tiles, y.first);
+    // 4. decode: as many waves as the LDS holds beside the table, one chain per lane
+    {
+        const uint32_t table = t.dec_lds_bytes;
+        const uint32_t lane_bytes = kSegLaneWords * 4;
+        int waves = (int)((kLdsBytes - table) / (64 * lane_bytes));
+        waves = waves > kSegDecMaxWaves ? kSegDecMaxWaves : waves;
+        if (waves < 1) return hipErrorInvalidValue;
+        hipError_t e = ensure_lds_limit((const void*)k_seg_decode, kLdsBytes);
+        if (e != hipSuccess) return e;
+        if ((e = hipMemsetAsync(y.end, 0xff, 8, s)) != hipSuccess) return e;
+        SegArgs z = y;
+        const uint64_t lanes = (uint64_t)waves * 64 * (uint64_t)ncu;
+        z.spc = (y.nseg + lanes - 1) / lanes;
+        z.nchains = (y.nseg + z.spc - 1) / z.spc;
+        const uint64_t wgs = (z.nchains + waves * 64 - 1) / (waves * 64);
+        hipLaunchKernelGGL(k_seg_decode, dim3(wgs), dim3(waves * 64), table + waves * 64 * lane_bytes, s, w, d, z,
+                           nsym);
+        if (d_end) {
+            if ((e = hipMemcpyAsync(d_end, y.end, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        }
+    }
+    return hipGetLastError();
 }
 
 }  // namespace hz

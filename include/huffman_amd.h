@@ -212,10 +212,24 @@ int hz_decode(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uin
 int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                    uint64_t nsym, uint64_t *d_index);
 
-/* Kernel timings of the last hz_hist16 / hz_pack / hz_decode call on this
- * context, in milliseconds (HIP events on the context stream). */
+/* Decode the first nsym codewords of an index-less stream (a .compressed file
+ * from the reference encoder; Decompressor.cu:259-291 decodes it serially) into
+ * d_out (2*nsym bytes, 16-byte aligned) with no block index: two passes of long
+ * chains over the payload (code lengths, then symbols written where the counts
+ * put them). *d_end_bit (device u64, optional) receives the end bit of codeword
+ * nsym - 1, counted from byte 0 of d_payload; a payload with fewer than nsym
+ * codewords gives an end bit past payload_bytes * 8 and undefined output (the
+ * caller checks, as `extract` does). Codebooks the two-pass decoder does not
+ * take (codes longer than 22 bits, DENSE / FIXED16 tables) go through
+ * hz_index_build + hz_decode, with the same result. Synchronises the stream. */
+int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                        uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
+
+/* Kernel timings of the last hz_hist16 / hz_pack / hz_decode / hz_index_build /
+ * hz_decode_indexless call on this context, in milliseconds (HIP events on the
+ * context stream). */
 int hz_last_kernel_ms(hz_ctx *ctx, int stage, float *ms);
-enum { HZ_STAGE_HIST = 0, HZ_STAGE_PACK = 1, HZ_STAGE_DECODE = 2, HZ_STAGE_INDEX = 3 };
+enum { HZ_STAGE_HIST = 0, HZ_STAGE_PACK = 1, HZ_STAGE_DECODE = 2, HZ_STAGE_INDEX = 3, HZ_STAGE_EXTRACT = 4 };
 
 /* Synthetic inputs on the device (DESIGN.md "Synthetic inputs"): byte i of the
  * stream = f(splitmix64(seed ^ (offset + i))); kind 0 uniform, 1 Zipf(alpha). */

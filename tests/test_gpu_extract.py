@@ -1,0 +1,116 @@
+"""The `extract` path without a block index (include/huffman_amd.h
+hz_decode_indexless: a length walk with per-segment entries and counts, the
+segment fix-ups, a count scan and the long-chain decoder) against the inputs it
+must restore and against hz_pack's own index (its end bit). The reference's
+decoder (Decompressor.cu:259-291) is serial; the CPU oracle pins the same
+streams in test_gpu.py / test_oracle.py, and the golden reference-encoder files
+go through this path via hz.decode (test_gpu.py::test_decode_golden_and_baseline_files).
+
+Tolerance: none -- every check is bit-exact (integer/bit work)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+@pytest.fixture(scope="module")
+def codec(built_lib):
+    from huffman_amd.pipeline import StreamCodec
+    return StreamCodec(0)
+
+
+def _check(codec, x, shift=0):
+    """Encode x on the device, decode its payload (optionally moved `shift` bytes into a
+    buffer) index-less; returns (output equal, end bit equal to pack's)."""
+    import torch
+    from huffman_amd import index_starts
+    n = x.numel()
+    nsym = n // 2
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    end_pack = int(index_starts(index.cpu().numpy(), nsym)[-1])
+    pay = payload
+    if shift:
+        pay = torch.zeros(payload.numel() + shift + 64, dtype=torch.uint8, device="cuda")
+        pay[shift:shift + payload.numel()] = payload
+    out = torch.empty(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+    end = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+    codec.dev.decode_indexless(pay.data_ptr(), pay.numel(), plan.start_bit + 8 * shift, nsym, out.data_ptr(),
+                               end.data_ptr())
+    codec.sync()
+    return bool(torch.equal(out[:2 * nsym], x[:2 * nsym])), int(end[0].item()) == end_pack + 8 * shift
+
+
+@pytest.mark.parametrize("n,shift", [(3, 0), (4099, 0), ((1 << 20) + 1, 0), ((1 << 20) + 2, 13), ((8 << 20) + 6, 0),
+                                     ((64 << 20) + 3, 5000), ((256 << 20) + 2, 0)])
+def test_indexless_zipf(codec, n, shift):
+    import torch
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=n % 97)
+    ok, end_ok = _check(codec, x, shift)
+    assert ok and end_ok
+
+
+@pytest.mark.parametrize("name", ["dense8", "short", "mid20", "long24"])
+def test_indexless_table_shapes(codec, name):
+    """Every table shape: the two-pass decoder where it applies (LUT tables, codes <= 22 bits),
+    hz_index_build + hz_decode otherwise (DENSE tables, codes > 22 bits): the same output."""
+    import torch
+    from test_gpu import _shape_stream
+    x = torch.from_numpy(_shape_stream(name)).cuda()
+    ok, end_ok = _check(codec, x)
+    assert ok and end_ok
+
+
+def test_indexless_uniform_fixed16(codec):
+    import torch
+    n = (16 << 20) + 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=0, alpha=1.1, seed=3)
+    ok, end_ok = _check(codec, x)
+    assert ok and end_ok
+
+
+def test_indexless_truncated_end_past_payload(codec):
+    """A payload cut short of nsym codewords: the end bit lands past the payload (the caller rejects)."""
+    import torch
+    n = (4 << 20) + 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=9)
+    plan, payload, _ = codec.encode(x)
+    cut = payload.numel() // 2
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    end = torch.zeros(2, dtype=torch.int64, device="cuda")
+    codec.dev.decode_indexless(payload.data_ptr(), cut, plan.start_bit, n // 2, out.data_ptr(), end.data_ptr())
+    codec.sync()
+    assert int(end[0].item()) > 8 * cut
+
+
+_NO_LEAD = r"""
+import sys, numpy as np
+sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+import oracle_lib, huffman_amd as hz
+data = oracle_lib.generate({n}, offset=0, kind=1, seed=12).tobytes()
+blob = oracle_lib.encode(data)
+assert hz.decode(blob) == data
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("lead", ["0", "64"])
+def test_indexless_fixups_without_lead_in(built_lib, lead):
+    """HZ_SEG_LEAD (test hook) shortens the walk chains' lead-in, so chains start unsynchronised and
+    the segment fix-ups (k_seg_fix) repair them: the file still decodes bit-exact."""
+    code = _NO_LEAD.format(root=ROOT, tests=os.path.join(ROOT, "tests"), n=(24 << 20) + 1)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, HZ_SEG_LEAD=lead))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
