@@ -354,6 +354,22 @@ def main():
     index_build = {"ms": round(codec.dev.kernel_ms(STAGE_INDEX), 3),
                    "matches_pack_index": bool(torch.equal(rebuilt[:nidx], state["index"][:nidx]))}
     del rebuilt
+    # `extract` of an index-less file on the device: hz_decode_indexless (no block index; two long-chain
+    # passes), its output checked against the input, its end bit against pack's index
+    from huffman_amd._lib import STAGE_EXTRACT
+    endb = torch.zeros(2, dtype=torch.int64, device=dev)
+    xms = []
+    for _ in range(2):
+        out.fill_(0)
+        codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit, nsym,
+                                   out.data_ptr(), endb.data_ptr())
+        codec.sync()
+        xms.append(codec.dev.kernel_ms(STAGE_EXTRACT))
+    nb_idx = (nsym + 2047) // 2048
+    extract = {"ms": round(float(np.mean(xms)), 3), "ms_runs": [round(v, 3) for v in xms],
+               "bit_exact": bool(torch.equal(out[:2 * nsym], x[:2 * nsym])),
+               "end_bit_matches_pack_index": int(endb[0].item()) == int(state["index"][nb_idx].item())}
+    ok = ok and extract["bit_exact"]
     reassembly = None
     if world > 1 and not args.no_reassemble:
         reassembly = reassemble(codec, plan, state["payload"], rank, world, n_total, kind, args, dev)
@@ -426,6 +442,7 @@ def main():
                              "kernel_ms and host_* come from two further serialised steps",
             "roundtrip_bit_exact": ok,
             "index_build_from_payload": index_build,
+            "extract_indexless": extract,
             # algorithmic HBM bytes of one step per GPU: hist N + pack (N + C) + decode (C + N)
             "step_algorithmic_GBps": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9, 1),
             "step_hbm_frac": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
@@ -436,13 +453,14 @@ def main():
             "encode_GBps_kernels": round(N / (enc_ms / 1e3) / 1e9, 1),
             "decode_GBps_kernel": round(N / (avg["decode"] / 1e3) / 1e9, 1),
             # what `extract` of a real (index-less) file costs beside the encode: hist -> pack ->
-            # index rebuilt from the payload alone -> decode (kernel times, data resident)
+            # index-less decode of the payload alone (kernel times, data resident); the API path that
+            # rebuilds the block index first (hz_index_build + hz_decode) beside it
             "file_roundtrip": {
-                "ms": round(avg["hist"] + avg["pack"] + index_build["ms"] + avg["decode"], 3),
-                "GBps_of_input": round(N / ((avg["hist"] + avg["pack"] + index_build["ms"] + avg["decode"]) / 1e3)
-                                       / 1e9, 1),
-                "extract_ms": round(index_build["ms"] + avg["decode"], 3),
-                "extract_GBps_of_output": round(N / ((index_build["ms"] + avg["decode"]) / 1e3) / 1e9, 1),
+                "ms": round(avg["hist"] + avg["pack"] + extract["ms"], 3),
+                "GBps_of_input": round(N / ((avg["hist"] + avg["pack"] + extract["ms"]) / 1e3) / 1e9, 1),
+                "extract_ms": extract["ms"],
+                "extract_GBps_of_output": round(N / (extract["ms"] / 1e3) / 1e9, 1),
+                "index_build_plus_decode_ms": round(index_build["ms"] + avg["decode"], 3),
             },
             "reassembly_outside_step": reassembly,
             "roofline": {
@@ -469,7 +487,20 @@ def main():
                 "traffic": sum(enc_traffic) if None not in enc_traffic else None,
                 "algorithmic_bytes_per_launch": enc_algo,
             },
-            # the index builder every real `extract` of an index-less file pays
+            # `extract` of an index-less file: the payload read (twice: the length walk and the decode
+            # pass) and the output written; algorithmic bytes C + N (payload in, symbols out)
+            "extract_roofline": {
+                "kernels": ["seg_walk", "seg_fix", "scan", "seg_decode"],
+                "bound": "hbm",
+                "ms": extract["ms"],
+                "achieved": round((C + 2 * nsym) / (extract["ms"] / 1e3) / 1e9, 1) if extract["ms"] else None,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round((C + 2 * nsym) / (extract["ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4) if extract["ms"] else None,
+                "traffic": pmc_traffic("extract"),
+                "algorithmic_bytes_per_launch": C + 2 * nsym,
+            },
+            # the block-index builder (hz_index_build, the API path for callers that keep an index)
             "index_roofline": {
                 "kernels": ["index_build"],
                 "bound": "hbm",

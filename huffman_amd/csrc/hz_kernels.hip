@@ -3298,7 +3298,75 @@ struct SegArgs {
 };
 
 constexpr int kSegWalkWaves = 16;
-constexpr uint32_t kSegRing = 16 + 1;  // payload ring words + pad (odd stride: lanes' rings start in distinct banks)
+// Per-lane payload ring of k_seg_walk / k_seg_decode: 4 chunks of 4 words, then a copy of word 0 (so the
+// window's two words q, q + 1 never wrap), odd stride (lanes' rings start in distinct banks).
+constexpr uint32_t kSegRing = 16 + 1;
+
+// The 32-bit window at ring bit position p (p >= 1; bit 0 of the ring = bit 0 of chunk 0): words
+// (p - 1) >> 5 and the next one, one ds_read2_b32.
+HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
+    const uint32_t* w = ring + (((p - 1) >> 5) & 15u);
+    return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
+}
+
+// Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
+HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
+    const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ring[4 * q + i] = v[i];
+    if (q == 0) ring[16] = v[0];
+}
+
+// The ring's loader state: the next chunk f and the 64-byte register group it comes from.
+struct SegFeed {
+    uint4 pre[kWalkGroup];
+    bool gin;
+    uint64_t bch;  // payload chunk of ring chunk 0
+    uint32_t f;    // next chunk to put (chunks below f are in the ring)
+};
+
+// Chunks 0..2 of a ring whose bit 0 is payload word 4 * bch, and the group holding chunk 3.
+HZ_DEV void seg_feed_init(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint64_t bch) {
+    constexpr uint32_t G = kWalkGroup;
+    fd.bch = bch;
+    uint4 v[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch + g));
+    const uint64_t gb = (bch + 3) & ~(uint64_t)(G - 1);
+    fd.gin = 4 * (gb + G) <= a.nwords && gb < a.nwords;
+#pragma unroll
+    for (uint32_t g = 0; g < G; ++g) fd.pre[g] = walk_load(a, 4 * (gb + g));
+#pragma unroll
+    for (int g = 0; g < 3; ++g) seg_ring_put(ring, (uint32_t)g, walk_fix(a, 4 * (bch + g), v[g]));
+    fd.f = 3;
+}
+
+// Once per round: chunk f goes into the ring when the chain at p no longer needs chunk f - 4; the
+// next group is loaded once the current one is in the ring.
+HZ_DEV void seg_feed(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint32_t p) {
+    constexpr uint32_t G = kWalkGroup;
+    bool ld = false;
+    if (fd.f <= ((p - 1) >> 7) + 3) {
+        const uint64_t q = fd.bch + fd.f;
+        uint4 x = pick_group<G>(fd.pre, (uint32_t)q & (G - 1));
+        if (!fd.gin) x = walk_fix(a, 4 * q, x);
+        seg_ring_put(ring, fd.f & 3, x);
+        ++fd.f;
+        ld = ((q + 1) & (G - 1)) == 0;
+    }
+    if (ld) {
+        const uint64_t q = fd.bch + fd.f;
+        fd.gin = 4 * (q + G) <= a.nwords;
+        if (fd.gin) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
+#pragma unroll
+            for (uint32_t i = 0; i < G; ++i) fd.pre[i] = src[i];
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < G; ++i) fd.pre[i] = walk_load(a, 4 * (q + i));
+        }
+    }
+}
 
 __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, SegArgs y) {
     // the length table at LDS address 0 (k_idx_walk's layout), the rings after it
@@ -3306,7 +3374,6 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(wtab, a.lds_img, a.lds_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
-    constexpr uint32_t G = kWalkGroup;
     const uint32_t k = (uint32_t)a.k, bias = (uint32_t)a.bias;
     uint32_t* ring = lds + threadIdx.x * kSegRing;
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3316,113 +3383,56 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     const uint64_t cs = seg0 * kSegBits, ce = seg1 * kSegBits;
     const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
     const uint64_t P0 = a.start + a.bit_adj + x0;
-    const uint64_t bch = (P0 >> 7) - 1;  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
-    uint32_t off = (uint32_t)(P0 - 128 * bch);
-    const uint64_t abs0 = a.start + x0 - off;  // absolute stream bit of ring position p: abs0 + p
-    const uint32_t end = live ? off + (uint32_t)(ce - x0) : off;
-    uint32_t nb = off + (uint32_t)(cs - x0);   // the next segment start to cross
-    uint64_t sj = seg0;                        // the segment that starts at nb (seg1: the chain's end)
-    uint32_t cc = 0;                           // codewords since the last crossing
-    // off moved past nb: off is the first codeword start of segment sj (or the chain's exit)
+    SegFeed fd;
+    seg_feed_init(a, ring, fd, (P0 >> 7) - 1);  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
+    uint32_t p = (uint32_t)(P0 - 128 * fd.bch);    // ring bit position of the walk (>= 128)
+    const uint64_t abs0 = a.start + x0 - p;        // absolute stream bit of ring position q: abs0 + q
+    const uint32_t end = live ? p + (uint32_t)(ce - x0) : p;
+    uint32_t nb = p + (uint32_t)(cs - x0);         // the next segment start to cross
+    uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
+    uint32_t cc = 0;                               // codewords since the last crossing
+    // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
     auto cross = [&]() {
-        if (__builtin_expect(off >= nb, 0) && sj <= seg1 && live) {
+        if (__builtin_expect(p >= nb, 0) && sj <= seg1 && live) {
             if (sj > seg0) y.cnt[sj - 1] = cc;
-            if (sj < seg1) y.ent[sj] = abs0 + off;
-            else y.xit[ch] = abs0 + off;
+            if (sj < seg1) y.ent[sj] = abs0 + p;
+            else y.xit[ch] = abs0 + p;
             cc = 0;
             ++sj;
             nb += kSegBits;
         }
     };
-    uint4 pre[G];
-    bool gin;
-    uint32_t w0, w1, sh, wn, nxt, f;
-    {
-        uint4 v[3];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch + g));
-        const uint64_t gb = (bch + 3) & ~(uint64_t)(G - 1);
-        gin = 4 * (gb + G) <= a.nwords && gb < a.nwords;
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) pre[g] = walk_load(a, 4 * (gb + g));
-#pragma unroll
-        for (int g = 0; g < 3; ++g) ring_put<1>(ring, (uint32_t)g, walk_fix(a, 4 * (bch + g), v[g]));
-        f = 3;
-        const uint32_t q0 = (off - 1) >> 5;
-        w0 = ring[q0];
-        w1 = ring[q0 + 1];
-        sh = (0u - off) & 31;
-        wn = q0 + 2;
-    }
     cross();  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
     for (;;) {
-        if (!__any(off < end)) break;
-        const uint32_t lim = min(end, 128 * f - 96);  // filled data: w0, w1 and nxt lie below off + 96
-        nxt = ring[wn & 15];
-        auto shift = [&](uint32_t L) {
-            const int32_t r = (int32_t)sh - (int32_t)L;  // >= -32 (codes <= 32 bits)
-            const bool cr = r < 0;
-            w0 = cr ? w1 : w0;
-            w1 = cr ? nxt : w1;
-            sh = (uint32_t)(cr ? r + 32 : r);
-            wn += cr ? 1u : 0u;
-            nxt = ring[wn & 15];
-        };
-        // a parked chain (code longer than the table's k bits): one gather from the escape table
-        auto resolve = [&]() {
-            if (pk) {
-                const uint32_t L = a.esc[pW >> (32 - a.m)];
-                ++cc;
-                off += L;
-                shift(L);
-                pk = false;
-                cross();
-            }
-        };
+        if (!__any(p < end)) break;
+        const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
-                const bool ok = !pk & (off < lim);
-                const uint32_t W = __builtin_amdgcn_alignbit(w0, w1, sh);
+                const bool ok = !pk & (p < lim);
+                const uint32_t W = seg_window(ring, p);
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
                 HZ_WALK_FENCE();
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
-                const uint32_t L = adv ? e + bias : 0u;
                 cc += adv ? 1u : 0u;
-                off += L;
-                shift(L);
+                p += adv ? e + bias : 0u;
                 pk |= park;
                 pW = park ? W : pW;
                 cross();
             }
-            resolve();
-        }
-        // chunk f goes into the ring when the chain no longer needs chunk f - 4
-        bool ld = false;
-        if (f <= ((off - 1) >> 7) + 3) {
-            const uint64_t q = bch + f;
-            uint4 x = pick_group<G>(pre, (uint32_t)q & (G - 1));
-            if (!gin) x = walk_fix(a, 4 * q, x);
-            ring_put<1>(ring, f & 3, x);
-            ++f;
-            ld = ((q + 1) & (G - 1)) == 0;  // the group is in the ring: load the next one
-        }
-        if (ld) {
-            const uint64_t q = bch + f;
-            gin = 4 * (q + G) <= a.nwords;
-            if (gin) {
-                const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
-#pragma unroll
-                for (uint32_t i = 0; i < G; ++i) pre[i] = src[i];
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < G; ++i) pre[i] = walk_load(a, 4 * (q + i));
+            // parked chains (codes longer than the table's k bits): one gather from the escape table
+            if (pk) {
+                p += a.esc[pW >> (32 - a.m)];
+                ++cc;
+                pk = false;
+                cross();
             }
         }
+        seg_feed(a, ring, fd, p);
     }
 }
 
@@ -3483,7 +3493,6 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
                                                                      uint64_t nsym) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, d.lds_img, d.lds_words);
-    constexpr uint32_t G = kWalkGroup;
     const uint32_t k = (uint32_t)d.k;
     uint32_t* ring = lds + d.lds_words + threadIdx.x * kSegLaneWords;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(ring + kSegRing);
@@ -3491,86 +3500,38 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k0 = ch * y.spc;
     const uint64_t k1 = k0 + y.spc < y.nseg ? k0 + y.spc : y.nseg;
-    uint64_t A0 = nsym, A1 = nsym;
-    uint32_t skip = 0;
-    uint64_t p0 = 0;
+    uint64_t A0 = nsym, A1 = nsym, F0 = nsym, p0 = 0;
     if (k0 < y.nseg) {
-        const uint64_t F0 = y.first[k0];
+        F0 = y.first[k0];
         A0 = (F0 + 7) & ~7ull;
         A0 = A0 < nsym ? A0 : nsym;
         A1 = k1 < y.nseg ? ((y.first[k1] + 7) & ~7ull) : nsym;
         A1 = A1 < nsym ? A1 : nsym;
-        skip = (uint32_t)(A0 - F0 < 8 ? A0 - F0 : 0);
         p0 = y.ent[k0];
     }
     const bool live = A0 < A1;
-    uint64_t rem = live ? A1 - A0 : 0;     // codewords still to emit
-    uint64_t ob = A0;                      // output symbol of obuf slot fl
-    uint32_t oc = 0, fl = 0;               // symbols put / flushed (obuf slot = count & 31)
+    // oc: codewords decoded minus the 0..7 the previous chain emits (they take slots -skip .. -1, free
+    // slots of the output ring); the chain is done at oc == q. Symbols oc' in [fl, oc) are pending.
+    const int32_t q = live ? (int32_t)(A1 - A0) : 0;
+    int32_t oc = live ? -(int32_t)(A0 - F0) : 0, fl = 0;
+    uint64_t ob = A0;  // output symbol of slot fl
     const uint64_t P0 = p0 + a.bit_adj;
-    const uint64_t bch = (P0 >> 7) - 1;
-    uint32_t off = (uint32_t)(P0 - 128 * bch);
-    const uint64_t abs0 = p0 - off;
-    uint4 pre[G];
-    bool gin;
-    uint32_t w0, w1, sh, wn, nxt, f;
-    {
-        uint4 v[3];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) v[g] = walk_load(a, 4 * (bch + g));
-        const uint64_t gb = (bch + 3) & ~(uint64_t)(G - 1);
-        gin = 4 * (gb + G) <= a.nwords && gb < a.nwords;
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) pre[g] = walk_load(a, 4 * (gb + g));
-#pragma unroll
-        for (int g = 0; g < 3; ++g) ring_put<1>(ring, (uint32_t)g, walk_fix(a, 4 * (bch + g), v[g]));
-        f = 3;
-        const uint32_t q0 = (off - 1) >> 5;
-        w0 = ring[q0];
-        w1 = ring[q0 + 1];
-        sh = (0u - off) & 31;
-        wn = q0 + 2;
-    }
+    SegFeed fd;
+    seg_feed_init(a, ring, fd, (P0 >> 7) - 1);
+    uint32_t p = (uint32_t)(P0 - 128 * fd.bch);
+    const uint64_t abs0 = p0 - p;
     uint8_t* out = d.out;
     bool pk = false;
-    uint32_t pgi = 0;
-    // one codeword (symbol s, length L) decoded: dropped while skip > 0, else put in obuf
-    auto put = [&](uint32_t sym, bool adv) {
-        const bool emit = adv & (skip == 0u);
-        skip -= (adv & (skip != 0u)) ? 1u : 0u;
-        obuf[oc & 31u] = (uint16_t)sym;  // slot oc is free (pending symbols: fl .. oc - 1, < 32)
-        oc += emit ? 1u : 0u;
-        rem -= emit ? 1u : 0u;
-    };
+    uint32_t pW = 0, pe = 0;
     for (;;) {
-        if (!__any(rem > 0)) break;
-        const uint32_t lim = 128 * f - 96;
-        nxt = ring[wn & 15];
-        auto shift = [&](uint32_t L) {
-            const int32_t r = (int32_t)sh - (int32_t)L;
-            const bool cr = r < 0;
-            w0 = cr ? w1 : w0;
-            w1 = cr ? nxt : w1;
-            sh = (uint32_t)(cr ? r + 32 : r);
-            wn += cr ? 1u : 0u;
-            nxt = ring[wn & 15];
-        };
-        auto resolve = [&]() {
-            const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(l2r, pk ? pgi : 0xfffffff0u, 0, 0);
-            if (pk) {
-                const uint32_t L = lut_leaf_len(g);
-                put(lut_leaf_sym(g), true);
-                off += L;
-                shift(L);
-                pk = false;
-            }
-        };
+        if (!__any(oc < q)) break;
+        const uint32_t lim = 128 * fd.f - 96;
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
-                const bool ok = !pk & (rem > 0) & (off < lim);
-                const uint32_t W = __builtin_amdgcn_alignbit(w0, w1, sh);
+                const bool ok = !pk & (oc < q) & (p < lim);
+                const uint32_t W = seg_window(ring, p);
                 uint32_t e = lds_at((W >> (32 - k)) << 2);
                 HZ_WALK_FENCE();
                 const bool h = lut_lds_link(e);
@@ -3579,52 +3540,40 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
                 e = h ? x : e;
                 const bool leaf = lut_leaf(e);
                 const bool adv = ok & leaf, park = ok & !leaf;
-                const uint32_t L = adv ? lut_leaf_len(e) : 0u;
-                put(lut_leaf_sym(e), adv);
-                off += L;
-                shift(L);
+                obuf[oc & 31] = (uint16_t)lut_leaf_sym(e);  // slot oc is free: a symbol that does not count
+                oc += adv ? 1 : 0;                          // is overwritten by the next one
+                p += adv ? lut_leaf_len(e) : 0u;
                 pk |= park;
-                pgi = park ? ((e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5)) << 2 : pgi;  // lut_l2_rsrc byte offset
+                pW = park ? W : pW;
+                pe = park ? e : pe;
             }
-            resolve();
+            // parked chains: one gather of their global entries (a leaf: max_len <= K1 + level bits);
+            // other lanes read past num_records (0, no memory access)
+            const uint32_t gb = ((pe >> 10) + __builtin_amdgcn_ubfe(pW, pe, pe >> 5)) << 2;
+            const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(l2r, pk ? gb : 0xfffffff0u, 0, 0);
+            if (pk) {
+                obuf[oc & 31] = (uint16_t)lut_leaf_sym(g);
+                ++oc;
+                p += lut_leaf_len(g);
+                pk = false;
+            }
         }
         // whole 8-symbol groups leave as 16-byte stores (16-byte aligned: ob is a multiple of 8)
-        while (oc - fl >= 8u) {
-            const uint32_t b = fl & 31u;  // 8-aligned slot
-            const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + (b >> 1);
+        while (oc - fl >= 8) {
+            const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + ((fl & 31) >> 1);
             store_nt16(reinterpret_cast<uint4*>(out + 2 * ob), make_uint4(ow[0], ow[1], ow[2], ow[3]));
             fl += 8;
             ob += 8;
         }
-        bool ld = false;
-        if (f <= ((off - 1) >> 7) + 3) {
-            const uint64_t q = bch + f;
-            uint4 xv = pick_group<G>(pre, (uint32_t)q & (G - 1));
-            if (!gin) xv = walk_fix(a, 4 * q, xv);
-            ring_put<1>(ring, f & 3, xv);
-            ++f;
-            ld = ((q + 1) & (G - 1)) == 0;
-        }
-        if (ld) {
-            const uint64_t q = bch + f;
-            gin = 4 * (q + G) <= a.nwords;
-            if (gin) {
-                const uint4* src = reinterpret_cast<const uint4*>(a.words) + q;
-#pragma unroll
-                for (uint32_t i = 0; i < G; ++i) pre[i] = src[i];
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < G; ++i) pre[i] = walk_load(a, 4 * (q + i));
-            }
-        }
+        seg_feed(a, ring, fd, p);
     }
     // the stream's last (partial) group: symbol by symbol
-    for (uint32_t j = fl; j < oc; ++j) {
-        const uint32_t v = obuf[j & 31u];
-        out[2 * (ob + (j - fl))] = (uint8_t)v;
-        out[2 * (ob + (j - fl)) + 1] = (uint8_t)(v >> 8);
+    for (int32_t j = fl; j < oc; ++j) {
+        const uint32_t v = obuf[j & 31];
+        out[2 * (ob + (uint32_t)(j - fl))] = (uint8_t)v;
+        out[2 * (ob + (uint32_t)(j - fl)) + 1] = (uint8_t)(v >> 8);
     }
-    if (live && A1 == nsym) *y.end = abs0 + off;  // past the payload: too few codewords (the caller checks)
+    if (live && A1 == nsym) *y.end = abs0 + p;  // past the payload: too few codewords (the caller checks)
 }
 
 uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {

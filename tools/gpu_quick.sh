@@ -13,5 +13,5 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --steps 5 --warmup 2 > gpuru
 python - <<PY
 import json
 d=json.load(open("gpurun_out/q_bench_$T.json"))
-print({k: d[k] for k in ("value","ms_per_step","roundtrip_bit_exact","kernel_ms")}, d["encode_roofline"]["frac"], d["index_build_from_payload"])
+print({k: d[k] for k in ("value","ms_per_step","roundtrip_bit_exact","kernel_ms")}, "enc_frac", d["encode_roofline"]["frac"], "enc_ms", d["encode_roofline"]["ms"], d["index_build_from_payload"], d["extract_indexless"])
 PY
