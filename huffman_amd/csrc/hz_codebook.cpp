@@ -332,10 +332,22 @@ std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m) {
     return img;
 }
 
-std::vector<uint32_t> build_enc_esc(const hz_codebook* cb) {
-    std::vector<uint32_t> t(HZ_NSYM, 0u);
-    for (uint32_t s = 0; s < HZ_NSYM; ++s)
-        if (cb->len[s] && cb->len[s] <= (uint32_t)kNarrowMaxLen) t[s] = ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
+// HOT escapes: for every slot, the entry (len << 26 | code) of the symbol that does NOT own it, at
+// the slot's LDS word index hot_word(slot): a miss reads it at the byte offset of its slot's load.
+std::vector<uint32_t> build_enc_esc(const hz_codebook* cb, uint32_t m) {
+    std::vector<uint32_t> t(32768, 0u);
+    for (uint32_t slot = 0; slot < 32768; ++slot) {
+        const uint32_t cands[2] = {slot, slot ^ (m & 0x7fffu) ^ 0x8000u};
+        int best = -1;
+        for (uint32_t s : cands) {
+            const uint32_t L = cb->len[s];
+            if (!L || L > (uint32_t)kHotMaxLen) continue;
+            if (best < 0 || L < cb->len[best]) best = (int)s;
+        }
+        for (uint32_t s : cands)
+            if ((int)s != best && cb->len[s] && cb->len[s] <= (uint32_t)kNarrowMaxLen)
+                t[hot_word(slot)] = ((uint32_t)cb->len[s] << 26) | (uint32_t)cb->code[s];
+    }
     return t;
 }
 

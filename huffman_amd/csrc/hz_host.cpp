@@ -30,7 +30,7 @@ std::vector<uint32_t> build_enc_fixed16(const hz_codebook* cb);
 std::vector<uint32_t> build_dec_fixed16(const hz_codebook* cb);
 std::vector<uint32_t> build_enc_hot(const hz_codebook* cb, uint32_t m);
 uint32_t choose_hot_mask(const hz_codebook* cb);
-std::vector<uint32_t> build_enc_esc(const hz_codebook* cb);
+std::vector<uint32_t> build_enc_esc(const hz_codebook* cb, uint32_t m);
 std::vector<uint32_t> build_len8(const hz_codebook* cb);
 std::vector<uint32_t> build_lenpair(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
@@ -342,7 +342,7 @@ static int hz_codebook_upload_encode_impl(hz_ctx* c, const hz_codebook* cb) {
         std::vector<uint32_t> img = build_enc_hot(cb, t.hot_mask);
         t.enc_lds_bytes = (uint32_t)(img.size() * 4);
         if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_lds, &c->cap_enc_lds, img))) return rc;
-        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_esc, &c->cap_enc_esc, build_enc_esc(cb)))) return rc;
+        if ((rc = stage_copy(c, c->stage_enc, &t.d_enc_esc, &c->cap_enc_esc, build_enc_esc(cb, t.hot_mask)))) return rc;
     }
     if (mode == ENC_WIDE &&
         (rc = stage_copy(c, c->stage_enc, &t.d_enc_wide, &c->cap_enc_wide, build_enc_wide(cb))))

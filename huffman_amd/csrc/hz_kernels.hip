@@ -95,6 +95,11 @@ HZ_DEV uint32_t wave_incl_sum(uint32_t v) {
 }
 
 HZ_DEV uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+// LDS word at byte address `byte` of a kernel without static LDS (its dynamic
+// LDS starts at address 0): no base add per access.
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte); }
 // The wave's index in its workgroup as a wave-uniform (SGPR) value: block numbers derived from it,
 // and the index / start loads they address, stay on the scalar unit.
 HZ_DEV uint32_t wave_id() {
@@ -402,6 +407,13 @@ struct PackArgs {
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
 template <> struct PackEnt<ENC_WIDE> { using T = uint64_t; static constexpr int kShift = 56; };
+// Code length of a register entry. A HOT hit keeps its slot's tag in bit 31, so the u32 forms
+// read the 5-bit field (every u32 entry is <= 26 bits long: kNarrowMaxLen).
+template <int MODE>
+HZ_DEV uint32_t ent_len(typename PackEnt<MODE>::T e) {
+    if constexpr (MODE == ENC_WIDE) return (uint32_t)(e >> 56);
+    else return __builtin_amdgcn_ubfe((uint32_t)e, 26, 5);
+}
 
 template <typename T, int SH>
 HZ_DEV T pack_dense_one(const uint32_t* lds, uint32_t s) {
@@ -479,40 +491,52 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         xe = pack_dense_one<T, SH>(lds, xs);
         mid();
     } else if constexpr (MODE == ENC_HOT) {
-        const uint32_t m = a.hot_mask;
-        uint32_t any = 0;
+        // Slot arithmetic on both symbols of a word at once (packed 16-bit shifts): slot =
+        // s ^ (mask if bit 15), LDS word hot_word(slot); byte addresses (the table sits at LDS
+        // byte 0 of k_pack_write). A slot's entry carries its owner's bit 15 as the tag in bit 31:
+        // hit <=> bit 31 of entry ^ (s << 16) is 0. A miss is the slot's other symbol, whose
+        // entry the escape table holds at the same byte offset, so the escape address is one AND.
+        const uint32_t m2 = a.hot_mask | (a.hot_mask << 16);
+        uint32_t ad[kSPT];
+#pragma unroll
+        for (int j = 0; j < kSPT / 2; ++j) {
+            const uint32_t r = raw[j];
+            uint32_t sgn;
+            asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(sgn) : "v"(r));
+            const uint32_t sl = r ^ (sgn & m2);
+            uint32_t hi8;
+            asm("v_pk_lshrrev_b16 %0, 8, %1" : "=v"(hi8) : "v"(sl));
+            const uint32_t hw = sl ^ (hi8 & 0x003f003fu);
+            ad[2 * j] = (hw << 2) & 0x3fffcu;
+            ad[2 * j + 1] = (hw >> 14) & 0x3fffcu;
+        }
+        uint32_t x[kSPT];
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
-            const uint32_t s = (raw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            const uint32_t slot = s ^ (m & (uint32_t)((int32_t)(s << 16) >> 31));
-            uint32_t x = lds[hot_word(slot)] ^ ((s << 16) & 0x80000000u);
-            if (!FULL) x = k < nvalid ? x : 0u;
-            e[k] = (T)x;
-            any |= x;
+            x[k] = lds_at(ad[k]);
+            if (!FULL) x[k] = k < nvalid ? x[k] : 0u;
         }
-        const uint32_t xslot = xs ^ (m & (uint32_t)((int32_t)(xs << 16) >> 31));
-        const uint32_t xx = lds[hot_word(xslot)] ^ ((xs << 16) & 0x80000000u);
-        xe = (T)xx;
-        // The escape table holds entries in the register format. Every lane loads
-        // (lanes without a miss read esc[0], one coalesced address) and the blend is
-        // a v_bfi the compiler cannot turn back into a select: written as
-        // `miss ? esc[s] : e` the loads become 33 exec-masked branches (12.73-12.87
-        // vs 12.61-12.67 ms at 16 GiB Zipf, round 3 A/B); an empty asm forcing each
-        // loaded value at its load serialises the loads (18.9 ms).
-        (void)any;
+        uint32_t xslot = xs ^ ((uint32_t)((int32_t)(xs << 16) >> 31) & a.hot_mask);
+        xslot = hot_word(xslot & 0x7fffu) << 2;
+        const uint32_t xx = lds_at(xslot);
+        const char* esc = reinterpret_cast<const char*>(a.esc);
         uint32_t v[kSPT], mk[kSPT];
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
-            mk[k] = 0u - ((uint32_t)e[k] >> 31);
-            v[k] = a.esc[((raw[k >> 1] >> (16 * (k & 1))) & 0xffffu) & mk[k]];
+            const uint32_t tag = (k & 1) ? raw[k >> 1] : raw[k >> 1] << 16;  // the symbol's bit 15 in bit 31
+            mk[k] = (uint32_t)((int32_t)(x[k] ^ tag) >> 31);
+            v[k] = *reinterpret_cast<const uint32_t*>(esc + (ad[k] & mk[k]));
         }
-        const uint32_t xmk = 0u - (xx >> 31);
-        const uint32_t xv = a.esc[xs & xmk];
+        const uint32_t xmk = (uint32_t)((int32_t)(xx ^ (xs << 16)) >> 31);
+        const uint32_t xv = *reinterpret_cast<const uint32_t*>(esc + (xslot & xmk));
         mid();
+        // the blend is a v_bfi the compiler cannot turn back into a select: written as
+        // `miss ? esc[s] : e` the loads become 33 exec-masked branches (12.73-12.87 vs
+        // 12.61-12.67 ms at 16 GiB Zipf, round 3 A/B)
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
             uint32_t r;
-            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"((uint32_t)e[k]));
+            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"(x[k]));
             e[k] = (T)r;
         }
         {
@@ -614,7 +638,7 @@ HZ_DEV void pack_emit(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& acc,
     constexpr T CMASK = (T(1) << SH) - 1;
 #pragma unroll
     for (int k = 0; k < kSPT; ++k) {
-        const uint32_t L = (uint32_t)(e[k] >> SH);
+        const uint32_t L = ent_len<MODE>(e[k]);
         const uint64_t c = (uint64_t)(e[k] & CMASK);
         if (MODE == ENC_WIDE && L > 32) {
             const uint32_t Lh = L - 32;
@@ -646,7 +670,7 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
     uint32_t* base = slot - 1;
 #pragma unroll
     for (int k = 0; k < kSPT; ++k) {
-        const uint32_t L = (uint32_t)(e[k] >> SH);
+        const uint32_t L = ent_len<MODE>(e[k]);
         const uint32_t c = (uint32_t)e[k] & ((1u << SH) - 1u);
         acc = (acc << L) | c;
         t += L;
@@ -748,7 +772,7 @@ HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
 #pragma unroll
     for (int k = 0; k < kSPT; ++k) {
         if (k % kChainSyms == 0) b.nc[k / kChainSyms] = n;
-        n += (uint32_t)(b.e[k] >> SH);
+        n += ent_len<MODE>(b.e[k]);
     }
     const uint32_t sn = wave_incl_sum(n);
     b.n = n;
@@ -772,7 +796,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     if (blk > 0) {
         // Concatenation scan (associative; (0, 0) is its identity, which is what
         // DPP lanes without a source read) over lanes 0..31: rows, then row 0 into row 1.
-        uint32_t pn = (uint32_t)(b.pe >> SH);
+        uint32_t pn = ent_len<MODE>(b.pe);
         uint32_t pt = (uint32_t)(b.pe & CMASK);  // low 32 bits of the code
         auto step = [&](uint32_t on, uint32_t ot) {
             pt = pn >= 32 ? pt : ((ot << pn) | pt);
@@ -865,7 +889,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
         uint64_t t64 = 0;
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
-            const uint32_t L = (uint32_t)(b.e[k] >> SH);
+            const uint32_t L = ent_len<MODE>(b.e[k]);
             t64 = L ? ((t64 << L) | (uint64_t)(b.e[k] & CMASK)) : t64;
         }
         uint32_t tn = n, st = (uint32_t)t64;
@@ -1752,10 +1776,6 @@ HZ_DEV void dec_pipe_lds2(const DecArgs& a, const uint32_t* lds, const uint32_t*
 // together whatever the scheduler would do (the decoder is order-sensitive).
 #define HZ_WALK_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-// LDS word at byte address `byte` of a kernel without static LDS (its dynamic
-// LDS starts at address 0): no base add per access.
-typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
-HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte); }
 
 // Global table l2 as a buffer whose byte 0 lies kLutGlobal words before l2[0]:
 // the byte offset of a global link's entry is (raw + index bits) * 4, one
