@@ -241,6 +241,15 @@ extern "C" int hz_codebook_build_device(hz_ctx* c, const uint64_t* d_hist, hz_co
     return arm_err_check(c);
 }
 
+#ifdef HZ_SEG_DEBUG  // variant builds only: the context's scratch (tools/debug/seg_debug.py)
+extern "C" int hz_debug_scratch(hz_ctx* c, uint64_t* out, uint64_t words) {
+    HZ_TRY(hipStreamSynchronize(c->stream));
+    if (words > c->desc_cap) return HZ_EINVAL;
+    HZ_TRY(hipMemcpy(out, c->d_desc, words * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return HZ_OK;
+}
+#endif
+
 #ifdef HZ_CB_PROF  // variant builds only: k_cb_generate's phase timestamps (tools/debug/cb_prof.py)
 extern "C" int hz_debug_cb_prof(hz_ctx* c, uint64_t* out) {
     HZ_TRY(hipStreamSynchronize(c->stream));

@@ -46,6 +46,9 @@ HZ_DEV uint64_t splitmix64(uint64_t x) {
 
 HZ_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+typedef short hz_i16x2 __attribute__((ext_vector_type(2)));           // packed 16-bit lanes (v_pk_*)
+typedef unsigned short hz_u16x2 __attribute__((ext_vector_type(2)));
+
 // 16 bytes at a 4-byte aligned address (global_load/store_dwordx4 need only dword alignment): the
 // FIXED16 block kernels move a stream that starts at any word behind the header.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -501,11 +504,11 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
 #pragma unroll
         for (int j = 0; j < kSPT / 2; ++j) {
             const uint32_t r = raw[j];
-            uint32_t sgn;
-            asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(sgn) : "v"(r));
+            // (inline asm with an inline-constant shift would shift the high half by 0: VOP3P takes
+            // a constant for the low half only; vector types let the compiler place the operands)
+            const uint32_t sgn = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_i16x2, r) >> (hz_i16x2){15, 15});
             const uint32_t sl = r ^ (sgn & m2);
-            uint32_t hi8;
-            asm("v_pk_lshrrev_b16 %0, 8, %1" : "=v"(hi8) : "v"(sl));
+            const uint32_t hi8 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_u16x2, sl) >> (hz_u16x2){8, 8});
             const uint32_t hw = sl ^ (hi8 & 0x003f003fu);
             ad[2 * j] = (hw << 2) & 0x3fffcu;
             ad[2 * j + 1] = (hw >> 14) & 0x3fffcu;

@@ -101,7 +101,7 @@ def test_range_plan_equals_three_pass(dev, kind, n, start_bit, lead):
     import torch
     x = {"zipf": lambda: _zipf(n, 9), "skewed": lambda: _skewed(n, 4), "wide": lambda: _fib_wide(n, 2)}[kind]()
     n = x.numel()
-    (h3, p3, i3, _, _), (hr, pr, ir, took, rb), nb, cb = _both(dev, x, start_bit, lead)
+    ((h3, p3, i3, _, _), (hr, pr, ir, took, rb)), nb, cb = _both(dev, x, start_bit, lead)
     assert rb > 0
     assert took == 1, "the range plan did not run"
     assert np.array_equal(h3, hr)
@@ -117,7 +117,7 @@ def test_range_plan_small_input_is_three_pass(dev):
     import torch
     x = _zipf(64 * MIB + 1, 3)
     assert dev.ranges_bytes(x.numel()) == 0
-    (h3, p3, i3, _, _), (hr, pr, ir, took, rb), nb, _ = _both(dev, x, 0, 0)
+    ((h3, p3, i3, _, _), (hr, pr, ir, took, rb)), nb, _ = _both(dev, x, 0, 0)
     assert took == 0 and rb == 0
     assert np.array_equal(h3, hr) and np.array_equal(p3, pr)
     assert np.array_equal(i3.view(np.uint8)[:nb], ir.view(np.uint8)[:nb])
