@@ -209,16 +209,34 @@ HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s, Rec re
 
 // The 8 symbols of a 16-byte vector: 8 LDS atomics; a fix-up is due exactly when the
 // incremented half was 0xffff (the half a symbol counts in is its bit 0, the shift 16 * bit 0).
+// HZ_HIST_PK: hist_word of both symbols of a dword at once (packed 16-bit shifts and multiply),
+// byte addresses from the table at LDS byte 0.
+#ifndef HZ_HIST_PK
+#define HZ_HIST_PK 1
+#endif
 template <typename Rec = NoRec>
 HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v, Rec rec = Rec()) {
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
     uint32_t old[8], sh[8];
+#if HZ_HIST_PK
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const hz_u16x2 w = __builtin_bit_cast(hz_u16x2, wd[j]);
+        const hz_u16x2 hw = (w >> (hz_u16x2){1, 1}) ^ (((w >> (hz_u16x2){8, 8}) * (hz_u16x2){13, 13}) & (hz_u16x2){0x3f, 0x3f});
+        const uint32_t a = __builtin_bit_cast(uint32_t, hw);  // hist_word of both symbols (< 32768 each)
+        sh[2 * j] = (wd[j] << 4) & 16u;
+        sh[2 * j + 1] = (wd[j] >> 12) & 16u;
+        old[2 * j] = atomicAdd(&lds[a & 0x7fffu], 1u << sh[2 * j]);
+        old[2 * j + 1] = atomicAdd(&lds[a >> 16], 1u << sh[2 * j + 1]);
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
         sh[k] = (s << 4) & 16u;
         old[k] = atomicAdd(&lds[hist_word(s)], 1u << sh[k]);
     }
+#endif
     bool any = false;
 #pragma unroll
     for (int k = 0; k < 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
