@@ -1,6 +1,6 @@
 """Extract-path timing harness: encode one synthetic stream on the device, then time the index-less
 decode (hz_decode_indexless) R times and, for comparison, hz_index_build + hz_decode.
-usage: python tools/debug/extract_loop.py [bytes] [reps] [zipf|uniform]"""
+usage: python tools/debug/extract_loop.py [bytes] [reps] [zipf|uniform] [--only-indexless]"""
 import os
 import sys
 
@@ -12,6 +12,7 @@ from huffman_amd.pipeline import StreamCodec  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16 << 30
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 kind = 0 if (len(sys.argv) > 3 and sys.argv[3] == "uniform") else 1
+only = "--only-indexless" in sys.argv
 c = StreamCodec(0)
 x = torch.empty(n, dtype=torch.uint8, device="cuda")
 c.dev.generate(x.data_ptr(), n, offset=0, kind=kind, alpha=1.1, seed=42)
@@ -25,6 +26,9 @@ for r in range(reps):
     c.sync()
     xm = c.dev.kernel_ms(STAGE_EXTRACT)
     ok = torch.equal(out[:n - (n & 1)], x[:n - (n & 1)])
+    if only:
+        print(f"rep {r} indexless {xm:.3f} ms ok {ok}", flush=True)
+        continue
     c.dev.index_build(pay.data_ptr(), pay.numel(), plan.start_bit, n // 2, idx.data_ptr())
     c.decode(pay, n // 2, idx, out)
     c.sync()

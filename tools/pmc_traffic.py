@@ -28,21 +28,26 @@ import os
 from collections import defaultdict
 
 # stage -> (kernels of the stage, kernels that mark one launch of the stage)
+# k_scan_* (count scans) are shared by the three-pass pack, the index builder and the index-less
+# extract: they count toward "extract" (the stage whose dedicated run, tools/debug/extract_loop.py
+# --only-indexless, launches them alone); the range-plan pack has its own k_range_* kernels.
 STAGES = {
-    "hist": (("k_hist16",), ("k_hist16",)),
-    "pack": (("k_pack_count", "k_scan_reduce", "k_scan_tiles", "k_scan_apply", "k_pack_write", "k_pack_fixed16",
-              "k_pack_fixed16_blk"),
+    "hist": (("k_hist16", "k_hist16_rng"), ("k_hist16", "k_hist16_rng")),
+    "pack": (("k_pack_count", "k_range_dot", "k_range_scan", "k_pack_write", "k_pack_fixed16", "k_pack_fixed16_blk"),
              ("k_pack_write", "k_pack_fixed16")),
     "decode": (("k_decode", "k_decode_fixed16", "k_decode_fixed16_blk"), ("k_decode", "k_decode_fixed16")),
     "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
                "k_sync_subs"),
               ("k_sync_subs", "k_idx_fixed16")),
+    "extract": (("k_seg_walk", "k_seg_fix", "k_seg_decode", "k_scan_reduce", "k_scan_tiles", "k_scan_apply"),
+                ("k_seg_decode",)),
 }
 
 
 # kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
-WIDE_READ = ("k_hist16", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16", "k_pack_fixed16_blk",
-             "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk")
+WIDE_READ = ("k_hist16", "k_hist16_rng", "k_range_dot", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16",
+             "k_pack_fixed16_blk", "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk", "k_seg_walk",
+             "k_seg_decode")
 
 
 def _is(name, k):
@@ -116,7 +121,7 @@ def main():
             "fetch_doubled": sorted(ffixed[st]),
             "build_id": bid,
         }
-    res[a.dist] = ent
+    res.setdefault(a.dist, {}).update(ent)  # a later pass (e.g. the extract-only run) replaces its stages
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps({a.dist: ent}))

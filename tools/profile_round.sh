@@ -20,6 +20,13 @@ for D in zipf uniform; do
     python3 bench.py --dist $D --steps 1 --warmup 0 --no-cpu-baseline > $O/write_$D.log 2>&1
   python3 tools/pmc_traffic.py --fetch $O/fetch_$D --write $O/write_$D --dist $D --size $((16 << 30)) \
     --out $O/pmc_traffic.json
+  # the extract path alone (its count scans share kernel names with the index builder's)
+  timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/xfetch_$D -o run --output-format csv -- \
+    python3 tools/debug/extract_loop.py $((16 << 30)) 1 $D --only-indexless > $O/xfetch_$D.log 2>&1
+  timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/xwrite_$D -o run --output-format csv -- \
+    python3 tools/debug/extract_loop.py $((16 << 30)) 1 $D --only-indexless > $O/xwrite_$D.log 2>&1
+  python3 tools/pmc_traffic.py --fetch $O/xfetch_$D --write $O/xwrite_$D --dist $D --size $((16 << 30)) \
+    --out $O/pmc_traffic.json
 done
 if [ -x tools/microbench/mbc ]; then
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- \
