@@ -3350,6 +3350,33 @@ HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
     return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
 }
 
+// HZ_SEG_REGWIN: the window kept in registers (k_idx_walk's form: w0, w1 at a shift, the next ring
+// word read one step ahead, off the critical path) instead of two ring words read at p every step.
+#ifndef HZ_SEG_REGWIN
+#define HZ_SEG_REGWIN 0
+#endif
+struct SegWin {
+    uint32_t w0, w1, sh, wn, nxt;
+    HZ_DEV void init(const uint32_t* ring, uint32_t p) {
+        const uint32_t q0 = (p - 1) >> 5;
+        w0 = ring[q0 & 15u];
+        w1 = ring[(q0 + 1) & 15u];
+        sh = (0u - p) & 31u;
+        wn = q0 + 2;
+    }
+    HZ_DEV uint32_t window() const { return __builtin_amdgcn_alignbit(w0, w1, sh); }
+    HZ_DEV void reload(const uint32_t* ring) { nxt = ring[wn & 15u]; }  // after the ring's refill
+    HZ_DEV void step(const uint32_t* ring, uint32_t L) {  // L <= 32
+        const int32_t r = (int32_t)sh - (int32_t)L;
+        const bool cr = r < 0;
+        w0 = cr ? w1 : w0;
+        w1 = cr ? nxt : w1;
+        sh = (uint32_t)(cr ? r + 32 : r);
+        wn += cr ? 1u : 0u;
+        nxt = ring[wn & 15u];
+    }
+};
+
 // Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
@@ -3446,28 +3473,47 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     cross();  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
+#if HZ_SEG_REGWIN
+    SegWin wv;
+    wv.init(ring, p);
+#endif
     for (;;) {
         if (!__any(p < end)) break;
         const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
+#if HZ_SEG_REGWIN
+        wv.reload(ring);
+#endif
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (p < lim);
+#if HZ_SEG_REGWIN
+                const uint32_t W = wv.window();
+#else
                 const uint32_t W = seg_window(ring, p);
+#endif
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
                 HZ_WALK_FENCE();
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
+                const uint32_t L = adv ? e + bias : 0u;
                 cc += adv ? 1u : 0u;
-                p += adv ? e + bias : 0u;
+                p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 pk |= park;
                 pW = park ? W : pW;
                 cross();
             }
             // parked chains (codes longer than the table's k bits): one gather from the escape table
             if (pk) {
-                p += a.esc[pW >> (32 - a.m)];
+                const uint32_t L = a.esc[pW >> (32 - a.m)];
+                p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 ++cc;
                 pk = false;
                 cross();
@@ -3564,15 +3610,26 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
     uint8_t* out = d.out;
     bool pk = false;
     uint32_t pW = 0, pe = 0;
+#if HZ_SEG_REGWIN
+    SegWin wv;
+    wv.init(ring, p);
+#endif
     for (;;) {
         if (!__any(oc < q)) break;
         const uint32_t lim = 128 * fd.f - 96;
+#if HZ_SEG_REGWIN
+        wv.reload(ring);
+#endif
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (oc < q) & (p < lim);
+#if HZ_SEG_REGWIN
+                const uint32_t W = wv.window();
+#else
                 const uint32_t W = seg_window(ring, p);
+#endif
                 uint32_t e = lds_at((W >> (32 - k)) << 2);
                 HZ_WALK_FENCE();
                 const bool h = lut_lds_link(e);
@@ -3583,7 +3640,11 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
                 const bool adv = ok & leaf, park = ok & !leaf;
                 obuf[oc & 31] = (uint16_t)lut_leaf_sym(e);  // slot oc is free: a symbol that does not count
                 oc += adv ? 1 : 0;                          // is overwritten by the next one
-                p += adv ? lut_leaf_len(e) : 0u;
+                const uint32_t L = adv ? lut_leaf_len(e) : 0u;
+                p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 pk |= park;
                 pW = park ? W : pW;
                 pe = park ? e : pe;
@@ -3595,7 +3656,11 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
             if (pk) {
                 obuf[oc & 31] = (uint16_t)lut_leaf_sym(g);
                 ++oc;
-                p += lut_leaf_len(g);
+                const uint32_t L = lut_leaf_len(g);
+                p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 pk = false;
             }
         }
