@@ -3568,12 +3568,15 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
 // Full decode of chains of segments (the pipelined decoder's LUT: level 1 + hot heads in
 // LDS, one global level). Lane chain i: segments [k0, k1) from ent[k0], codewords
 // [A0, A1) emitted (A = F rounded up to 8; A1 of the last chain = nsym). Per lane a
-// payload ring (k_seg_walk's) and a 32-symbol output ring in LDS; a code that needs the
+// payload ring (k_seg_walk's) and a 16-symbol output ring in LDS; a code that needs the
 // global level parks its chain until the end of the half-round (one gather for all
 // parked chains), as the walk's escapes do. Full 16-byte groups leave as 16-byte stores
 // at 16-byte aligned output addresses.
-constexpr uint32_t kSegOutWords = 16 + 1;  // 32 u16 symbols + pad
+constexpr uint32_t kSegOutSyms = 16;       // output ring: flushed every half-round (<= 7 + 7 pending)
+constexpr uint32_t kSegOutWords = kSegOutSyms / 2 + 2;  // + pad: an odd lane stride (27 words)
 constexpr uint32_t kSegLaneWords = kSegRing + kSegOutWords;
+static_assert(kWalkSteps / kWalkHalves + 1 + 7 <= (int)kSegOutSyms, "a half-round fits the output ring");
+static_assert(kSegLaneWords & 1, "odd lane stride");
 constexpr int kSegDecMaxWaves = 16;
 
 __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a, DecArgs d, SegArgs y,
@@ -3599,6 +3602,7 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
     const bool live = A0 < A1;
     // oc: codewords decoded minus the 0..7 the previous chain emits (they take slots -skip .. -1, free
     // slots of the output ring); the chain is done at oc == q. Symbols oc' in [fl, oc) are pending.
+    constexpr int32_t OM = (int32_t)kSegOutSyms - 1;
     const int32_t q = live ? (int32_t)(A1 - A0) : 0;
     int32_t oc = live ? -(int32_t)(A0 - F0) : 0, fl = 0;
     uint64_t ob = A0;  // output symbol of slot fl
@@ -3638,7 +3642,7 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
                 e = h ? x : e;
                 const bool leaf = lut_leaf(e);
                 const bool adv = ok & leaf, park = ok & !leaf;
-                obuf[oc & 31] = (uint16_t)lut_leaf_sym(e);  // slot oc is free: a symbol that does not count
+                obuf[oc & OM] = (uint16_t)lut_leaf_sym(e);  // slot oc is free: a symbol that does not count
                 oc += adv ? 1 : 0;                          // is overwritten by the next one
                 const uint32_t L = adv ? lut_leaf_len(e) : 0u;
                 p += L;
@@ -3654,7 +3658,7 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
             const uint32_t gb = ((pe >> 10) + __builtin_amdgcn_ubfe(pW, pe, pe >> 5)) << 2;
             const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(l2r, pk ? gb : 0xfffffff0u, 0, 0);
             if (pk) {
-                obuf[oc & 31] = (uint16_t)lut_leaf_sym(g);
+                obuf[oc & OM] = (uint16_t)lut_leaf_sym(g);
                 ++oc;
                 const uint32_t L = lut_leaf_len(g);
                 p += L;
@@ -3663,19 +3667,19 @@ __global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a,
 #endif
                 pk = false;
             }
-        }
-        // whole 8-symbol groups leave as 16-byte stores (16-byte aligned: ob is a multiple of 8)
-        while (oc - fl >= 8) {
-            const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + ((fl & 31) >> 1);
-            store_nt16(reinterpret_cast<uint4*>(out + 2 * ob), make_uint4(ow[0], ow[1], ow[2], ow[3]));
-            fl += 8;
-            ob += 8;
+            // whole 8-symbol groups leave as 16-byte stores (16-byte aligned: ob is a multiple of 8)
+            while (oc - fl >= 8) {
+                const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + ((fl & OM) >> 1);
+                store_nt16(reinterpret_cast<uint4*>(out + 2 * ob), make_uint4(ow[0], ow[1], ow[2], ow[3]));
+                fl += 8;
+                ob += 8;
+            }
         }
         seg_feed(a, ring, fd, p);
     }
     // the stream's last (partial) group: symbol by symbol
     for (int32_t j = fl; j < oc; ++j) {
-        const uint32_t v = obuf[j & 31];
+        const uint32_t v = obuf[j & OM];
         out[2 * (ob + (uint32_t)(j - fl))] = (uint8_t)v;
         out[2 * (ob + (uint32_t)(j - fl)) + 1] = (uint8_t)(v >> 8);
     }
