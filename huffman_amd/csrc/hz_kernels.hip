@@ -249,19 +249,33 @@ HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v,
 }
 
 // Vectors [i0, end) of in4 with stride `step` from this thread's i0: software pipelined over
-// two register buffers (no copies), the next vector's load in flight while this one's LDS
-// atomics run (loads and LDS ops use separate counters).
+// HZ_HIST_DEPTH register buffers (no copies). One workgroup per CU leaves 16 waves to cover
+// HBM latency, so each lane keeps DEPTH - 1 loads in flight while one vector's LDS atomics
+// run (loads and LDS ops use separate counters). Refills past the end re-read the last
+// vector (branch-free, so the waits stay vmcnt(DEPTH - 1)); the tail counts what is left.
+#ifndef HZ_HIST_DEPTH
+#define HZ_HIST_DEPTH 4
+#endif
 template <typename Rec = NoRec>
 HZ_DEV void hist_sweep(uint32_t* lds, unsigned long long* hist, const uint4* in4, uint64_t i, uint64_t end,
                        uint64_t step, Rec rec = Rec()) {
-    uint4 va = i < end ? in4[i] : make_uint4(0, 0, 0, 0), vb;
-    for (; i < end; i += 2 * step) {
-        if (i + step < end) vb = in4[i + step];
-        hist_count8(lds, hist, va, rec);
-        if (i + step >= end) break;
-        if (i + 2 * step < end) va = in4[i + 2 * step];
-        hist_count8(lds, hist, vb, rec);
+    constexpr int D = HZ_HIST_DEPTH;
+    if (i >= end) return;
+    const uint64_t last = end - 1;
+    uint4 v[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[k] = in4[i + k * step < end ? i + k * step : last];
+    for (; i + (D - 1) * step < end; i += D * step) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            hist_count8(lds, hist, v[k], rec);
+            const uint64_t nx = i + (k + D) * step;
+            v[k] = in4[nx < end ? nx : last];
+        }
     }
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k)
+        if (i + k * step < end) hist_count8(lds, hist, v[k], rec);
 }
 
 // Adds the workgroup's LDS histogram to the global one.

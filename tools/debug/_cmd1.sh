@@ -8,7 +8,7 @@ for v in lib lib_regwin; do
   HZ_LIB_VARIANT=$v timeout -k 10 200 python tools/debug/extract_loop.py 17179869184 2 zipf --only-indexless > gpurun_out/xloop_$v.log 2>&1 || { tail -5 gpurun_out/xloop_$v.log; exit 4; }
   echo "$v: $(grep rep gpurun_out/xloop_$v.log | tr '\n' ' ')"
 done
-for v in lib lib_histold; do
+for v in lib lib_hd2 lib_histold; do
   HZ_LIB_VARIANT=$v timeout -k 10 200 python tools/debug/stage_loop.py 17179869184 3 zipf h > gpurun_out/hloop_$v.log 2>&1 || { tail -5 gpurun_out/hloop_$v.log; exit 5; }
   echo "$v: $(grep 'rep 2' gpurun_out/hloop_$v.log)"
 done
