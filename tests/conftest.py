@@ -47,3 +47,16 @@ def built_lib():
     build.build()
     import huffman_amd
     return huffman_amd.load()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _default_torch_stream():
+    """StreamCodec makes its own (non-blocking) stream torch's current stream for the process;
+    restore the default stream after every module, so a later module's Device(0) (the null
+    stream) and its torch tensors are ordered again."""
+    yield
+    if "torch" in sys.modules:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+            torch.cuda.set_stream(torch.cuda.default_stream())

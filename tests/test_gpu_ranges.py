@@ -64,7 +64,9 @@ def _both(dev, x, start_bit, lead):
     n = x.numel()
     nsym = n // 2
     hist = torch.zeros(65536, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # torch's fills / copies are on torch's stream, the library's calls on dev's
     dev.hist16(x.data_ptr(), n, hist.data_ptr())
+    dev.sync()
     h = hist.cpu().numpy().view(np.uint64).copy()
     cb = build_codebook(h)
     dev.upload_encode(cb)
@@ -77,6 +79,7 @@ def _both(dev, x, start_bit, lead):
             rb = dev.ranges_bytes(n)
             ranges = torch.empty(max(rb, 16), dtype=torch.uint8, device="cuda")
             hist2 = torch.zeros(65536, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
             dev.hist16_ranges(x.data_ptr(), n, hist2.data_ptr(), ranges.data_ptr())
             dev.pack_ranges(x.data_ptr(), n, start_bit, lead, out.data_ptr(), out.numel(), idx.data_ptr(),
                             ranges.data_ptr())
@@ -84,6 +87,7 @@ def _both(dev, x, start_bit, lead):
             dev.sync()
             res.append((hist2.cpu().numpy().view(np.uint64).copy(), out.cpu().numpy(), idx.cpu().numpy(), took, rb))
         else:
+            torch.cuda.synchronize()
             dev.pack(x.data_ptr(), n, start_bit, lead, out.data_ptr(), out.numel(), idx.data_ptr())
             dev.sync()
             res.append((h, out.cpu().numpy(), idx.cpu().numpy(), 0, 0))
