@@ -36,7 +36,8 @@ std::vector<uint32_t> build_lenpair(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl,
+                  std::vector<uint32_t>* seg_img = nullptr);
 void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
                     int& bias);
 }  // namespace hz
@@ -84,7 +85,7 @@ struct hz_ctx {
     uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
-           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0;
+           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_seg_lds = 0;
     int last_pack_ranges = 0;       // the last hz_pack_ranges call took the range plan
 };
 
@@ -114,6 +115,7 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_len8);
     (void)hipFree(t.d_lenpair);
     (void)hipFree(t.d_dec_lds);
+    (void)hipFree(t.d_seg_lds);
     (void)hipFree(t.d_dec_l2);
     (void)hipFree(t.d_walk_lds);
     (void)hipFree(t.d_walk_esc);
@@ -382,11 +384,16 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.dec_max_len = (int)cb->max_len;
     t.dec_min_len = (int)cb->min_len;
     const int mode = select_dec_mode(cb);
-    std::vector<uint32_t> dimg, l2, wimg, wesc;
+    std::vector<uint32_t> dimg, l2, wimg, wesc, simg;
     if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
     else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
-    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, t.dec_level_bits);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, t.dec_level_bits, &simg);
     if (rc) return rc;
+    t.seg_lds_bytes = 0;
+    if (!simg.empty()) {
+        if ((rc = stage_copy(c, c->stage_dec, &t.d_seg_lds, &c->cap_seg_lds, simg))) return rc;
+        t.seg_lds_bytes = (uint32_t)(simg.size() * 4);
+    }
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
     if (mode != DEC_FIXED16 && t.dec_lds_bytes + 4 * dec_slot_words_max(t.dec_max_len) > kLdsBytes)
@@ -509,6 +516,35 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     return arm_err_check(c);
 }
 
+// hz_decode_indexless through a rebuilt block index (hz_index_build, then the block decoder): for
+// codebooks the piece decoder does not take and segments with more pieces than it planned.
+static int hz_decode_indexless_via_index(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes,
+                                         uint64_t start_bit, uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
+    const uint64_t ib = hz_index_bytes(nsym);
+    if (c->xidx_cap < ib) {
+        HZ_TRY(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_xidx);
+        c->d_xidx = nullptr;
+        c->xidx_cap = 0;
+        HZ_TRY(hipMalloc(&c->d_xidx, ib));
+        c->xidx_cap = ib;
+    }
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
+    int rc = hz_index_build(c, d_payload, payload_bytes, start_bit, nsym, (uint64_t*)c->d_xidx);
+    if (rc) return rc;
+    const uint64_t* end = (const uint64_t*)c->d_xidx + index_blocks(nsym);
+    if (d_end_bit) HZ_TRY(hipMemcpyAsync(d_end_bit, end, 8, hipMemcpyDeviceToDevice, c->stream));
+    // a payload with fewer than nsym codewords (end bit all ones) must not reach the decoder
+    uint64_t eb = 0;
+    HZ_TRY(hipMemcpyAsync(&eb, end, 8, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = hz_ctx_sync(c))) return rc;
+    if (eb > payload_bytes * 8) return HZ_OK;  // the caller sees the end bit past the payload
+    if ((rc = hz_decode(c, d_payload, payload_bytes, nsym, (const uint64_t*)c->d_xidx, d_out))) return rc;
+    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
+    c->ev_used[HZ_STAGE_EXTRACT] = true;
+    return arm_err_check(c);
+}
+
 extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
                                    uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
     if (!c) return HZ_EINVAL;
@@ -519,38 +555,20 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
     // nsym codewords end within nsym * max_len bits: the rest of a longer buffer is never walked
     const uint64_t reach = (start_bit + nsym * (uint64_t)std::max(c->t.dec_max_len, 1) + 7) / 8 + 8;
     if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
-    if (!seg_decode_supported(c->t) || payload_bytes < 16) {
-        // codebooks the two-pass decoder does not take: block index, then the block decoder
-        const uint64_t ib = hz_index_bytes(nsym);
-        if (c->xidx_cap < ib) {
-            HZ_TRY(hipStreamSynchronize(c->stream));
-            (void)hipFree(c->d_xidx);
-            c->d_xidx = nullptr;
-            c->xidx_cap = 0;
-            HZ_TRY(hipMalloc(&c->d_xidx, ib));
-            c->xidx_cap = ib;
-        }
-        HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
-        int rc = hz_index_build(c, d_payload, payload_bytes, start_bit, nsym, (uint64_t*)c->d_xidx);
-        if (rc) return rc;
-        const uint64_t* end = (const uint64_t*)c->d_xidx + index_blocks(nsym);
-        if (d_end_bit) HZ_TRY(hipMemcpyAsync(d_end_bit, end, 8, hipMemcpyDeviceToDevice, c->stream));
-        // a payload with fewer than nsym codewords (end bit all ones) must not reach the decoder
-        uint64_t eb = 0;
-        HZ_TRY(hipMemcpyAsync(&eb, end, 8, hipMemcpyDeviceToHost, c->stream));
-        if ((rc = hz_ctx_sync(c))) return rc;
-        if (eb > payload_bytes * 8) return HZ_OK;  // the caller sees the end bit past the payload
-        if ((rc = hz_decode(c, d_payload, payload_bytes, nsym, (const uint64_t*)c->d_xidx, d_out))) return rc;
-        HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
-        c->ev_used[HZ_STAGE_EXTRACT] = true;
-        return arm_err_check(c);
-    }
-    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit));
+    // codebooks the piece decoder does not take: block index, then the block decoder
+    if (!seg_decode_supported(c->t) || payload_bytes < 16)
+        return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
+    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit, nsym, c->t.dec_max_len));
     if (rc) return rc;
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
-    HZ_TRY(launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
-                                   reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err, c->h_err + 2,
-                                   c->ncu, c->stream));
+    const hipError_t e = launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
+                                                 reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err,
+                                                 c->h_err + 2, c->ncu, c->stream);
+    if (e == hipErrorNotSupported) {  // more pieces in a segment than planned: through the block index
+        (void)hipGetLastError();
+        return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
+    }
+    HZ_TRY(e);
     HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
     c->ev_used[HZ_STAGE_EXTRACT] = true;
     return arm_err_check(c);

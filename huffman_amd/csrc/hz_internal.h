@@ -129,6 +129,40 @@ __host__ __device__ inline uint32_t lut_leaf_entry(uint32_t L, uint32_t sym) {
 __host__ __device__ inline uint32_t lut_leaf_len(uint32_t e) { return (e >> 24) & 63u; }
 __host__ __device__ inline uint32_t lut_leaf_sym(uint32_t e) { return (e >> 8) & 0xffffu; }
 constexpr int kDecMaxWaves = 16;
+// Index-less decoder (k_piece_decode, hz_kernels.hip): waves per workgroup and the per-wave LDS
+// of a group of segments (payload slot + output buffer). The walk records the start of every
+// 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
+#ifndef HZ_PIECE_WAVES
+#define HZ_PIECE_WAVES 12
+#endif
+constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
+struct PieceGeom {
+    uint32_t gs;          // segments per group (<= 8)
+    uint32_t rcap;        // piece records per segment (multiple of 8)
+    uint32_t slot_words;  // payload staging words (multiple of 4)
+    uint32_t obuf_syms;   // output buffer symbols (multiple of 8; 64 per-lane dummy slots follow)
+    uint32_t wave_words;
+};
+__host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words, uint32_t obuf_syms) {
+    return slot_words + (obuf_syms + 64) / 2;
+}
+// avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
+// over the expected count of a segment (a segment past it sets error flag 64: the caller
+// decodes through the block index instead).
+inline PieceGeom piece_geom(double avg_bits, int max_len) {
+    PieceGeom g;
+    const double per_seg = 4096.0 / (avg_bits > 1.0 ? avg_bits : 1.0);  // codewords per segment
+    const double recs = per_seg / 8.0;
+    uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 7.0) / 8.0) * 8u;
+    g.rcap = rcap < 8u ? 8u : (rcap > 520u ? 520u : rcap);
+    uint32_t gs = (uint32_t)(230.0 / (recs + 1.0));  // ~230 of a round's 256 pieces
+    g.gs = gs < 1u ? 1u : (gs > 8u ? 8u : gs);
+    g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;
+    g.obuf_syms = ((g.gs * 8u * (g.rcap + 1u) + 8u) + 7u) & ~7u;
+    g.wave_words = piece_wave_words(g.slot_words, g.obuf_syms);
+    return g;
+}
+
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
 // beside a 4-bit code-length table of the top kWalkK window bits.
@@ -180,7 +214,9 @@ struct Tables {
     uint32_t* d_lenpair = nullptr; // range plan: u8 lengths of both symbols of every histogram word (u16 each)
     uint32_t hot_mask = 0x8000;    // HOT pairing: s and s ^ hot_mask share slot
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
-    uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels
+    uint32_t* d_seg_lds = nullptr; // LUT: the index-less decoder's LDS image (level 1 + the heads beside its waves)
+    uint32_t seg_lds_bytes = 0;
+    uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels (shared by both images)
     uint64_t dec_l2_entries = 0;
     uint32_t* d_walk_lds = nullptr; // index walker: 4-bit code length - walk_bias per walk_k-bit window (0 = longer code)
     uint32_t walk_lds_bytes = 0;    // 0 = no walker tables (the segment walkers build the index)
@@ -223,8 +259,10 @@ bool seg_decode_supported(const Tables& t);
 hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                                    uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
                                    unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
-                                   hipStream_t s);  // synchronises the stream (fix-ups to a fixed point)
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit);
+                                   hipStream_t s);  // synchronises the stream (fix-ups to a fixed point);
+                                                    // hipErrorNotSupported: a segment holds more pieces than
+                                                    // planned (nothing written; decode through the index)
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len);
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -3322,24 +3322,26 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
 
 // ===========================================================================
 // Index-less decode without a block index: the `extract` path of a reference
-// file (Decompressor.cu:259-291 decodes it serially). Two passes of LONG
-// chains over the payload, no boundary bitmap and no select:
-//   k_seg_walk   : lengths only (k_idx_walk's table, payload ring and escape
-//                  parking); per 4096-bit segment its ENTRY (absolute bit of
-//                  the first codeword starting at or after the segment's first
-//                  bit) and COUNT (codewords starting in it), per chain its EXIT
-//                  (the first codeword start at or after the chain's end)
-//   k_seg_fix    : a chain whose lead-in had not resynchronised disagrees with
-//                  the previous chain's exit at its first entry: walk the true
-//                  path from that exit, rewriting entries and counts, until it
-//                  lands on a recorded entry (from there both paths agree);
-//                  host loop to a fixed point (typically one pass)
-//   k_scan_*     : counts -> F[k], the number of the first codeword of segment k
-//   k_seg_decode : every chain decodes from its first segment's true entry and
-//                  emits the codewords [A_i, A_{i+1}), A = F rounded up to a
-//                  multiple of 8 (it decodes and drops the few before A_i, which
-//                  the previous chain emits): each lane's output is one
-//                  contiguous, 16-byte aligned run, stored 16 bytes at a time
+// file (Decompressor.cu:259-291 decodes it serially). One pass of LONG chains
+// over the payload, then a block-parallel decode; no boundary bitmap, no select:
+//   k_seg_walk    : lengths only (k_idx_walk's table, payload ring and escape
+//                   parking); per 4096-bit segment its ENTRY (absolute bit of
+//                   the first codeword starting at or after the segment's first
+//                   bit), its COUNT (codewords starting in it) and the start of
+//                   every 8th codeword counted from its entry (a u16 offset from
+//                   the segment's first bit: the PIECE records); per chain its
+//                   EXIT (the first codeword start at or after the chain's end)
+//   k_seg_fix     : a chain whose lead-in had not resynchronised disagrees with
+//                   the previous chain's exit at its first entry: walk the true
+//                   path from that exit, rewriting entries, counts and records,
+//                   until it lands on a recorded entry (from there both paths
+//                   agree); host loop to a fixed point (typically one pass)
+//   k_scan_*      : counts -> F[k], the number of the first codeword of segment k
+//   k_piece_decode: one wave per group of segments; piece i of segment k is its
+//                   codewords [8 i, 8 i + 8) (F[k] + 8 i in the output), four
+//                   pieces per lane decoded like k_decode's chains (staged payload,
+//                   LDS tables, global gathers consumed a pair-walk later), the
+//                   group's symbols collected in LDS and stored contiguously
 // ===========================================================================
 struct SegArgs {
     uint64_t nseg, spc, nchains;
@@ -3347,9 +3349,11 @@ struct SegArgs {
     unsigned long long* cnt;    // [nseg] codewords starting in it
     unsigned long long* xit;    // [nchains] exit bit of every walk chain
     unsigned long long* first;  // [nseg] F (k_scan_apply of cnt)
+    uint16_t* rec;              // [nseg][rcap] piece records (16-byte aligned rows)
+    uint32_t rcap;              // records per segment (multiple of 8; more is an error, flag 64)
     uint32_t* dirty[2];         // k_seg_fix: chains to check, ping-pong
     uint32_t* changed;
-    unsigned long long* end;    // k_seg_decode: end bit of codeword nsym - 1
+    uint32_t* err;
 };
 
 constexpr int kSegWalkWaves = 16;
@@ -3363,33 +3367,6 @@ HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
     const uint32_t* w = ring + (((p - 1) >> 5) & 15u);
     return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
 }
-
-// HZ_SEG_REGWIN: the window kept in registers (k_idx_walk's form: w0, w1 at a shift, the next ring
-// word read one step ahead, off the critical path) instead of two ring words read at p every step.
-#ifndef HZ_SEG_REGWIN
-#define HZ_SEG_REGWIN 0
-#endif
-struct SegWin {
-    uint32_t w0, w1, sh, wn, nxt;
-    HZ_DEV void init(const uint32_t* ring, uint32_t p) {
-        const uint32_t q0 = (p - 1) >> 5;
-        w0 = ring[q0 & 15u];
-        w1 = ring[(q0 + 1) & 15u];
-        sh = (0u - p) & 31u;
-        wn = q0 + 2;
-    }
-    HZ_DEV uint32_t window() const { return __builtin_amdgcn_alignbit(w0, w1, sh); }
-    HZ_DEV void reload(const uint32_t* ring) { nxt = ring[wn & 15u]; }  // after the ring's refill
-    HZ_DEV void step(const uint32_t* ring, uint32_t L) {  // L <= 32
-        const int32_t r = (int32_t)sh - (int32_t)L;
-        const bool cr = r < 0;
-        w0 = cr ? w1 : w0;
-        w1 = cr ? nxt : w1;
-        sh = (uint32_t)(cr ? r + 32 : r);
-        wn += cr ? 1u : 0u;
-        nxt = ring[wn & 15u];
-    }
-};
 
 // Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
@@ -3473,13 +3450,45 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     uint32_t nb = p + (uint32_t)(cs - x0);         // the next segment start to cross
     uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
     uint32_t cc = 0;                               // codewords since the last crossing
+    // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 7
+    // codewords), held in rfl / roff until the half-round's end, then packed into rb (8 u16)
+    // and stored 16 bytes at a time.
+    uint32_t rb[4] = {0u, 0u, 0u, 0u}, rj = 0, roff = 0;
+    bool rfl = false;
+    auto rec_put = [&]() {
+        const uint32_t sl = rj & 7u, sh = (sl & 1u) << 4, v = (roff & 0xffffu) << sh, keep = ~(0xffffu << sh);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) rb[i] = (sl >> 1) == i ? ((rb[i] & keep) | v) : rb[i];
+        ++rj;
+        rfl = false;
+    };
+    auto rec_store = [&]() {  // the group of 8 holding record rj - 1
+        if (rj <= y.rcap)
+            *reinterpret_cast<uint4*>(y.rec + (sj - 1) * y.rcap + ((rj - 1) & ~7u)) = make_uint4(rb[0], rb[1], rb[2], rb[3]);
+        else
+            atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
+    };
+    // after a codeword: its end p is the start of the segment's codeword cc; every 8th is a record
+    auto note = [&](bool adv) {
+        const bool rn = adv & ((cc & 7u) == 0u) & (p < nb) & (sj > seg0);
+        roff = rn ? p + kSegBits - nb : roff;
+        rfl |= rn;
+    };
     // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
     auto cross = [&]() {
         if (__builtin_expect(p >= nb, 0) && sj <= seg1 && live) {
-            if (sj > seg0) y.cnt[sj - 1] = cc;
+            if (sj > seg0) {
+                y.cnt[sj - 1] = cc;
+                if (rfl) {
+                    rec_put();
+                    if ((rj & 7u) == 0u) rec_store();
+                }
+                if (rj & 7u) rec_store();  // the segment's last, partial group
+            }
             if (sj < seg1) y.ent[sj] = abs0 + p;
             else y.xit[ch] = abs0 + p;
             cc = 0;
+            rj = 0;
             ++sj;
             nb += kSegBits;
         }
@@ -3487,26 +3496,15 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     cross();  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
-#if HZ_SEG_REGWIN
-    SegWin wv;
-    wv.init(ring, p);
-#endif
     for (;;) {
         if (!__any(p < end)) break;
         const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
-#if HZ_SEG_REGWIN
-        wv.reload(ring);
-#endif
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (p < lim);
-#if HZ_SEG_REGWIN
-                const uint32_t W = wv.window();
-#else
                 const uint32_t W = seg_window(ring, p);
-#endif
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
                 HZ_WALK_FENCE();
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
@@ -3514,23 +3512,23 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
                 const uint32_t L = adv ? e + bias : 0u;
                 cc += adv ? 1u : 0u;
                 p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
                 pk |= park;
                 pW = park ? W : pW;
+                note(adv);
                 cross();
             }
             // parked chains (codes longer than the table's k bits): one gather from the escape table
             if (pk) {
                 const uint32_t L = a.esc[pW >> (32 - a.m)];
                 p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
                 ++cc;
                 pk = false;
+                note(true);
                 cross();
+            }
+            if (rfl) {
+                rec_put();
+                if ((rj & 7u) == 0u) rec_store();
             }
         }
         seg_feed(a, ring, fd, p);
@@ -3538,9 +3536,9 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
 }
 
 // Chain i (>= 1) against chain i - 1's exit: the true path enters segment seg0(i) at xit[i - 1].
-// When that is not the recorded entry, walk the true path segment by segment (entries and counts
-// rewritten) until a segment's true entry equals its recorded one; a walk that leaves the chain
-// hands its exit to chain i + 1 for the next iteration. it == 0 checks every chain.
+// When that is not the recorded entry, walk the true path segment by segment (entries, counts
+// and piece records rewritten) until a segment's true entry equals its recorded one; a walk that
+// leaves the chain hands its exit to chain i + 1 for the next iteration. it == 0 checks every chain.
 template <int MODE>
 __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, uint64_t start, int it) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -3568,6 +3566,11 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
                 if (L == 0) { atomicOr(a.err, 2u); p = sb; break; }
                 p += L;
                 ++n;
+                if ((n & 7u) == 0 && p < sb) {
+                    const uint64_t j = (n >> 3) - 1;
+                    if (j < y.rcap) y.rec[s * y.rcap + j] = (uint16_t)(p + kSegBits - sb);
+                    else atomicOr(y.err, 64u);
+                }
             }
             y.cnt[s] = n;
         }
@@ -3579,137 +3582,186 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
     }
 }
 
-// Full decode of chains of segments (the pipelined decoder's LUT: level 1 + hot heads in
-// LDS, one global level). Lane chain i: segments [k0, k1) from ent[k0], codewords
-// [A0, A1) emitted (A = F rounded up to 8; A1 of the last chain = nsym). Per lane a
-// payload ring (k_seg_walk's) and a 16-symbol output ring in LDS; a code that needs the
-// global level parks its chain until the end of the half-round (one gather for all
-// parked chains), as the walk's escapes do. Full 16-byte groups leave as 16-byte stores
-// at 16-byte aligned output addresses.
-constexpr uint32_t kSegOutSyms = 16;       // output ring: flushed every half-round (<= 7 + 7 pending)
-constexpr uint32_t kSegOutWords = kSegOutSyms / 2 + 2;  // + pad: an odd lane stride (27 words)
-constexpr uint32_t kSegLaneWords = kSegRing + kSegOutWords;
-static_assert(kWalkSteps / kWalkHalves + 1 + 7 <= (int)kSegOutSyms, "a half-round fits the output ring");
-static_assert(kSegLaneWords & 1, "odd lane stride");
-constexpr int kSegDecMaxWaves = 16;
+// Block-parallel decode of groups of y.gs segments (k_decode's chain machinery): the
+// group's payload bits [start + 4096 k0, + 4096 gs + 8 max_len) staged (descending) in the
+// wave's slot; rounds of 256 pieces, lane l taking pieces 64 c + l (c < 4) as two pairs
+// whose global gathers land behind the other pair's LDS walk; every symbol goes to the
+// wave's LDS output buffer at its place (slot 0 = output symbol F0 rounded down to 8), and
+// the group's run [F0, F1) leaves as 16-byte stores (2-byte stores at its two ends).
+constexpr uint32_t kPieceSyms = 8;  // codewords per piece: one decode chain
+constexpr int kPieceChains = 4;     // pieces per lane per round
+static_assert(kPieceChains == 4, "two pairs");
+constexpr uint32_t kPieceMaxGroup = 8;
+#ifndef HZ_PIECE_WAVES
+#define HZ_PIECE_WAVES 12
+#endif
+constexpr int kPieceWaves = HZ_PIECE_WAVES;
+static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
 
-__global__ __launch_bounds__(kSegDecMaxWaves * 64) void k_seg_decode(WalkArgs a, DecArgs d, SegArgs y,
-                                                                     uint64_t nsym) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, d.lds_img, d.lds_words);
-    const uint32_t k = (uint32_t)d.k;
-    uint32_t* ring = lds + d.lds_words + threadIdx.x * kSegLaneWords;
-    uint16_t* obuf = reinterpret_cast<uint16_t*>(ring + kSegRing);
-    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
-    const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t k0 = ch * y.spc;
-    const uint64_t k1 = k0 + y.spc < y.nseg ? k0 + y.spc : y.nseg;
-    uint64_t A0 = nsym, A1 = nsym, F0 = nsym, p0 = 0;
-    if (k0 < y.nseg) {
-        F0 = y.first[k0];
-        A0 = (F0 + 7) & ~7ull;
-        A0 = A0 < nsym ? A0 : nsym;
-        A1 = k1 < y.nseg ? ((y.first[k1] + 7) & ~7ull) : nsym;
-        A1 = A1 < nsym ? A1 : nsym;
-        p0 = y.ent[k0];
-    }
-    const bool live = A0 < A1;
-    // oc: codewords decoded minus the 0..7 the previous chain emits (they take slots -skip .. -1, free
-    // slots of the output ring); the chain is done at oc == q. Symbols oc' in [fl, oc) are pending.
-    constexpr int32_t OM = (int32_t)kSegOutSyms - 1;
-    const int32_t q = live ? (int32_t)(A1 - A0) : 0;
-    int32_t oc = live ? -(int32_t)(A0 - F0) : 0, fl = 0;
-    uint64_t ob = A0;  // output symbol of slot fl
-    const uint64_t P0 = p0 + a.bit_adj;
-    SegFeed fd;
-    seg_feed_init(a, ring, fd, (P0 >> 7) - 1);
-    uint32_t p = (uint32_t)(P0 - 128 * fd.bch);
-    const uint64_t abs0 = p0 - p;
-    uint8_t* out = d.out;
-    bool pk = false;
-    uint32_t pW = 0, pe = 0;
-#if HZ_SEG_REGWIN
-    SegWin wv;
-    wv.init(ring, p);
-#endif
-    for (;;) {
-        if (!__any(oc < q)) break;
-        const uint32_t lim = 128 * fd.f - 96;
-#if HZ_SEG_REGWIN
-        wv.reload(ring);
-#endif
-#pragma unroll
-        for (int half = 0; half < kWalkHalves; ++half) {
-#pragma unroll
-            for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
-                const bool ok = !pk & (oc < q) & (p < lim);
-#if HZ_SEG_REGWIN
-                const uint32_t W = wv.window();
-#else
-                const uint32_t W = seg_window(ring, p);
-#endif
-                uint32_t e = lds_at((W >> (32 - k)) << 2);
-                HZ_WALK_FENCE();
-                const bool h = lut_lds_link(e);
-                const uint32_t x = lds_at(((e >> 10) + __builtin_amdgcn_ubfe(W, e, e >> 5)) << 2);  // past LDS unless h
-                HZ_WALK_FENCE();
-                e = h ? x : e;
-                const bool leaf = lut_leaf(e);
-                const bool adv = ok & leaf, park = ok & !leaf;
-                obuf[oc & OM] = (uint16_t)lut_leaf_sym(e);  // slot oc is free: a symbol that does not count
-                oc += adv ? 1 : 0;                          // is overwritten by the next one
-                const uint32_t L = adv ? lut_leaf_len(e) : 0u;
-                p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
-                pk |= park;
-                pW = park ? W : pW;
-                pe = park ? e : pe;
-            }
-            // parked chains: one gather of their global entries (a leaf: max_len <= K1 + level bits);
-            // other lanes read past num_records (0, no memory access)
-            const uint32_t gb = ((pe >> 10) + __builtin_amdgcn_ubfe(pW, pe, pe >> 5)) << 2;
-            const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(l2r, pk ? gb : 0xfffffff0u, 0, 0);
-            if (pk) {
-                obuf[oc & OM] = (uint16_t)lut_leaf_sym(g);
-                ++oc;
-                const uint32_t L = lut_leaf_len(g);
-                p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
-                pk = false;
-            }
-            // whole 8-symbol groups leave as 16-byte stores (16-byte aligned: ob is a multiple of 8)
-            while (oc - fl >= 8) {
-                const uint32_t* ow = reinterpret_cast<const uint32_t*>(obuf) + ((fl & OM) >> 1);
-                store_nt16(reinterpret_cast<uint4*>(out + 2 * ob), make_uint4(ow[0], ow[1], ow[2], ow[3]));
-                fl += 8;
-                ob += 8;
-            }
-        }
-        seg_feed(a, ring, fd, p);
-    }
-    // the stream's last (partial) group: symbol by symbol
-    for (int32_t j = fl; j < oc; ++j) {
-        const uint32_t v = obuf[j & OM];
-        out[2 * (ob + (uint32_t)(j - fl))] = (uint8_t)v;
-        out[2 * (ob + (uint32_t)(j - fl)) + 1] = (uint8_t)(v >> 8);
-    }
-    if (live && A1 == nsym) *y.end = abs0 + p;  // past the payload: too few codewords (the caller checks)
+struct PieceArgs {
+    const unsigned long long* ent;
+    const unsigned long long* cnt;
+    const unsigned long long* first;
+    const uint16_t* rec;
+    uint32_t rcap, gs;
+    uint32_t slot_words;   // staging words per wave (multiple of 4)
+    uint32_t obuf_syms;    // output buffer symbols per wave (multiple of 8), + 64 dummy slots after it
+    uint64_t nseg, start, nsym;
+    unsigned long long* end;  // bit after codeword nsym - 1
+};
+
+HZ_DEV uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)readlane((uint32_t)(v >> 32), l) << 32) | readlane((uint32_t)v, l);
 }
 
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit) {
+__global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, PieceArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, d.lds_img, d.lds_words);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = wave_id();
+    const uint32_t wave_words = piece_wave_words(y.slot_words, y.obuf_syms);
+    uint32_t* stg = lds + d.lds_words + wid * wave_words;
+    uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
+    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
+    const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
+    const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
+    const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t dummy = y.obuf_syms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
+    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid; g < ngroups; g += gstride) {
+        const uint64_t k0 = g * y.gs;
+        const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
+        // the group's segments in lanes 0 .. ns - 1: pieces per segment and their exclusive prefix
+        uint64_t sc = 0, se = 0, sf = 0;
+        if ((uint32_t)lane < ns) {
+            sc = y.cnt[k0 + lane];
+            se = y.ent[k0 + lane];
+            sf = y.first[k0 + lane];
+        }
+        const uint32_t np = (uint32_t)((sc + kPieceSyms - 1) / kPieceSyms);
+        const uint32_t incl = wave_incl_sum(np);
+        const uint32_t T = readlane(incl, (int)ns - 1);
+        const uint64_t F0 = readlane64(sf, 0);
+        const uint64_t F1 = readlane64(sf, (int)ns - 1) + readlane64(sc, (int)ns - 1);
+        const uint64_t F0a = F0 & ~7ull;
+        uint32_t Qs[kPieceMaxGroup];
+        uint64_t Cs[kPieceMaxGroup], Es[kPieceMaxGroup], Fs[kPieceMaxGroup];
+#pragma unroll
+        for (uint32_t t = 0; t < kPieceMaxGroup; ++t) {
+            Qs[t] = t < ns ? readlane(incl - np, (int)t) : 0xffffffffu;
+            Cs[t] = readlane64(sc, (int)t);
+            Es[t] = readlane64(se, (int)t);
+            Fs[t] = readlane64(sf, (int)t);
+        }
+        // the group's payload bits, staged descending (k_decode's layout)
+        PipeMeta m;
+        m.b0 = y.start + k0 * kSegBits;
+        m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
+        m.sub = 0;
+        uint4 sv[kStageUnroll];
+        dec_stage_prefetch(d, m, lane, sv);
+        uint64_t w0;
+        __builtin_amdgcn_wave_barrier();  // the previous group's output copy has read the buffer
+        dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, sv, w0);
+        const uint32_t base = top * 32u - (uint32_t)(m.b0 + d.bit_adj - (w0 << 5));
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t r0 = 0; r0 < T; r0 += 64 * kPieceChains) {
+            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], rv[kPieceChains];
+            uint64_t pst[kPieceChains];
+            bool p0[kPieceChains];
+#pragma unroll
+            for (int c = 0; c < kPieceChains; ++c) {
+                const uint32_t q = r0 + 64u * (uint32_t)c + (uint32_t)lane;
+                uint32_t sg = 0;
+#pragma unroll
+                for (uint32_t t = 1; t < kPieceMaxGroup; ++t) sg = q >= Qs[t] ? t : sg;
+                uint64_t cs = Cs[0], es = Es[0], fs = Fs[0];
+                uint32_t qs = Qs[0];
+#pragma unroll
+                for (uint32_t t = 1; t < kPieceMaxGroup; ++t) {
+                    cs = sg == t ? Cs[t] : cs;
+                    es = sg == t ? Es[t] : es;
+                    fs = sg == t ? Fs[t] : fs;
+                    qs = sg == t ? Qs[t] : qs;
+                }
+                const bool valid = q < T;
+                const uint32_t i = valid ? q - qs : 0;
+                const uint64_t o = fs + (uint64_t)kPieceSyms * i;
+                uint64_t n = valid ? cs - (uint64_t)kPieceSyms * i : 0;
+                n = n < kPieceSyms ? n : kPieceSyms;
+                n = o < y.nsym ? (o + n <= y.nsym ? n : y.nsym - o) : 0;
+                cn[c] = (uint32_t)n;
+                ob[c] = (uint32_t)(o - F0a);
+                p0[c] = i == 0;
+                // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
+                // segment's first bit); all four record loads in flight together
+                rv[c] = y.rec[i ? (k0 + sg) * y.rcap + i - 1 : 0];
+                pst[c] = i ? y.start + (k0 + sg) * kSegBits : es;
+            }
+#pragma unroll
+            for (int c = 0; c < kPieceChains; ++c) {
+                const uint64_t sbit = pst[c] + (p0[c] ? 0u : rv[c]);
+                p1[c] = base - (uint32_t)(sbit - m.b0);
+            }
+            PipeLane st[kPieceChains];
+            uint32_t gv[kPieceChains];
+            auto issue2 = [&](int c) {
+                dec_pipe_ldsn<2>(d, lds, p1 + c, st + c);
+                gv[c] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c].gi, 0, 0);
+                gv[c + 1] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + 1].gi, 0, 0);
+            };
+            auto finish = [&](int c, uint32_t t) {
+                const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : gv[c];
+                p1[c] -= lut_leaf_len(ee);
+                const bool keep = t < cn[c];
+                obuf[keep ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
+                if (__builtin_expect(keep && t + 1 == cn[c], 0) && (uint64_t)ob[c] + F0a + t + 1 == y.nsym)
+                    *y.end = m.b0 + (uint64_t)(base - p1[c]);  // the stream's last codeword ends here
+            };
+            issue2(0);
+#pragma unroll
+            for (uint32_t t = 0; t < kPieceSyms; ++t) {
+                issue2(2);
+                finish(0, t);
+                finish(1, t);
+                if (t + 1 < kPieceSyms) issue2(0);
+                finish(2, t);
+                finish(3, t);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the group's symbols [F0, F1) (clamped to the stream): 16-byte stores of whole aligned
+        // groups of 8, single symbols at the two ends (the neighbouring groups own the rest)
+        const uint64_t Fe = F1 < y.nsym ? F1 : y.nsym;
+        if (F0 < Fe) {
+            uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
+            const uint64_t h1 = ((F0 + 7) & ~7ull) < Fe ? ((F0 + 7) & ~7ull) : Fe;
+            if ((uint64_t)lane < h1 - F0) out16[F0 + lane] = obuf[F0 + lane - F0a];
+            const uint64_t t0 = (Fe & ~7ull) > h1 ? (Fe & ~7ull) : h1;
+            for (uint64_t cg = h1 / 8 + (uint64_t)lane; cg < t0 / 8; cg += 64)
+                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - F0a / 8];
+            if ((uint64_t)lane < Fe - t0) out16[t0 + lane] = obuf[t0 + lane - F0a];
+        }
+    }
+}
+
+// The piece geometry of a payload: expected bits per codeword from its size.
+static PieceGeom seg_piece_geom(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len) {
+    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    return piece_geom(nsym ? (double)bits / (double)nsym : 16.0, max_len);
+}
+
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len) {
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
     const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
     const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    // ent, cnt, first, xit (<= nseg chains) (u64); dirty[2] (u32); changed, end; tiles
-    return 4 * nseg + nseg + 4 + ntiles + 24;
+    const PieceGeom pg = seg_piece_geom(payload_bytes, start_bit, nsym, max_len);
+    // records (u16, 16-byte rows); ent, cnt, first, xit (<= nseg chains) (u64); dirty[2] (u32); changed,
+    // end; tiles
+    return (nseg * pg.rcap + 3) / 4 + 2 + 4 * nseg + nseg + 4 + ntiles + 24;
 }
 
 bool seg_decode_supported(const Tables& t) {
-    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.dec_max_len <= 32 &&
+    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.seg_lds_bytes > 0 && t.dec_max_len <= 32 &&
            t.dec_max_len <= t.dec_k + t.dec_level_bits;
 }
 
@@ -3724,10 +3776,19 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     d.starts = nullptr; d.subs = nullptr; d.out = d_out; d.err = d_err;
     if (d.nwords < 4) return hipErrorInvalidValue;
     const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    const PieceGeom pg = seg_piece_geom(payload_bytes, start_bit, nsym, t.dec_max_len);
+    // the decoder's waves: as many as its LDS image leaves room for (the image was sized for the
+    // codebook's Kraft estimate, the geometry here for the payload's own bits per codeword)
+    int waves = (int)((kLdsBytes / 4 - t.seg_lds_bytes / 4) / pg.wave_words);
+    waves = waves > kPieceWaves ? kPieceWaves : waves;
+    if (waves < 1) return hipErrorNotSupported;
     SegArgs y;
     y.nseg = (bits + kSegBits - 1) / kSegBits;
     if (y.nseg == 0) return hipErrorInvalidValue;
+    y.rcap = pg.rcap;
+    y.err = d_err;
     unsigned long long* p = d_scratch;
+    y.rec = reinterpret_cast<uint16_t*>(p); p += (y.nseg * y.rcap + 3) / 4 + 2;
     y.ent = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     y.first = p; p += y.nseg;
@@ -3736,7 +3797,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     y.dirty[1] = y.dirty[0] + y.nseg;
     p += y.nseg;
     y.changed = reinterpret_cast<uint32_t*>(p); p += 2;
-    y.end = p; p += 2;
+    unsigned long long* endw = p; p += 2;
     unsigned long long* tiles = p;
     WalkArgs w;
     w.words = d.words; w.nwords = d.nwords; w.bit_adj = d.bit_adj;
@@ -3758,7 +3819,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
         const uint64_t wgs = (y.nchains + kSegWalkWaves * 64 - 1) / (kSegWalkWaves * 64);
         hipLaunchKernelGGL(k_seg_walk, dim3(wgs), dim3(kSegWalkWaves * 64), ring_bytes, s, w, y);
     }
-    // 2. fix-ups to a fixed point (host loop)
+    // 2. fix-ups to a fixed point (host loop); then the records' overflow flag
     {
         hipError_t e = ensure_lds_limit((const void*)k_seg_fix<DEC_LUT>, kLdsBytes);
         if (e != hipSuccess) return e;
@@ -3770,8 +3831,15 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
             hipLaunchKernelGGL(k_seg_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y, start_bit,
                                it);
             if ((e = hipMemcpyAsync(h_scratch, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(h_scratch + 1, d_err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-            if (*h_scratch == 0 || it > (int)y.nchains) break;
+            if (h_scratch[0] == 0 || it > (int)y.nchains || (h_scratch[1] & 64u)) break;
+        }
+        if (h_scratch[1] & 64u) {  // a segment with more pieces than planned: the caller takes the index path
+            h_scratch[1] &= ~64u;
+            if ((e = hipMemcpyAsync(d_err, h_scratch + 1, 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+            return hipErrorNotSupported;
         }
     }
     // 3. F = exclusive scan of the counts
@@ -3781,25 +3849,24 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
                        (const unsigned long long*)tiles, y.first);
-    // 4. decode: as many waves as the LDS holds beside the table, one chain per lane
+    // 4. the piece decoder: groups of gs segments, one wave each (persistent)
     {
-        const uint32_t table = t.dec_lds_bytes;
-        const uint32_t lane_bytes = kSegLaneWords * 4;
-        int waves = (int)((kLdsBytes - table) / (64 * lane_bytes));
-        waves = waves > kSegDecMaxWaves ? kSegDecMaxWaves : waves;
-        if (waves < 1) return hipErrorInvalidValue;
-        hipError_t e = ensure_lds_limit((const void*)k_seg_decode, kLdsBytes);
+        hipError_t e = ensure_lds_limit((const void*)k_piece_decode, kLdsBytes);
         if (e != hipSuccess) return e;
-        if ((e = hipMemsetAsync(y.end, 0xff, 8, s)) != hipSuccess) return e;
-        SegArgs z = y;
-        const uint64_t lanes = (uint64_t)waves * 64 * (uint64_t)ncu;
-        z.spc = (y.nseg + lanes - 1) / lanes;
-        z.nchains = (y.nseg + z.spc - 1) / z.spc;
-        const uint64_t wgs = (z.nchains + waves * 64 - 1) / (waves * 64);
-        hipLaunchKernelGGL(k_seg_decode, dim3(wgs), dim3(waves * 64), table + waves * 64 * lane_bytes, s, w, d, z,
-                           nsym);
+        if ((e = hipMemsetAsync(endw, 0xff, 8, s)) != hipSuccess) return e;
+        PieceArgs z;
+        z.ent = y.ent; z.cnt = y.cnt; z.first = y.first; z.rec = y.rec;
+        z.rcap = pg.rcap; z.gs = pg.gs; z.slot_words = pg.slot_words; z.obuf_syms = pg.obuf_syms;
+        z.nseg = y.nseg; z.start = start_bit; z.nsym = nsym; z.end = endw;
+        d.lds_img = t.d_seg_lds;
+        d.lds_words = t.seg_lds_bytes / 4;
+        const uint64_t ngroups = (y.nseg + pg.gs - 1) / pg.gs;
+        uint64_t wgs = (ngroups + waves - 1) / waves;
+        wgs = wgs < (uint64_t)ncu ? wgs : (uint64_t)ncu;
+        const uint32_t lds = 4 * (d.lds_words + (uint32_t)waves * pg.wave_words);
+        hipLaunchKernelGGL(k_piece_decode, dim3(wgs), dim3(waves * 64), lds, s, d, z);
         if (d_end) {
-            if ((e = hipMemcpyAsync(d_end, y.end, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(d_end, endw, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
         }
     }
     return hipGetLastError();

@@ -214,14 +214,17 @@ int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes
 
 /* Decode the first nsym codewords of an index-less stream (a .compressed file
  * from the reference encoder; Decompressor.cu:259-291 decodes it serially) into
- * d_out (2*nsym bytes, 16-byte aligned) with no block index: two passes of long
- * chains over the payload (code lengths, then symbols written where the counts
- * put them). *d_end_bit (device u64, optional) receives the end bit of codeword
- * nsym - 1, counted from byte 0 of d_payload; a payload with fewer than nsym
- * codewords gives an end bit past payload_bytes * 8 and undefined output (the
- * caller checks, as `extract` does). Codebooks the two-pass decoder does not
- * take (codes longer than 22 bits, DENSE / FIXED16 tables) go through
- * hz_index_build + hz_decode, with the same result. Synchronises the stream. */
+ * d_out (2*nsym bytes, 16-byte aligned) with no block index: a length walk of
+ * long chains over the payload (per 4096-bit segment: its first codeword start,
+ * its codeword count and the start of every 8th codeword), then a block-parallel
+ * decode of 8-codeword pieces placed by the scanned counts. *d_end_bit (device
+ * u64, optional) receives the end bit of codeword nsym - 1, counted from byte 0
+ * of d_payload; a payload with fewer than nsym codewords leaves it at UINT64_MAX
+ * (past payload_bytes * 8) with undefined output (the caller checks, as
+ * `extract` does). Codebooks the piece decoder does not take (codes longer than
+ * 22 bits, DENSE / FIXED16 tables), and payloads whose segments hold more
+ * codewords than it planned for, go through hz_index_build + hz_decode, with the
+ * same result. Synchronises the stream. */
 int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                         uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
 

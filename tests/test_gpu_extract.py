@@ -92,7 +92,7 @@ def test_indexless_truncated_end_past_payload(codec):
     end = torch.zeros(2, dtype=torch.int64, device="cuda")
     codec.dev.decode_indexless(payload.data_ptr(), cut, plan.start_bit, n // 2, out.data_ptr(), end.data_ptr())
     codec.sync()
-    assert int(end[0].item()) > 8 * cut
+    assert int(end[0].item()) & ((1 << 64) - 1) > 8 * cut  # UINT64_MAX: fewer than nsym codewords
 
 
 _NO_LEAD = r"""
