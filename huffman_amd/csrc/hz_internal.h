@@ -130,21 +130,22 @@ __host__ __device__ inline uint32_t lut_leaf_len(uint32_t e) { return (e >> 24) 
 __host__ __device__ inline uint32_t lut_leaf_sym(uint32_t e) { return (e >> 8) & 0xffffu; }
 constexpr int kDecMaxWaves = 16;
 // Index-less decoder (k_piece_decode, hz_kernels.hip): waves per workgroup and the per-wave LDS
-// of a group of segments (payload slot + output buffer). The walk records the start of every
-// 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
+// (a group of segments' payload slot + one round's output buffer). The walk records the start of
+// every 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
 #ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES 12
+#define HZ_PIECE_WAVES 16
 #endif
 constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
+constexpr uint32_t kPieceObufSyms = 256 * 8 + 8;  // a round's 256 pieces of 8, from an 8-aligned start
 struct PieceGeom {
     uint32_t gs;          // segments per group (<= 8)
-    uint32_t rcap;        // piece records per segment (multiple of 8)
+    uint32_t rcap;        // piece records per segment (multiple of 16)
     uint32_t slot_words;  // payload staging words (multiple of 4)
-    uint32_t obuf_syms;   // output buffer symbols (multiple of 8; 64 per-lane dummy slots follow)
     uint32_t wave_words;
 };
-__host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words, uint32_t obuf_syms) {
-    return slot_words + (obuf_syms + 64) / 2;
+// slot + output buffer (+ 64 per-lane dummy slots) + the group's segment table (8 x 3 u64)
+__host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
+    return slot_words + (kPieceObufSyms + 64) / 2 + 48;
 }
 // avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
 // over the expected count of a segment (a segment past it sets error flag 64: the caller
@@ -153,13 +154,12 @@ inline PieceGeom piece_geom(double avg_bits, int max_len) {
     PieceGeom g;
     const double per_seg = 4096.0 / (avg_bits > 1.0 ? avg_bits : 1.0);  // codewords per segment
     const double recs = per_seg / 8.0;
-    uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 7.0) / 8.0) * 8u;
-    g.rcap = rcap < 8u ? 8u : (rcap > 520u ? 520u : rcap);
+    uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16u;
+    g.rcap = rcap < 16u ? 16u : (rcap > 528u ? 528u : rcap);
     uint32_t gs = (uint32_t)(230.0 / (recs + 1.0));  // ~230 of a round's 256 pieces
     g.gs = gs < 1u ? 1u : (gs > 8u ? 8u : gs);
     g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;
-    g.obuf_syms = ((g.gs * 8u * (g.rcap + 1u) + 8u) + 7u) & ~7u;
-    g.wave_words = piece_wave_words(g.slot_words, g.obuf_syms);
+    g.wave_words = piece_wave_words(g.slot_words);
     return g;
 }
 

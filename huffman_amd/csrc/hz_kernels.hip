@@ -3451,39 +3451,47 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
     uint32_t cc = 0;                               // codewords since the last crossing
     // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 7
-    // codewords), held in rfl / roff until the half-round's end, then packed into rb (8 u16)
-    // and stored 16 bytes at a time.
-    uint32_t rb[4] = {0u, 0u, 0u, 0u}, rj = 0, roff = 0;
+    // codewords), held in rfl / roff until the half-round's end, then written to the lane's
+    // 16-byte LDS record buffer (after the rings) and stored 8 records at a time.
+#ifndef HZ_EXP_REC
+#define HZ_EXP_REC 1  // timing builds only: 0 = no records (the decode is then wrong)
+#endif
+    constexpr uint32_t RG = 8;
+    uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + kSegWalkWaves * 64 * kSegRing) + 8 * threadIdx.x;
+    uint32_t rj = 0, roff = 0;
     bool rfl = false;
+    // roff: the ring position of the pending record (converted to a segment offset when put)
     auto rec_put = [&]() {
-        const uint32_t sl = rj & 7u, sh = (sl & 1u) << 4, v = (roff & 0xffffu) << sh, keep = ~(0xffffu << sh);
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) rb[i] = (sl >> 1) == i ? ((rb[i] & keep) | v) : rb[i];
+        rbuf[rj & (RG - 1)] = (uint16_t)(roff + kSegBits - nb);
         ++rj;
         rfl = false;
     };
-    auto rec_store = [&]() {  // the group of 8 holding record rj - 1
+    auto rec_store = [&]() {  // the group holding record rj - 1 (nothing in the lead-in before seg0)
+        if (sj == seg0) return;
         if (rj <= y.rcap)
-            *reinterpret_cast<uint4*>(y.rec + (sj - 1) * y.rcap + ((rj - 1) & ~7u)) = make_uint4(rb[0], rb[1], rb[2], rb[3]);
+            *reinterpret_cast<uint4*>(y.rec + (sj - 1) * y.rcap + ((rj - 1) & ~(RG - 1))) =
+                *reinterpret_cast<const uint4*>(rbuf);
         else
             atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
     };
     // after a codeword: its end p is the start of the segment's codeword cc; every 8th is a record
+    // (one the crossing below turns into the next segment's entry is dropped there)
     auto note = [&](bool adv) {
-        const bool rn = adv & ((cc & 7u) == 0u) & (p < nb) & (sj > seg0);
-        roff = rn ? p + kSegBits - nb : roff;
+        const bool rn = HZ_EXP_REC & adv & ((cc & 7u) == 0u);
+        roff = rn ? p : roff;
         rfl |= rn;
     };
     // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
     auto cross = [&]() {
         if (__builtin_expect(p >= nb, 0) && sj <= seg1 && live) {
+            if (rfl && roff < nb) {  // a record inside the segment (not its successor's entry)
+                rec_put();
+                if ((rj & (RG - 1)) == 0u) rec_store();
+            }
+            rfl = false;
             if (sj > seg0) {
                 y.cnt[sj - 1] = cc;
-                if (rfl) {
-                    rec_put();
-                    if ((rj & 7u) == 0u) rec_store();
-                }
-                if (rj & 7u) rec_store();  // the segment's last, partial group
+                if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
             }
             if (sj < seg1) y.ent[sj] = abs0 + p;
             else y.xit[ch] = abs0 + p;
@@ -3528,7 +3536,7 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             }
             if (rfl) {
                 rec_put();
-                if ((rj & 7u) == 0u) rec_store();
+                if ((rj & (RG - 1)) == 0u) rec_store();
             }
         }
         seg_feed(a, ring, fd, p);
@@ -3585,15 +3593,19 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
 // Block-parallel decode of groups of y.gs segments (k_decode's chain machinery): the
 // group's payload bits [start + 4096 k0, + 4096 gs + 8 max_len) staged (descending) in the
 // wave's slot; rounds of 256 pieces, lane l taking pieces 64 c + l (c < 4) as two pairs
-// whose global gathers land behind the other pair's LDS walk; every symbol goes to the
-// wave's LDS output buffer at its place (slot 0 = output symbol F0 rounded down to 8), and
-// the group's run [F0, F1) leaves as 16-byte stores (2-byte stores at its two ends).
+// whose global gathers land behind the other pair's LDS walk; a round's symbols (one
+// contiguous output run: its pieces are consecutive) go to the wave's LDS output buffer at
+// their place (slot 0 = the run's first symbol rounded down to 8) and leave as 16-byte
+// stores (2-byte stores at the run's two ends). A group's segment records and staging
+// loads are issued together (one memory round trip), its piece records in a second.
 constexpr uint32_t kPieceSyms = 8;  // codewords per piece: one decode chain
 constexpr int kPieceChains = 4;     // pieces per lane per round
 static_assert(kPieceChains == 4, "two pairs");
 constexpr uint32_t kPieceMaxGroup = 8;
+constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
+static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h output buffer");
 #ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES 12
+#define HZ_PIECE_WAVES 16
 #endif
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
 static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
@@ -3605,7 +3617,6 @@ struct PieceArgs {
     const uint16_t* rec;
     uint32_t rcap, gs;
     uint32_t slot_words;   // staging words per wave (multiple of 4)
-    uint32_t obuf_syms;    // output buffer symbols per wave (multiple of 8), + 64 dummy slots after it
     uint64_t nseg, start, nsym;
     unsigned long long* end;  // bit after codeword nsym - 1
 };
@@ -3614,87 +3625,102 @@ HZ_DEV uint64_t readlane64(uint64_t v, int l) {
     return ((uint64_t)readlane((uint32_t)(v >> 32), l) << 32) | readlane((uint32_t)v, l);
 }
 
+// A group's segment records (lanes < ns) and staging chunks, issued together.
+struct PieceIn {
+    uint64_t c, e, f;
+    uint4 sv[kStageUnroll];
+};
+HZ_DEV void piece_prefetch(const DecArgs& d, const PieceArgs& y, uint64_t g, int lane, PieceIn& x) {
+    const uint64_t gg = g * y.gs < y.nseg ? g : 0;  // past the end: any group, never used
+    const uint64_t k0 = gg * y.gs;
+    const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
+    const uint64_t kk = k0 + ((uint32_t)lane < ns ? (uint32_t)lane : 0u);
+    x.c = y.cnt[kk];
+    x.e = y.ent[kk];
+    x.f = y.first[kk];
+    PipeMeta m;
+    m.b0 = y.start + k0 * kSegBits;
+    m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
+    m.sub = 0;
+    dec_stage_prefetch(d, m, lane, x.sv);
+}
+
 __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, PieceArgs y) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, d.lds_img, d.lds_words);
     const int lane = threadIdx.x & 63;
     const uint32_t wid = wave_id();
-    const uint32_t wave_words = piece_wave_words(y.slot_words, y.obuf_syms);
+    const uint32_t wave_words = piece_wave_words(y.slot_words);
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
+    unsigned long long* sinfo = reinterpret_cast<unsigned long long*>(obuf + kPieceObufSyms + 64);  // 8 x 3 u64
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
     const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t dummy = y.obuf_syms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
-    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid; g < ngroups; g += gstride) {
+    const uint32_t dummy = kPieceObufSyms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
+    uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+    PieceIn cur, nxt;
+    if (g < ngroups) piece_prefetch(d, y, g, lane, cur);
+    for (; g < ngroups; g += gstride) {
         const uint64_t k0 = g * y.gs;
         const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
         // the group's segments in lanes 0 .. ns - 1: pieces per segment and their exclusive prefix
-        uint64_t sc = 0, se = 0, sf = 0;
-        if ((uint32_t)lane < ns) {
-            sc = y.cnt[k0 + lane];
-            se = y.ent[k0 + lane];
-            sf = y.first[k0 + lane];
-        }
+        const bool sl = (uint32_t)lane < ns;
+        const uint64_t sc = sl ? cur.c : 0, se = cur.e, sf = cur.f;
         const uint32_t np = (uint32_t)((sc + kPieceSyms - 1) / kPieceSyms);
         const uint32_t incl = wave_incl_sum(np);
         const uint32_t T = readlane(incl, (int)ns - 1);
-        const uint64_t F0 = readlane64(sf, 0);
-        const uint64_t F1 = readlane64(sf, (int)ns - 1) + readlane64(sc, (int)ns - 1);
-        const uint64_t F0a = F0 & ~7ull;
+        // piece prefix per segment in SGPRs; counts, entries and F in the wave's LDS table
         uint32_t Qs[kPieceMaxGroup];
-        uint64_t Cs[kPieceMaxGroup], Es[kPieceMaxGroup], Fs[kPieceMaxGroup];
 #pragma unroll
-        for (uint32_t t = 0; t < kPieceMaxGroup; ++t) {
-            Qs[t] = t < ns ? readlane(incl - np, (int)t) : 0xffffffffu;
-            Cs[t] = readlane64(sc, (int)t);
-            Es[t] = readlane64(se, (int)t);
-            Fs[t] = readlane64(sf, (int)t);
+        for (uint32_t t = 0; t < kPieceMaxGroup; ++t) Qs[t] = t < ns ? readlane(incl - np, (int)t) : 0xffffffffu;
+        if (sl) {
+            sinfo[3 * lane] = sc;
+            sinfo[3 * lane + 1] = se;
+            sinfo[3 * lane + 2] = sf;
         }
         // the group's payload bits, staged descending (k_decode's layout)
         PipeMeta m;
         m.b0 = y.start + k0 * kSegBits;
         m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
         m.sub = 0;
-        uint4 sv[kStageUnroll];
-        dec_stage_prefetch(d, m, lane, sv);
         uint64_t w0;
-        __builtin_amdgcn_wave_barrier();  // the previous group's output copy has read the buffer
-        dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, sv, w0);
+        __builtin_amdgcn_wave_barrier();  // the previous round's output copy has read the buffer
+        dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, cur.sv, w0);
         const uint32_t base = top * 32u - (uint32_t)(m.b0 + d.bit_adj - (w0 << 5));
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t r0 = 0; r0 < T; r0 += 64 * kPieceChains) {
+        for (uint32_t r0 = 0; r0 < T; r0 += kPieceRound) {
             uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], rv[kPieceChains];
             uint64_t pst[kPieceChains];
             bool p0[kPieceChains];
+            // the round's output run: pieces r0 .. min(T, r0 + 256) - 1
+            uint64_t R0 = 0;
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
                 const uint32_t q = r0 + 64u * (uint32_t)c + (uint32_t)lane;
-                uint32_t sg = 0;
-#pragma unroll
-                for (uint32_t t = 1; t < kPieceMaxGroup; ++t) sg = q >= Qs[t] ? t : sg;
-                uint64_t cs = Cs[0], es = Es[0], fs = Fs[0];
-                uint32_t qs = Qs[0];
+                uint32_t sg = 0, qs = 0;
 #pragma unroll
                 for (uint32_t t = 1; t < kPieceMaxGroup; ++t) {
-                    cs = sg == t ? Cs[t] : cs;
-                    es = sg == t ? Es[t] : es;
-                    fs = sg == t ? Fs[t] : fs;
-                    qs = sg == t ? Qs[t] : qs;
+                    const bool in = q >= Qs[t];
+                    sg = in ? t : sg;
+                    qs = in ? Qs[t] : qs;
                 }
+                const uint64_t cs = sinfo[3 * sg], es = sinfo[3 * sg + 1], fs = sinfo[3 * sg + 2];
                 const bool valid = q < T;
                 const uint32_t i = valid ? q - qs : 0;
                 const uint64_t o = fs + (uint64_t)kPieceSyms * i;
+                if (c == 0) R0 = readlane64(o, 0) & ~7ull;  // piece r0 (lane 0, chain 0) opens the run
                 uint64_t n = valid ? cs - (uint64_t)kPieceSyms * i : 0;
                 n = n < kPieceSyms ? n : kPieceSyms;
                 n = o < y.nsym ? (o + n <= y.nsym ? n : y.nsym - o) : 0;
                 cn[c] = (uint32_t)n;
-                ob[c] = (uint32_t)(o - F0a);
+                ob[c] = (uint32_t)(o - R0);
                 p0[c] = i == 0;
                 // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
                 // segment's first bit); all four record loads in flight together
-                rv[c] = y.rec[i ? (k0 + sg) * y.rcap + i - 1 : 0];
+                rv[c] = y.rec[(k0 + sg) * y.rcap + (i ? i - 1 : 0)];
                 pst[c] = i ? y.start + (k0 + sg) * kSegBits : es;
             }
 #pragma unroll
@@ -3714,7 +3740,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 p1[c] -= lut_leaf_len(ee);
                 const bool keep = t < cn[c];
                 obuf[keep ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
-                if (__builtin_expect(keep && t + 1 == cn[c], 0) && (uint64_t)ob[c] + F0a + t + 1 == y.nsym)
+                if (__builtin_expect(keep && t + 1 == cn[c], 0) && (uint64_t)ob[c] + R0 + t + 1 == y.nsym)
                     *y.end = m.b0 + (uint64_t)(base - p1[c]);  // the stream's last codeword ends here
             };
             issue2(0);
@@ -3727,20 +3753,25 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 finish(2, t);
                 finish(3, t);
             }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // the group's symbols [F0, F1) (clamped to the stream): 16-byte stores of whole aligned
-        // groups of 8, single symbols at the two ends (the neighbouring groups own the rest)
-        const uint64_t Fe = F1 < y.nsym ? F1 : y.nsym;
-        if (F0 < Fe) {
-            uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
-            const uint64_t h1 = ((F0 + 7) & ~7ull) < Fe ? ((F0 + 7) & ~7ull) : Fe;
-            if ((uint64_t)lane < h1 - F0) out16[F0 + lane] = obuf[F0 + lane - F0a];
-            const uint64_t t0 = (Fe & ~7ull) > h1 ? (Fe & ~7ull) : h1;
+            __builtin_amdgcn_wave_barrier();
+            // the round's run [Ra, Rb) (clamped to the stream): 16-byte stores of whole aligned groups
+            // of 8, single symbols at the two ends (the neighbouring runs own the rest)
+            const uint32_t rl = (T - r0 < kPieceRound ? T - r0 : kPieceRound) - 1;  // the round's last piece
+            const uint64_t Ra = readlane64((uint64_t)ob[0] + R0, 0);
+            const uint64_t Rl = readlane64((uint64_t)ob[rl >> 6] + R0 + cn[rl >> 6], (int)(rl & 63));
+            uint64_t Rb = Rl < y.nsym ? Rl : y.nsym;
+            Rb = Rb > Ra ? Rb : Ra;
+            const uint64_t h1 = ((Ra + 7) & ~7ull) < Rb ? ((Ra + 7) & ~7ull) : Rb;
+            if ((uint64_t)lane < h1 - Ra) out16[Ra + lane] = obuf[Ra + lane - R0];
+            const uint64_t t0 = (Rb & ~7ull) > h1 ? (Rb & ~7ull) : h1;
             for (uint64_t cg = h1 / 8 + (uint64_t)lane; cg < t0 / 8; cg += 64)
-                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - F0a / 8];
-            if ((uint64_t)lane < Fe - t0) out16[t0 + lane] = obuf[t0 + lane - F0a];
+                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - R0 / 8];
+            if ((uint64_t)lane < Rb - t0) out16[t0 + lane] = obuf[t0 + lane - R0];
         }
+        // the next group's records and staging chunks (after the last round: their 22 VGPRs beside the
+        // chains' spill at 1024 threads)
+        piece_prefetch(d, y, g + gstride, lane, nxt);
+        cur = nxt;
     }
 }
 
@@ -3810,7 +3841,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     w.lead = lead;
     // 1. walk: chains of spc segments, one per lane
     {
-        const uint32_t ring_bytes = kSegWalkWaves * 64 * kSegRing * 4;
+        const uint32_t ring_bytes = kSegWalkWaves * 64 * (kSegRing * 4 + 16);  // rings, record buffers
         hipError_t e = ensure_lds_limit((const void*)k_seg_walk, (int)ring_bytes);
         if (e != hipSuccess) return e;
         const uint64_t target = (uint64_t)kSegWalkWaves * 64 * (uint64_t)ncu;
@@ -3856,7 +3887,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
         if ((e = hipMemsetAsync(endw, 0xff, 8, s)) != hipSuccess) return e;
         PieceArgs z;
         z.ent = y.ent; z.cnt = y.cnt; z.first = y.first; z.rec = y.rec;
-        z.rcap = pg.rcap; z.gs = pg.gs; z.slot_words = pg.slot_words; z.obuf_syms = pg.obuf_syms;
+        z.rcap = pg.rcap; z.gs = pg.gs; z.slot_words = pg.slot_words;
         z.nseg = y.nseg; z.start = start_bit; z.nsym = nsym; z.end = endw;
         d.lds_img = t.d_seg_lds;
         d.lds_words = t.seg_lds_bytes / 4;
