@@ -143,9 +143,9 @@ struct PieceGeom {
     uint32_t slot_words;  // payload staging words (multiple of 4)
     uint32_t wave_words;
 };
-// slot + output buffer (+ 64 per-lane dummy slots) + the group's segment table (8 x 3 u64)
+// slot + output buffer (+ 64 per-lane dummy slots) + the group's segment table (8 x 3 u32)
 __host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
-    return slot_words + (kPieceObufSyms + 64) / 2 + 48;
+    return slot_words + (kPieceObufSyms + 64) / 2 + 24;
 }
 // avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
 // over the expected count of a segment (a segment past it sets error flag 64: the caller

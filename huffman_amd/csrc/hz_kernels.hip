@@ -3368,6 +3368,34 @@ HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
     return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
 }
 
+// HZ_SEG_REGWIN (k_seg_walk): the window kept in registers -- two ring words at a funnel shift,
+// the next word read one step ahead -- so a step's critical path holds one LDS read (the length
+// table) instead of two. Valid for codes of <= 32 bits (the walker's <= 22).
+#ifndef HZ_SEG_REGWIN
+#define HZ_SEG_REGWIN 0
+#endif
+struct SegWin {
+    uint32_t w0, w1, sh, wn, nxt;
+    HZ_DEV void init(const uint32_t* ring, uint32_t p) {
+        const uint32_t q0 = (p - 1) >> 5;
+        w0 = ring[q0 & 15u];
+        w1 = ring[(q0 + 1) & 15u];
+        sh = (0u - p) & 31u;
+        wn = q0 + 2;
+    }
+    HZ_DEV uint32_t window() const { return __builtin_amdgcn_alignbit(w0, w1, sh); }
+    HZ_DEV void reload(const uint32_t* ring) { nxt = ring[wn & 15u]; }  // after the ring's refill
+    HZ_DEV void step(const uint32_t* ring, uint32_t L) {  // L <= 32
+        const int32_t r = (int32_t)sh - (int32_t)L;
+        const bool cr = r < 0;
+        w0 = cr ? w1 : w0;
+        w1 = cr ? nxt : w1;
+        sh = (uint32_t)(cr ? r + 32 : r);
+        wn += cr ? 1u : 0u;
+        nxt = ring[wn & 15u];
+    }
+};
+
 // Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
@@ -3504,15 +3532,26 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     cross();  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
+#if HZ_SEG_REGWIN
+    SegWin wv;
+    wv.init(ring, p);
+#endif
     for (;;) {
         if (!__any(p < end)) break;
         const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
+#if HZ_SEG_REGWIN
+        wv.reload(ring);
+#endif
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (p < lim);
+#if HZ_SEG_REGWIN
+                const uint32_t W = wv.window();
+#else
                 const uint32_t W = seg_window(ring, p);
+#endif
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
                 HZ_WALK_FENCE();
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
@@ -3520,6 +3559,9 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
                 const uint32_t L = adv ? e + bias : 0u;
                 cc += adv ? 1u : 0u;
                 p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 pk |= park;
                 pW = park ? W : pW;
                 note(adv);
@@ -3529,6 +3571,9 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             if (pk) {
                 const uint32_t L = a.esc[pW >> (32 - a.m)];
                 p += L;
+#if HZ_SEG_REGWIN
+                wv.step(ring, L);
+#endif
                 ++cc;
                 pk = false;
                 note(true);
@@ -3653,50 +3698,52 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     const uint32_t wave_words = piece_wave_words(y.slot_words);
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
-    unsigned long long* sinfo = reinterpret_cast<unsigned long long*>(obuf + kPieceObufSyms + 64);  // 8 x 3 u64
+    uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + kPieceObufSyms + 64);  // per segment: cnt, entry, F (u32)
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
     const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t dummy = kPieceObufSyms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
     uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
+    const uint32_t dummy = kPieceObufSyms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
     uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
     PieceIn cur, nxt;
     if (g < ngroups) piece_prefetch(d, y, g, lane, cur);
     for (; g < ngroups; g += gstride) {
         const uint64_t k0 = g * y.gs;
         const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
-        // the group's segments in lanes 0 .. ns - 1: pieces per segment and their exclusive prefix
+        const uint64_t b0 = y.start + k0 * kSegBits;  // the group's first bit
+        // the group's segments in lanes 0 .. ns - 1: pieces per segment and their exclusive prefix;
+        // counts, entries (from b0) and F (from F0) as u32 in the wave's LDS table
         const bool sl = (uint32_t)lane < ns;
-        const uint64_t sc = sl ? cur.c : 0, se = cur.e, sf = cur.f;
+        const uint64_t sc = sl ? cur.c : 0;
         const uint32_t np = (uint32_t)((sc + kPieceSyms - 1) / kPieceSyms);
         const uint32_t incl = wave_incl_sum(np);
         const uint32_t T = readlane(incl, (int)ns - 1);
-        // piece prefix per segment in SGPRs; counts, entries and F in the wave's LDS table
+        const uint64_t F0 = readlane64(cur.f, 0);
+        // output symbols [F0, F0 + lim) exist (u32: a group holds < 2^32 symbols)
+        const uint32_t lim = y.nsym > F0 ? (y.nsym - F0 < 0xffffffffull ? (uint32_t)(y.nsym - F0) : 0xffffffffu) : 0u;
         uint32_t Qs[kPieceMaxGroup];
 #pragma unroll
         for (uint32_t t = 0; t < kPieceMaxGroup; ++t) Qs[t] = t < ns ? readlane(incl - np, (int)t) : 0xffffffffu;
         if (sl) {
-            sinfo[3 * lane] = sc;
-            sinfo[3 * lane + 1] = se;
-            sinfo[3 * lane + 2] = sf;
+            sinfo[3 * lane] = (uint32_t)sc;
+            sinfo[3 * lane + 1] = (uint32_t)(cur.e - b0);
+            sinfo[3 * lane + 2] = (uint32_t)(cur.f - F0);
         }
         // the group's payload bits, staged descending (k_decode's layout)
         PipeMeta m;
-        m.b0 = y.start + k0 * kSegBits;
-        m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
+        m.b0 = b0;
+        m.b1 = b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
         m.sub = 0;
         uint64_t w0;
         __builtin_amdgcn_wave_barrier();  // the previous round's output copy has read the buffer
         dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, cur.sv, w0);
-        const uint32_t base = top * 32u - (uint32_t)(m.b0 + d.bit_adj - (w0 << 5));
+        const uint32_t base = top * 32u - (uint32_t)(b0 + d.bit_adj - (w0 << 5));
+        const uint16_t* recg = y.rec + k0 * y.rcap;  // the group's record rows
         __builtin_amdgcn_wave_barrier();
         for (uint32_t r0 = 0; r0 < T; r0 += kPieceRound) {
-            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], rv[kPieceChains];
-            uint64_t pst[kPieceChains];
-            bool p0[kPieceChains];
-            // the round's output run: pieces r0 .. min(T, r0 + 256) - 1
-            uint64_t R0 = 0;
+            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], st0[kPieceChains];
+            int32_t R0 = 0;  // the round's output run starts at F0 + R0, rounded down to 8 (from F0)
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
                 const uint32_t q = r0 + 64u * (uint32_t)c + (uint32_t)lane;
@@ -3707,27 +3754,23 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                     sg = in ? t : sg;
                     qs = in ? Qs[t] : qs;
                 }
-                const uint64_t cs = sinfo[3 * sg], es = sinfo[3 * sg + 1], fs = sinfo[3 * sg + 2];
+                const uint32_t cs = sinfo[3 * sg], es = sinfo[3 * sg + 1], fs = sinfo[3 * sg + 2];
                 const bool valid = q < T;
                 const uint32_t i = valid ? q - qs : 0;
-                const uint64_t o = fs + (uint64_t)kPieceSyms * i;
-                if (c == 0) R0 = readlane64(o, 0) & ~7ull;  // piece r0 (lane 0, chain 0) opens the run
-                uint64_t n = valid ? cs - (uint64_t)kPieceSyms * i : 0;
+                const uint32_t o = fs + kPieceSyms * i;  // from F0
+                if (c == 0) R0 = (int32_t)((readlane(o, 0) + (uint32_t)(F0 & 7)) & ~7u) - (int32_t)(F0 & 7);
+                uint32_t n = valid ? cs - kPieceSyms * i : 0;
                 n = n < kPieceSyms ? n : kPieceSyms;
-                n = o < y.nsym ? (o + n <= y.nsym ? n : y.nsym - o) : 0;
-                cn[c] = (uint32_t)n;
-                ob[c] = (uint32_t)(o - R0);
-                p0[c] = i == 0;
+                n = o < lim ? (lim - o < n ? lim - o : n) : 0;
+                cn[c] = n;
+                ob[c] = (uint32_t)((int32_t)o - R0);
                 // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
                 // segment's first bit); all four record loads in flight together
-                rv[c] = y.rec[(k0 + sg) * y.rcap + (i ? i - 1 : 0)];
-                pst[c] = i ? y.start + (k0 + sg) * kSegBits : es;
+                const uint32_t rv = recg[sg * y.rcap + (i ? i - 1 : 0)];
+                st0[c] = i ? sg * kSegBits + rv : es;  // from b0
             }
 #pragma unroll
-            for (int c = 0; c < kPieceChains; ++c) {
-                const uint64_t sbit = pst[c] + (p0[c] ? 0u : rv[c]);
-                p1[c] = base - (uint32_t)(sbit - m.b0);
-            }
+            for (int c = 0; c < kPieceChains; ++c) p1[c] = base - st0[c];
             PipeLane st[kPieceChains];
             uint32_t gv[kPieceChains];
             auto issue2 = [&](int c) {
@@ -3735,13 +3778,12 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 gv[c] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c].gi, 0, 0);
                 gv[c + 1] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + 1].gi, 0, 0);
             };
+            // a symbol goes to the round's output buffer at its place (a piece's steps past its count to
+            // the lane's dummy slot)
             auto finish = [&](int c, uint32_t t) {
                 const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : gv[c];
                 p1[c] -= lut_leaf_len(ee);
-                const bool keep = t < cn[c];
-                obuf[keep ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
-                if (__builtin_expect(keep && t + 1 == cn[c], 0) && (uint64_t)ob[c] + R0 + t + 1 == y.nsym)
-                    *y.end = m.b0 + (uint64_t)(base - p1[c]);  // the stream's last codeword ends here
+                obuf[t < cn[c] ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
             };
             issue2(0);
 #pragma unroll
@@ -3753,20 +3795,41 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 finish(2, t);
                 finish(3, t);
             }
+            // the stream's last codeword: its chain is decoded again, alone, for its end bit
+#pragma unroll
+            for (int c = 0; c < kPieceChains; ++c) {
+                const bool is_end = cn[c] > 0 && (uint64_t)(int64_t)((int32_t)ob[c] + R0) + F0 + cn[c] == y.nsym;
+                if (__builtin_expect(is_end, 0)) {
+                    uint32_t pp = base - st0[c];
+                    for (uint32_t t = 0; t < cn[c]; ++t) {
+                        PipeLane one;
+                        dec_pipe_ldsn<1>(d, lds, &pp, &one);
+                        const uint32_t ee = lut_leaf(one.e) ? one.e : __builtin_amdgcn_raw_buffer_load_b32(l2r, one.gi, 0, 0);
+                        pp -= lut_leaf_len(ee);
+                    }
+                    *y.end = b0 + (uint64_t)(base - pp);
+                }
+            }
             __builtin_amdgcn_wave_barrier();
             // the round's run [Ra, Rb) (clamped to the stream): 16-byte stores of whole aligned groups
             // of 8, single symbols at the two ends (the neighbouring runs own the rest)
             const uint32_t rl = (T - r0 < kPieceRound ? T - r0 : kPieceRound) - 1;  // the round's last piece
-            const uint64_t Ra = readlane64((uint64_t)ob[0] + R0, 0);
-            const uint64_t Rl = readlane64((uint64_t)ob[rl >> 6] + R0 + cn[rl >> 6], (int)(rl & 63));
-            uint64_t Rb = Rl < y.nsym ? Rl : y.nsym;
+            const uint64_t Rz = F0 + (uint64_t)(int64_t)R0;                           // obuf slot 0
+            const uint64_t Ra = Rz + readlane(ob[0], 0);
+            uint32_t obl = ob[0], cnl = cn[0];
+#pragma unroll
+            for (int c = 1; c < kPieceChains; ++c) {
+                obl = (rl >> 6) == (uint32_t)c ? ob[c] : obl;
+                cnl = (rl >> 6) == (uint32_t)c ? cn[c] : cnl;
+            }
+            uint64_t Rb = Rz + readlane(obl, (int)(rl & 63)) + readlane(cnl, (int)(rl & 63));
             Rb = Rb > Ra ? Rb : Ra;
             const uint64_t h1 = ((Ra + 7) & ~7ull) < Rb ? ((Ra + 7) & ~7ull) : Rb;
-            if ((uint64_t)lane < h1 - Ra) out16[Ra + lane] = obuf[Ra + lane - R0];
+            if ((uint64_t)lane < h1 - Ra) out16[Ra + lane] = obuf[Ra + lane - Rz];
             const uint64_t t0 = (Rb & ~7ull) > h1 ? (Rb & ~7ull) : h1;
             for (uint64_t cg = h1 / 8 + (uint64_t)lane; cg < t0 / 8; cg += 64)
-                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - R0 / 8];
-            if ((uint64_t)lane < Rb - t0) out16[t0 + lane] = obuf[t0 + lane - R0];
+                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - Rz / 8];
+            if ((uint64_t)lane < Rb - t0) out16[t0 + lane] = obuf[t0 + lane - Rz];
         }
         // the next group's records and staging chunks (after the last round: their 22 VGPRs beside the
         // chains' spill at 1024 threads)
