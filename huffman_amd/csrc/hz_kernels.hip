@@ -52,6 +52,7 @@ typedef unsigned short hz_u16x2 __attribute__((ext_vector_type(2)));
 // 16 bytes at a 4-byte aligned address (global_load/store_dwordx4 need only dword alignment): the
 // FIXED16 block kernels move a stream that starts at any word behind the header.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4a2 __attribute__((ext_vector_type(4), aligned(2)));  // 16 bytes at a 2-byte aligned address
 
 // One 16-byte non-temporal store (global_store_dwordx4 ... nt).
 HZ_DEV void store_nt16(uint4* p, uint4 v) {
@@ -3654,6 +3655,9 @@ static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h out
 #endif
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
 static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
+#ifndef HZ_PIECE_DIRECT
+#define HZ_PIECE_DIRECT 0  // 1: output stored from registers (16 GiB Zipf 17.1 vs 16.5 ms through the LDS buffer)
+#endif
 
 struct PieceArgs {
     const unsigned long long* ent;
@@ -3778,6 +3782,17 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 gv[c] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c].gi, 0, 0);
                 gv[c + 1] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + 1].gi, 0, 0);
             };
+#if HZ_PIECE_DIRECT
+            // symbols packed in registers (an even step keeps the entry, the odd one packs both symbols,
+            // leaf bytes 1-2, by one v_perm); a whole piece leaves as one 16-byte store at its place
+            uint32_t pk[kPieceChains][kPieceSyms / 2];
+            auto finish = [&](int c, uint32_t t) {
+                const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : gv[c];
+                p1[c] -= lut_leaf_len(ee);
+                if (t & 1) pk[c][t >> 1] = __builtin_amdgcn_perm(ee, pk[c][t >> 1], 0x06050201u);
+                else pk[c][t >> 1] = ee;
+            };
+#else
             // a symbol goes to the round's output buffer at its place (a piece's steps past its count to
             // the lane's dummy slot)
             auto finish = [&](int c, uint32_t t) {
@@ -3785,6 +3800,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 p1[c] -= lut_leaf_len(ee);
                 obuf[t < cn[c] ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
             };
+#endif
             issue2(0);
 #pragma unroll
             for (uint32_t t = 0; t < kPieceSyms; ++t) {
@@ -3795,6 +3811,26 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 finish(2, t);
                 finish(3, t);
             }
+#if HZ_PIECE_DIRECT
+            // whole pieces: 16 bytes at output symbol F0 + o (2-byte aligned: the hardware takes unaligned
+            // global stores; a lane's neighbours write the adjacent 16 bytes, so a store instruction covers
+            // about 1 KiB); short pieces (a segment's last, the stream's end) symbol by symbol, so they
+            // never touch the next piece's symbols
+#pragma unroll
+            for (int c = 0; c < kPieceChains; ++c) {
+                const uint64_t o = F0 + (uint64_t)(int64_t)((int32_t)ob[c] + R0);
+                if (cn[c] == kPieceSyms) {
+                    *reinterpret_cast<u32x4a2*>(out16 + o) = u32x4a2{pk[c][0], pk[c][1], pk[c][2], pk[c][3]};
+                } else {
+                    for (uint32_t t = 0; t < cn[c]; ++t) {
+                        uint32_t w = pk[c][0];
+#pragma unroll
+                        for (uint32_t u = 1; u < kPieceSyms / 2; ++u) w = (t >> 1) == u ? pk[c][u] : w;
+                        out16[o + t] = (uint16_t)(w >> (16 * (t & 1)));
+                    }
+                }
+            }
+#endif
             // the stream's last codeword: its chain is decoded again, alone, for its end bit
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
@@ -3810,6 +3846,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                     *y.end = b0 + (uint64_t)(base - pp);
                 }
             }
+#if !HZ_PIECE_DIRECT
             __builtin_amdgcn_wave_barrier();
             // the round's run [Ra, Rb) (clamped to the stream): 16-byte stores of whole aligned groups
             // of 8, single symbols at the two ends (the neighbouring runs own the rest)
@@ -3830,6 +3867,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             for (uint64_t cg = h1 / 8 + (uint64_t)lane; cg < t0 / 8; cg += 64)
                 reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - Rz / 8];
             if ((uint64_t)lane < Rb - t0) out16[t0 + lane] = obuf[t0 + lane - Rz];
+#endif
         }
         // the next group's records and staging chunks (after the last round: their 22 VGPRs beside the
         // chains' spill at 1024 threads)
