@@ -490,7 +490,7 @@ def main():
             # `extract` of an index-less file: the payload read (twice: the length walk and the decode
             # pass) and the output written; algorithmic bytes C + N (payload in, symbols out)
             "extract_roofline": {
-                "kernels": ["seg_walk", "seg_fix", "scan", "seg_decode"],
+                "kernels": ["seg_walk", "seg_fix", "scan", "piece_decode"],
                 "bound": "hbm",
                 "ms": extract["ms"],
                 "achieved": round((C + 2 * nsym) / (extract["ms"] / 1e3) / 1e9, 1) if extract["ms"] else None,

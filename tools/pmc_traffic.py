@@ -39,15 +39,15 @@ STAGES = {
     "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
                "k_sync_subs"),
               ("k_sync_subs", "k_idx_fixed16")),
-    "extract": (("k_seg_walk", "k_seg_fix", "k_seg_decode", "k_scan_reduce", "k_scan_tiles", "k_scan_apply"),
-                ("k_seg_decode",)),
+    "extract": (("k_seg_walk", "k_seg_fix", "k_piece_decode", "k_scan_reduce", "k_scan_tiles", "k_scan_apply"),
+                ("k_piece_decode",)),
 }
 
 
 # kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
 WIDE_READ = ("k_hist16", "k_hist16_rng", "k_range_dot", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16",
              "k_pack_fixed16_blk", "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk", "k_seg_walk",
-             "k_seg_decode")
+             "k_piece_decode")
 
 
 def _is(name, k):
