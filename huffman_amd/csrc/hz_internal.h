@@ -132,20 +132,34 @@ constexpr int kDecMaxWaves = 16;
 // Index-less decoder (k_piece_decode, hz_kernels.hip): waves per workgroup and the per-wave LDS
 // (a group of segments' payload slot + one round's output buffer). The walk records the start of
 // every 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
+// HZ_PIECE_QUADS: pieces per lane per round in quads (2: eight chains as two quads, each quad's
+// global gathers landing behind the other's LDS walk, like k_decode's two blocks per wave; 1: four
+// chains as two pairs)
+#ifndef HZ_PIECE_QUADS
+#define HZ_PIECE_QUADS 1
+#endif
+// HZ_PIECE_DIRECT: whole pieces leave as 16-byte stores from registers (no LDS output buffer: its
+// room goes to the LUT's LDS heads, fewer global gathers); 0: through a per-round LDS buffer
+#ifndef HZ_PIECE_DIRECT
+#define HZ_PIECE_DIRECT 1
+#endif
 #ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES 16
+#define HZ_PIECE_WAVES (HZ_PIECE_QUADS == 2 ? 8 : 16)
 #endif
 constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
-constexpr uint32_t kPieceObufSyms = 256 * 8 + 8;  // a round's 256 pieces of 8, from an 8-aligned start
+constexpr uint32_t kPieceLaneChains = 4 * HZ_PIECE_QUADS;
+constexpr uint32_t kPieceMaxGroup = 8 * HZ_PIECE_QUADS;               // segments per group
+constexpr uint32_t kPieceObufSyms = 64 * kPieceLaneChains * 8 + 8;     // a round's pieces of 8, from an 8-aligned start
 struct PieceGeom {
-    uint32_t gs;          // segments per group (<= 8)
+    uint32_t gs;          // segments per group (<= kPieceMaxGroup)
     uint32_t rcap;        // piece records per segment (multiple of 16)
     uint32_t slot_words;  // payload staging words (multiple of 4)
     uint32_t wave_words;
 };
-// slot + output buffer (+ 64 per-lane dummy slots) + the group's segment table (8 x 3 u32)
+// slot + output buffer (+ 64 per-lane dummy slots; none when HZ_PIECE_DIRECT) + the group's segment
+// table (3 u32 per segment)
 __host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
-    return slot_words + (kPieceObufSyms + 64) / 2 + 24;
+    return slot_words + (HZ_PIECE_DIRECT ? 0u : (kPieceObufSyms + 64) / 2) + ((3 * kPieceMaxGroup + 3) & ~3u);
 }
 // avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
 // over the expected count of a segment (a segment past it sets error flag 64: the caller
@@ -156,8 +170,8 @@ inline PieceGeom piece_geom(double avg_bits, int max_len) {
     const double recs = per_seg / 8.0;
     uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16u;
     g.rcap = rcap < 16u ? 16u : (rcap > 528u ? 528u : rcap);
-    uint32_t gs = (uint32_t)(230.0 / (recs + 1.0));  // ~230 of a round's 256 pieces
-    g.gs = gs < 1u ? 1u : (gs > 8u ? 8u : gs);
+    uint32_t gs = (uint32_t)(0.9 * 64.0 * kPieceLaneChains / (recs + 1.0));  // ~90 % of a round's pieces
+    g.gs = gs < 1u ? 1u : (gs > kPieceMaxGroup ? kPieceMaxGroup : gs);
     g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;
     g.wave_words = piece_wave_words(g.slot_words);
     return g;

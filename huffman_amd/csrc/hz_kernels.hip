@@ -3638,26 +3638,21 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
 
 // Block-parallel decode of groups of y.gs segments (k_decode's chain machinery): the
 // group's payload bits [start + 4096 k0, + 4096 gs + 8 max_len) staged (descending) in the
-// wave's slot; rounds of 256 pieces, lane l taking pieces 64 c + l (c < 4) as two pairs
-// whose global gathers land behind the other pair's LDS walk; a round's symbols (one
+// wave's slot; rounds of 64 * kPieceChains pieces, lane l taking pieces 64 c + l as two halves
+// (pairs or quads) whose global gathers land behind the other half's LDS walk; a round's symbols (one
 // contiguous output run: its pieces are consecutive) go to the wave's LDS output buffer at
 // their place (slot 0 = the run's first symbol rounded down to 8) and leave as 16-byte
 // stores (2-byte stores at the run's two ends). A group's segment records and staging
 // loads are issued together (one memory round trip), its piece records in a second.
 constexpr uint32_t kPieceSyms = 8;  // codewords per piece: one decode chain
-constexpr int kPieceChains = 4;     // pieces per lane per round
-static_assert(kPieceChains == 4, "two pairs");
-constexpr uint32_t kPieceMaxGroup = 8;
+constexpr int kPieceChains = (int)kPieceLaneChains;  // pieces per lane per round
+constexpr int kPieceHalf = kPieceChains / 2;          // a pair or a quad
+static_assert(kPieceChains == 4 || kPieceChains == 8, "two pairs or two quads");
 constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
 static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h output buffer");
-#ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES 16
-#endif
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
 static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
-#ifndef HZ_PIECE_DIRECT
-#define HZ_PIECE_DIRECT 0  // 1: output stored from registers (16 GiB Zipf 17.1 vs 16.5 ms through the LDS buffer)
-#endif
+
 
 struct PieceArgs {
     const unsigned long long* ent;
@@ -3702,7 +3697,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     const uint32_t wave_words = piece_wave_words(y.slot_words);
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
-    uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + kPieceObufSyms + 64);  // per segment: cnt, entry, F (u32)
+    uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + (HZ_PIECE_DIRECT ? 0u : kPieceObufSyms + 64));  // cnt, entry, F
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
@@ -3777,10 +3772,10 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             for (int c = 0; c < kPieceChains; ++c) p1[c] = base - st0[c];
             PipeLane st[kPieceChains];
             uint32_t gv[kPieceChains];
-            auto issue2 = [&](int c) {
-                dec_pipe_ldsn<2>(d, lds, p1 + c, st + c);
-                gv[c] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c].gi, 0, 0);
-                gv[c + 1] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + 1].gi, 0, 0);
+            auto issueh = [&](int c) {  // a half's LDS walk, then its global gathers
+                dec_pipe_ldsn<kPieceHalf>(d, lds, p1 + c, st + c);
+#pragma unroll
+                for (int u = 0; u < kPieceHalf; ++u) gv[c + u] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + u].gi, 0, 0);
             };
 #if HZ_PIECE_DIRECT
             // symbols packed in registers (an even step keeps the entry, the odd one packs both symbols,
@@ -3801,15 +3796,15 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 obuf[t < cn[c] ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
             };
 #endif
-            issue2(0);
+            issueh(0);
 #pragma unroll
             for (uint32_t t = 0; t < kPieceSyms; ++t) {
-                issue2(2);
-                finish(0, t);
-                finish(1, t);
-                if (t + 1 < kPieceSyms) issue2(0);
-                finish(2, t);
-                finish(3, t);
+                issueh(kPieceHalf);
+#pragma unroll
+                for (int u = 0; u < kPieceHalf; ++u) finish(u, t);
+                if (t + 1 < kPieceSyms) issueh(0);
+#pragma unroll
+                for (int u = kPieceHalf; u < kPieceChains; ++u) finish(u, t);
             }
 #if HZ_PIECE_DIRECT
             // whole pieces: 16 bytes at output symbol F0 + o (2-byte aligned: the hardware takes unaligned
@@ -3834,7 +3829,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             // the stream's last codeword: its chain is decoded again, alone, for its end bit
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
-                const bool is_end = cn[c] > 0 && (uint64_t)(int64_t)((int32_t)ob[c] + R0) + F0 + cn[c] == y.nsym;
+                const bool is_end = cn[c] > 0 && (uint32_t)((int32_t)ob[c] + R0) + cn[c] == lim && lim == y.nsym - F0;
                 if (__builtin_expect(is_end, 0)) {
                     uint32_t pp = base - st0[c];
                     for (uint32_t t = 0; t < cn[c]; ++t) {
@@ -3849,24 +3844,26 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
 #if !HZ_PIECE_DIRECT
             __builtin_amdgcn_wave_barrier();
             // the round's run [Ra, Rb) (clamped to the stream): 16-byte stores of whole aligned groups
-            // of 8, single symbols at the two ends (the neighbouring runs own the rest)
+            // of 8, single symbols at the two ends (the neighbouring runs own the rest); offsets from
+            // obuf slot 0 = output symbol Rz (a multiple of 8)
             const uint32_t rl = (T - r0 < kPieceRound ? T - r0 : kPieceRound) - 1;  // the round's last piece
-            const uint64_t Rz = F0 + (uint64_t)(int64_t)R0;                           // obuf slot 0
-            const uint64_t Ra = Rz + readlane(ob[0], 0);
             uint32_t obl = ob[0], cnl = cn[0];
 #pragma unroll
             for (int c = 1; c < kPieceChains; ++c) {
                 obl = (rl >> 6) == (uint32_t)c ? ob[c] : obl;
                 cnl = (rl >> 6) == (uint32_t)c ? cn[c] : cnl;
             }
-            uint64_t Rb = Rz + readlane(obl, (int)(rl & 63)) + readlane(cnl, (int)(rl & 63));
-            Rb = Rb > Ra ? Rb : Ra;
-            const uint64_t h1 = ((Ra + 7) & ~7ull) < Rb ? ((Ra + 7) & ~7ull) : Rb;
-            if ((uint64_t)lane < h1 - Ra) out16[Ra + lane] = obuf[Ra + lane - Rz];
-            const uint64_t t0 = (Rb & ~7ull) > h1 ? (Rb & ~7ull) : h1;
-            for (uint64_t cg = h1 / 8 + (uint64_t)lane; cg < t0 / 8; cg += 64)
-                reinterpret_cast<uint4*>(d.out)[cg] = reinterpret_cast<const uint4*>(obuf)[cg - Rz / 8];
-            if ((uint64_t)lane < Rb - t0) out16[t0 + lane] = obuf[t0 + lane - Rz];
+            const uint32_t a0 = readlane(ob[0], 0);
+            uint32_t b1 = readlane(obl, (int)(rl & 63)) + readlane(cnl, (int)(rl & 63));
+            b1 = b1 > a0 ? b1 : a0;
+            const uint32_t h1 = ((a0 + 7) & ~7u) < b1 ? ((a0 + 7) & ~7u) : b1;  // the first whole group
+            const uint32_t t0 = (b1 & ~7u) > h1 ? (b1 & ~7u) : h1;              // past the last one
+            uint16_t* orun = out16 + F0 + (uint64_t)(int64_t)R0;                   // output symbol Rz
+            if ((uint32_t)lane < h1 - a0) orun[a0 + lane] = obuf[a0 + lane];
+            uint4* o4 = reinterpret_cast<uint4*>(orun);
+            const uint4* b4 = reinterpret_cast<const uint4*>(obuf);
+            for (uint32_t cg = h1 / 8 + (uint32_t)lane; cg < t0 / 8; cg += 64) o4[cg] = b4[cg];
+            if ((uint32_t)lane < b1 - t0) orun[t0 + lane] = obuf[t0 + lane];
 #endif
         }
         // the next group's records and staging chunks (after the last round: their 22 VGPRs beside the
