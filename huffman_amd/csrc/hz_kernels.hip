@@ -255,7 +255,7 @@ HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v,
 // run (loads and LDS ops use separate counters). Refills past the end re-read the last
 // vector (branch-free, so the waits stay vmcnt(DEPTH - 1)); the tail counts what is left.
 #ifndef HZ_HIST_DEPTH
-#define HZ_HIST_DEPTH 4
+#define HZ_HIST_DEPTH 8
 #endif
 template <typename Rec = NoRec>
 HZ_DEV void hist_sweep(uint32_t* lds, unsigned long long* hist, const uint4* in4, uint64_t i, uint64_t end,
