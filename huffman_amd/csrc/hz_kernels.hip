@@ -3495,11 +3495,14 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
         ++rj;
         rfl = false;
     };
+    // segment sj - 1's record row, count and (segment sj's) entry: pointers advanced at each crossing
+    uint16_t* rrow = y.rec + seg0 * y.rcap;
+    unsigned long long* cntp = y.cnt + seg0;
+    unsigned long long* entp = y.ent + seg0;
     auto rec_store = [&]() {  // the group holding record rj - 1 (nothing in the lead-in before seg0)
         if (sj == seg0) return;
         if (rj <= y.rcap)
-            *reinterpret_cast<uint4*>(y.rec + (sj - 1) * y.rcap + ((rj - 1) & ~(RG - 1))) =
-                *reinterpret_cast<const uint4*>(rbuf);
+            *reinterpret_cast<uint4*>(rrow + ((rj - 1) & ~(RG - 1))) = *reinterpret_cast<const uint4*>(rbuf);
         else
             atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
     };
@@ -3511,22 +3514,25 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
         rfl |= rn;
     };
     // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
+    bool more = live;  // sj <= seg1 for a live chain: crossings still to record
     auto cross = [&]() {
-        if (__builtin_expect(p >= nb, 0) && sj <= seg1 && live) {
+        if (__builtin_expect(p >= nb, 0) && more) {
             if (rfl && roff < nb) {  // a record inside the segment (not its successor's entry)
                 rec_put();
                 if ((rj & (RG - 1)) == 0u) rec_store();
             }
             rfl = false;
             if (sj > seg0) {
-                y.cnt[sj - 1] = cc;
+                *cntp++ = cc;
                 if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
+                rrow += y.rcap;
             }
-            if (sj < seg1) y.ent[sj] = abs0 + p;
-            else y.xit[ch] = abs0 + p;
+            *(sj < seg1 ? entp : y.xit + ch) = abs0 + p;
+            ++entp;
             cc = 0;
             rj = 0;
             ++sj;
+            more = sj <= seg1;
             nb += kSegBits;
         }
     };
