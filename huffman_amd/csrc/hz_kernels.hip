@@ -3657,6 +3657,9 @@ static_assert(kPieceChains == 4 || kPieceChains == 8, "two pairs or two quads");
 constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
 static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h output buffer");
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
+#ifndef HZ_PIECE_EARLY
+#define HZ_PIECE_EARLY 0  // 1: the next group's loads issued at this group's start (their VGPRs live throughout)
+#endif
 static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
 
 
@@ -3679,6 +3682,7 @@ HZ_DEV uint64_t readlane64(uint64_t v, int l) {
 struct PieceIn {
     uint64_t c, e, f;
     uint4 sv[kStageUnroll];
+    uint4 rr;  // 16 bytes of the group's record rows (1 KiB per wave: all of them, host geometry)
 };
 HZ_DEV void piece_prefetch(const DecArgs& d, const PieceArgs& y, uint64_t g, int lane, PieceIn& x) {
     const uint64_t gg = g * y.gs < y.nseg ? g : 0;  // past the end: any group, never used
@@ -3688,6 +3692,8 @@ HZ_DEV void piece_prefetch(const DecArgs& d, const PieceArgs& y, uint64_t g, int
     x.c = y.cnt[kk];
     x.e = y.ent[kk];
     x.f = y.first[kk];
+    const uint32_t rbytes = ns * y.rcap * 2u, ro = 16u * (uint32_t)lane;
+    x.rr = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(y.rec + k0 * y.rcap) + (ro < rbytes ? ro : 0u));
     PipeMeta m;
     m.b0 = y.start + k0 * kSegBits;
     m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
@@ -3704,6 +3710,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
     uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + (HZ_PIECE_DIRECT ? 0u : kPieceObufSyms + 64));  // cnt, entry, F
+    uint16_t* rlds = reinterpret_cast<uint16_t*>(sinfo + ((3 * kPieceMaxGroup + 3) & ~3u));  // the group's records
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
@@ -3735,6 +3742,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             sinfo[3 * lane + 1] = (uint32_t)(cur.e - b0);
             sinfo[3 * lane + 2] = (uint32_t)(cur.f - F0);
         }
+        reinterpret_cast<uint4*>(rlds)[lane] = cur.rr;
         // the group's payload bits, staged descending (k_decode's layout)
         PipeMeta m;
         m.b0 = b0;
@@ -3744,8 +3752,10 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
         __builtin_amdgcn_wave_barrier();  // the previous round's output copy has read the buffer
         dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, cur.sv, w0);
         const uint32_t base = top * 32u - (uint32_t)(b0 + d.bit_adj - (w0 << 5));
-        const uint16_t* recg = y.rec + k0 * y.rcap;  // the group's record rows
         __builtin_amdgcn_wave_barrier();
+#if HZ_PIECE_EARLY
+        piece_prefetch(d, y, g + gstride, lane, nxt);  // the next group's loads, a whole group ahead
+#endif
         for (uint32_t r0 = 0; r0 < T; r0 += kPieceRound) {
             uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], st0[kPieceChains];
             int32_t R0 = 0;  // the round's output run starts at F0 + R0, rounded down to 8 (from F0)
@@ -3770,8 +3780,8 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 cn[c] = n;
                 ob[c] = (uint32_t)((int32_t)o - R0);
                 // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
-                // segment's first bit); all four record loads in flight together
-                const uint32_t rv = recg[sg * y.rcap + (i ? i - 1 : 0)];
+                // segment's first bit, prefetched with the group into LDS)
+                const uint32_t rv = rlds[sg * y.rcap + (i ? i - 1 : 0)];
                 st0[c] = i ? sg * kSegBits + rv : es;  // from b0
             }
 #pragma unroll
@@ -3872,9 +3882,11 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             if ((uint32_t)lane < b1 - t0) orun[t0 + lane] = obuf[t0 + lane];
 #endif
         }
-        // the next group's records and staging chunks (after the last round: their 22 VGPRs beside the
+#if !HZ_PIECE_EARLY
+        // the next group's records and staging chunks (after the last round: their VGPRs beside the
         // chains' spill at 1024 threads)
         piece_prefetch(d, y, g + gstride, lane, nxt);
+#endif
         cur = nxt;
     }
 }

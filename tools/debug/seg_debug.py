@@ -44,7 +44,7 @@ lib = load()
 # scratch layout (hz_kernels.hip launch_decode_indexless): piece records (u16) first, then ent, cnt, first
 per_seg = 4096.0 / max(bits / nsym, 1.0)
 recs = per_seg / 8.0
-rcap = min(max(int((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16, 16), 528)
+rcap = min(max(int((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16, 16), 512)
 REC = (nseg * rcap + 3) // 4 + 2
 words = REC + 5 * nseg + 8
 buf = np.zeros(words, dtype=np.uint64)
