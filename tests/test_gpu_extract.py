@@ -114,3 +114,21 @@ def test_indexless_fixups_without_lead_in(built_lib, lead):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, HZ_SEG_LEAD=lead))
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def test_indexless_dense_run_takes_the_index_path(codec):
+    """A long run of the most frequent symbol packs ~1800 codewords into a 4096-bit segment, far
+    more piece records than planned from the stream's average code length: the walk flags it
+    (error bit 64) and hz_decode_indexless decodes through hz_index_build + hz_decode instead;
+    the output and the end bit are the same."""
+    import torch
+    rng = np.random.default_rng(11)
+    nsym = 8 << 20
+    sym = rng.integers(1, 32769, nsym).astype("<u2")
+    sym[nsym // 3: nsym // 3 + nsym // 5] = 0  # 20 % of the stream, one contiguous run
+    x = torch.from_numpy(sym.view(np.uint8).copy()).cuda()
+    ok, end_ok = _check(codec, x)
+    assert ok and end_ok
+    # and the device context is clean afterwards (the overflow flag was cleared)
+    ok2, end_ok2 = _check(codec, x, shift=3)
+    assert ok2 and end_ok2
