@@ -3499,10 +3499,12 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     uint16_t* rrow = y.rec + seg0 * y.rcap;
     unsigned long long* cntp = y.cnt + seg0;
     unsigned long long* entp = y.ent + seg0;
-    bool ovf = false;  // a segment with more records than rcap (flag 64 once, at the end)
-    auto rec_store = [&]() {  // the group holding record rj - 1 (rj > 0, segment sj - 1 >= seg0)
-        if (rj <= y.rcap) *reinterpret_cast<uint4*>(rrow + ((rj - 1) & ~(RG - 1))) = *reinterpret_cast<const uint4*>(rbuf);
-        ovf |= rj > y.rcap;
+    auto rec_store = [&]() {  // the group holding record rj - 1 (nothing in the lead-in before seg0)
+        if (sj == seg0) return;
+        if (rj <= y.rcap)
+            *reinterpret_cast<uint4*>(rrow + ((rj - 1) & ~(RG - 1))) = *reinterpret_cast<const uint4*>(rbuf);
+        else
+            atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
     };
     // after a codeword: its end p is the start of the segment's codeword cc; every 8th is a record
     // (one the crossing below turns into the next segment's entry is dropped there)
@@ -3512,15 +3514,17 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
         rfl |= rn;
     };
     // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
-    bool more = live;     // sj <= seg1 for a live chain: crossings still to record
-    bool inseg = false;   // sj > seg0: past the lead-in
+    bool more = live;  // sj <= seg1 for a live chain: crossings still to record
     auto cross = [&]() {
         if (__builtin_expect(p >= nb, 0) && more) {
-            if (rfl && roff < nb) rec_put();  // a record inside the segment (not its successor's entry)
+            if (rfl && roff < nb) {  // a record inside the segment (not its successor's entry)
+                rec_put();
+                if ((rj & (RG - 1)) == 0u) rec_store();
+            }
             rfl = false;
-            if (inseg) {
+            if (sj > seg0) {
                 *cntp++ = cc;
-                if (rj) rec_store();  // the segment's last group (again when full: the same bytes)
+                if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
                 rrow += y.rcap;
             }
             *(sj < seg1 ? entp : y.xit + ch) = abs0 + p;
@@ -3529,7 +3533,6 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             rj = 0;
             ++sj;
             more = sj <= seg1;
-            inseg = true;
             nb += kSegBits;
         }
     };
@@ -3585,12 +3588,11 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             }
             if (rfl) {
                 rec_put();
-                if ((rj & (RG - 1)) == 0u && inseg) rec_store();
+                if ((rj & (RG - 1)) == 0u) rec_store();
             }
         }
         seg_feed(a, ring, fd, p);
     }
-    if (ovf) atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
 }
 
 // Chain i (>= 1) against chain i - 1's exit: the true path enters segment seg0(i) at xit[i - 1].
