@@ -803,7 +803,6 @@ HZ_DEV void pack_copyout(const PackArgs& a, const uint32_t* slot, int lane, cons
 // Lane bits, decode-chain offsets, wave scan of the bit counts.
 template <int MODE>
 HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
-    constexpr int SH = PackEnt<MODE>::kShift;
     uint32_t n = 0;
 #pragma unroll
     for (int k = 0; k < kSPT; ++k) {
@@ -3716,7 +3715,9 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
     const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
+#if !HZ_PIECE_DIRECT
     const uint32_t dummy = kPieceObufSyms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
+#endif
     uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
     PieceIn cur, nxt;
     if (g < ngroups) piece_prefetch(d, y, g, lane, cur);
