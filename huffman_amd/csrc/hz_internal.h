@@ -157,9 +157,9 @@ struct PieceGeom {
     uint32_t wave_words;
 };
 // slot + output buffer (+ 64 per-lane dummy slots; none when HZ_PIECE_DIRECT) + the group's segment
-// table (3 u32 per segment) + its record rows (1 KiB)
+// table (3 u32 per segment) + its piece starts (u16, 2 KiB)
 __host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
-    return slot_words + (HZ_PIECE_DIRECT ? 0u : (kPieceObufSyms + 64) / 2) + ((3 * kPieceMaxGroup + 3) & ~3u) + 256u;
+    return slot_words + (HZ_PIECE_DIRECT ? 0u : (kPieceObufSyms + 64) / 2) + ((3 * kPieceMaxGroup + 3) & ~3u) + 512u;
 }
 // avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
 // over the expected count of a segment (a segment past it sets error flag 64: the caller
@@ -169,10 +169,10 @@ inline PieceGeom piece_geom(double avg_bits, int max_len) {
     const double per_seg = 4096.0 / (avg_bits > 1.0 ? avg_bits : 1.0);  // codewords per segment
     const double recs = per_seg / 8.0;
     uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16u;
-    g.rcap = rcap < 16u ? 16u : (rcap > 512u ? 512u : rcap);
+    g.rcap = rcap < 16u ? 16u : (rcap > 1024u ? 1024u : rcap);
     uint32_t gs = (uint32_t)(0.9 * 64.0 * kPieceLaneChains / (recs + 1.0));  // ~90 % of a round's pieces
     g.gs = gs < 1u ? 1u : (gs > kPieceMaxGroup ? kPieceMaxGroup : gs);
-    if (g.gs * g.rcap > 512u) g.gs = 512u / g.rcap > 0u ? 512u / g.rcap : 1u;  // records of a group <= 1 KiB
+    if (g.gs * g.rcap > 1024u) g.gs = 1024u / g.rcap > 0u ? 1024u / g.rcap : 1u;  // a group's records <= 1 KiB
     g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;
     g.wave_words = piece_wave_words(g.slot_words);
     return g;

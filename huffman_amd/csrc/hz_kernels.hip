@@ -3349,8 +3349,8 @@ struct SegArgs {
     unsigned long long* cnt;    // [nseg] codewords starting in it
     unsigned long long* xit;    // [nchains] exit bit of every walk chain
     unsigned long long* first;  // [nseg] F (k_scan_apply of cnt)
-    uint16_t* rec;              // [nseg][rcap] piece records (16-byte aligned rows)
-    uint32_t rcap;              // records per segment (multiple of 8; more is an error, flag 64)
+    uint8_t* rec;               // [nseg][rcap] piece records: u8 deltas (16-byte aligned rows)
+    uint32_t rcap;              // records per segment (multiple of 16; more is an error, flag 64)
     uint32_t* dirty[2];         // k_seg_fix: chains to check, ping-pong
     uint32_t* changed;
     uint32_t* err;
@@ -3484,18 +3484,21 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
 #ifndef HZ_EXP_REC
 #define HZ_EXP_REC 1  // timing builds only: 0 = no records (the decode is then wrong)
 #endif
-    constexpr uint32_t RG = 8;
-    uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + kSegWalkWaves * 64 * kSegRing) + 8 * threadIdx.x;
-    uint32_t rj = 0, roff = 0;
+    // A record is the distance in bits from the previous one (from the segment's entry for the
+    // first): at most 8 codes of <= 22 bits, so one byte (the decoder rebuilds the offsets by a scan).
+    constexpr uint32_t RG = 16;
+    uint8_t* rbuf = reinterpret_cast<uint8_t*>(lds + kSegWalkWaves * 64 * kSegRing) + 16 * threadIdx.x;
+    uint32_t rj = 0, roff = 0, rprev = 0;
     bool rfl = false;
-    // roff: the ring position of the pending record (converted to a segment offset when put)
+    // roff: the ring position of the pending record; rprev: the previous record's (or the entry's)
     auto rec_put = [&]() {
-        rbuf[rj & (RG - 1)] = (uint16_t)(roff + kSegBits - nb);
+        rbuf[rj & (RG - 1)] = (uint8_t)(roff - rprev);
+        rprev = roff;
         ++rj;
         rfl = false;
     };
     // segment sj - 1's record row, count and (segment sj's) entry: pointers advanced at each crossing
-    uint16_t* rrow = y.rec + seg0 * y.rcap;
+    uint8_t* rrow = y.rec + seg0 * y.rcap;
     unsigned long long* cntp = y.cnt + seg0;
     unsigned long long* entp = y.ent + seg0;
     auto rec_store = [&]() {  // the group holding record rj - 1 (nothing in the lead-in before seg0)
@@ -3530,6 +3533,7 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             ++entp;
             cc = 0;
             rj = 0;
+            rprev = p;  // the new segment's entry
             ++sj;
             more = sj <= seg1;
             nb += kSegBits;
@@ -3618,7 +3622,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
             if (p == y.ent[s]) { met = true; break; }
             y.ent[s] = p;
             const uint64_t sb = start + (s + 1) * kSegBits;
-            uint64_t n = 0;
+            uint64_t n = 0, pprev = p;
             while (p < sb) {
                 uint32_t sym;
                 const uint32_t L = br_next<MODE>(r, a, lds, sym);
@@ -3627,8 +3631,9 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
                 ++n;
                 if ((n & 7u) == 0 && p < sb) {
                     const uint64_t j = (n >> 3) - 1;
-                    if (j < y.rcap) y.rec[s * y.rcap + j] = (uint16_t)(p + kSegBits - sb);
+                    if (j < y.rcap) y.rec[s * y.rcap + j] = (uint8_t)(p - pprev);
                     else atomicOr(y.err, 64u);
+                    pprev = p;
                 }
             }
             y.cnt[s] = n;
@@ -3666,7 +3671,7 @@ struct PieceArgs {
     const unsigned long long* ent;
     const unsigned long long* cnt;
     const unsigned long long* first;
-    const uint16_t* rec;
+    const uint8_t* rec;
     uint32_t rcap, gs;
     uint32_t slot_words;   // staging words per wave (multiple of 4)
     uint64_t nseg, start, nsym;
@@ -3691,8 +3696,8 @@ HZ_DEV void piece_prefetch(const DecArgs& d, const PieceArgs& y, uint64_t g, int
     x.c = y.cnt[kk];
     x.e = y.ent[kk];
     x.f = y.first[kk];
-    const uint32_t rbytes = ns * y.rcap * 2u, ro = 16u * (uint32_t)lane;
-    x.rr = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(y.rec + k0 * y.rcap) + (ro < rbytes ? ro : 0u));
+    const uint32_t rbytes = ns * y.rcap, ro = 16u * (uint32_t)lane;
+    x.rr = *reinterpret_cast<const uint4*>(y.rec + k0 * y.rcap + (ro < rbytes ? ro : 0u));
     PipeMeta m;
     m.b0 = y.start + k0 * kSegBits;
     m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
@@ -3709,7 +3714,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
     uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
     uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + (HZ_PIECE_DIRECT ? 0u : kPieceObufSyms + 64));  // cnt, entry, F
-    uint16_t* rlds = reinterpret_cast<uint16_t*>(sinfo + ((3 * kPieceMaxGroup + 3) & ~3u));  // the group's records
+    uint16_t* rlds = reinterpret_cast<uint16_t*>(sinfo + ((3 * kPieceMaxGroup + 3) & ~3u));  // piece starts (from b0)
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
@@ -3743,7 +3748,35 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             sinfo[3 * lane + 1] = (uint32_t)(cur.e - b0);
             sinfo[3 * lane + 2] = (uint32_t)(cur.f - F0);
         }
-        reinterpret_cast<uint4*>(rlds)[lane] = cur.rr;
+        // the group's piece starts from its records: lane l holds records 16 l .. 16 l + 15 (one row
+        // never splits a lane: rcap % 16 == 0); in-lane prefix, then a scan across the lanes of a row
+        // (segmented at row starts), plus the row's entry; u16 offsets from b0 into LDS
+        {
+            const uint32_t w[4] = {cur.rr.x, cur.rr.y, cur.rr.z, cur.rr.w};
+            uint32_t pre[16], acc = 0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                acc += (w[t >> 2] >> (8 * (t & 3))) & 0xffu;
+                pre[t] = acc;
+            }
+            const uint32_t row = 16u * (uint32_t)lane / y.rcap;                // the lane's segment in the group
+            const bool head = (16u * (uint32_t)lane) % y.rcap == 0u;
+            uint32_t v = acc;                                                  // segmented inclusive scan
+            bool f = head;
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t ov = shfl_up_u32(v, dd);
+                const uint32_t of = shfl_up_u32(f ? 1u : 0u, dd);
+                if (lane >= dd && !f) { v += ov; f = of != 0u; }
+            }
+            const uint32_t base0 = (row < ns ? sinfo[3 * row + 1] : 0u) + v - acc;  // entry + records before the lane
+            uint32_t o2[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) o2[t] = ((base0 + pre[2 * t]) & 0xffffu) | ((base0 + pre[2 * t + 1]) << 16);
+            uint4* r4 = reinterpret_cast<uint4*>(rlds) + 2 * lane;
+            r4[0] = make_uint4(o2[0], o2[1], o2[2], o2[3]);
+            r4[1] = make_uint4(o2[4], o2[5], o2[6], o2[7]);
+        }
         // the group's payload bits, staged descending (k_decode's layout)
         PipeMeta m;
         m.b0 = b0;
@@ -3783,7 +3816,7 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
                 // segment's first bit, prefetched with the group into LDS)
                 const uint32_t rv = rlds[sg * y.rcap + (i ? i - 1 : 0)];
-                st0[c] = i ? sg * kSegBits + rv : es;  // from b0
+                st0[c] = i ? rv : es;  // from b0
             }
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) p1[c] = base - st0[c];
@@ -3905,7 +3938,7 @@ uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t 
     const PieceGeom pg = seg_piece_geom(payload_bytes, start_bit, nsym, max_len);
     // records (u16, 16-byte rows); ent, cnt, first, xit (<= nseg chains) (u64); dirty[2] (u32); changed,
     // end; tiles
-    return (nseg * pg.rcap + 3) / 4 + 2 + 4 * nseg + nseg + 4 + ntiles + 24;
+    return (nseg * pg.rcap + 7) / 8 + 2 + 4 * nseg + nseg + 4 + ntiles + 24;
 }
 
 bool seg_decode_supported(const Tables& t) {
@@ -3936,7 +3969,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     y.rcap = pg.rcap;
     y.err = d_err;
     unsigned long long* p = d_scratch;
-    y.rec = reinterpret_cast<uint16_t*>(p); p += (y.nseg * y.rcap + 3) / 4 + 2;
+    y.rec = reinterpret_cast<uint8_t*>(p); p += (y.nseg * y.rcap + 7) / 8 + 2;
     y.ent = p; p += y.nseg;
     y.cnt = p; p += y.nseg;
     y.first = p; p += y.nseg;

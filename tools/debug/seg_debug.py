@@ -44,13 +44,13 @@ lib = load()
 # scratch layout (hz_kernels.hip launch_decode_indexless): piece records (u16) first, then ent, cnt, first
 per_seg = 4096.0 / max(bits / nsym, 1.0)
 recs = per_seg / 8.0
-rcap = min(max(int((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16, 16), 512)
-REC = (nseg * rcap + 3) // 4 + 2
+rcap = min(max(int((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16, 16), 1024)
+REC = (nseg * rcap + 7) // 8 + 2
 words = REC + 5 * nseg + 8
 buf = np.zeros(words, dtype=np.uint64)
 rc = lib.hz_debug_scratch(c.dev.h, buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint64(words))
 print("scratch rc", rc, "nseg", nseg, "rcap", rcap)
-rec = buf[:REC].view(np.uint16)[:nseg * rcap].reshape(nseg, rcap)
+rec = buf[:REC].view(np.uint8)[:nseg * rcap].reshape(nseg, rcap)
 buf = buf[REC:]
 ent, cnt, first = buf[:nseg], buf[nseg:2 * nseg], buf[2 * nseg:3 * nseg]
 starts = plan.start_bit + 4096 * np.arange(nseg, dtype=np.uint64)
@@ -68,13 +68,13 @@ print("segments checked", lim, "entry diffs", de.size, de[:10], "count diffs", d
 for k in list(de[:3]) + list(dc[:3]):
     print(" seg", k, "ent", int(ent[k]), "true", int(true_ent[k]), "cnt", int(cnt[k]), "true", int(true_cnt[k]),
           "F", int(first[k]), "true", int(true_first[k]))
-# piece records: every 8th codeword start of a segment, as an offset from the segment's first bit
+# piece records: every 8th codeword start of a segment, as u8 distances from the previous one (the entry first)
 bad_rec = 0
 for k in range(min(lim, 2000)):
     e0 = np.searchsorted(tb, starts[k])
     e1 = np.searchsorted(tb, starts[k] + 4096)
     want = tb[e0 + 8:e1:8] - starts[k]
-    got_r = rec[k, :want.size].astype(np.uint64)
+    got_r = (int(ent[k]) - int(starts[k]) + np.cumsum(rec[k, :want.size].astype(np.int64))).astype(np.uint64)
     if want.size and not np.array_equal(want, got_r):
         bad_rec += 1
         if bad_rec <= 3:
