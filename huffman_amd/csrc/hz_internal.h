@@ -132,11 +132,11 @@ constexpr int kDecMaxWaves = 16;
 // Index-less decoder (k_piece_decode, hz_kernels.hip): waves per workgroup and the per-wave LDS
 // (a group of segments' payload slot + one round's output buffer). The walk records the start of
 // every 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
-// HZ_PIECE_QUADS: pieces per lane per round in quads (2: eight chains as two quads, each quad's
-// global gathers landing behind the other's LDS walk, like k_decode's two blocks per wave; 1: four
-// chains as two pairs)
-#ifndef HZ_PIECE_QUADS
-#define HZ_PIECE_QUADS 1
+// HZ_PIECE_CHAINS: pieces per lane per round, walked as pairs (4: two pairs, 6: three pairs) -- each
+// pair's global gathers land behind the other pairs' LDS walks -- or as two quads (8, like k_decode's
+// two blocks per wave)
+#ifndef HZ_PIECE_CHAINS
+#define HZ_PIECE_CHAINS 4
 #endif
 // HZ_PIECE_DIRECT: whole pieces leave as 16-byte stores from registers (no LDS output buffer: its
 // room goes to the LUT's LDS heads, fewer global gathers); 0: through a per-round LDS buffer
@@ -144,11 +144,11 @@ constexpr int kDecMaxWaves = 16;
 #define HZ_PIECE_DIRECT 1
 #endif
 #ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES (HZ_PIECE_QUADS == 2 ? 8 : 16)
+#define HZ_PIECE_WAVES (HZ_PIECE_CHAINS == 8 ? 8 : (HZ_PIECE_CHAINS == 6 ? 12 : 16))
 #endif
 constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
-constexpr uint32_t kPieceLaneChains = 4 * HZ_PIECE_QUADS;
-constexpr uint32_t kPieceMaxGroup = 8 * HZ_PIECE_QUADS;               // segments per group
+constexpr uint32_t kPieceLaneChains = HZ_PIECE_CHAINS;
+constexpr uint32_t kPieceMaxGroup = HZ_PIECE_CHAINS == 8 ? 16 : 8;  // segments per group
 constexpr uint32_t kPieceObufSyms = 64 * kPieceLaneChains * 8 + 8;     // a round's pieces of 8, from an 8-aligned start
 struct PieceGeom {
     uint32_t gs;          // segments per group (<= kPieceMaxGroup)
@@ -170,7 +170,7 @@ inline PieceGeom piece_geom(double avg_bits, int max_len) {
     const double recs = per_seg / 8.0;
     uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16u;
     g.rcap = rcap < 16u ? 16u : (rcap > 1024u ? 1024u : rcap);
-    uint32_t gs = (uint32_t)(0.9 * 64.0 * kPieceLaneChains / (recs + 1.0));  // ~90 % of a round's pieces
+    uint32_t gs = (uint32_t)(0.93 * 64.0 * kPieceLaneChains / (recs + 1.0));  // ~93 % of a round's pieces
     g.gs = gs < 1u ? 1u : (gs > kPieceMaxGroup ? kPieceMaxGroup : gs);
     if (g.gs * g.rcap > 1024u) g.gs = 1024u / g.rcap > 0u ? 1024u / g.rcap : 1u;  // a group's records <= 1 KiB
     g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;

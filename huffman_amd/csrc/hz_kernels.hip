@@ -3656,8 +3656,9 @@ __global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, 
 // loads are issued together (one memory round trip), its piece records in a second.
 constexpr uint32_t kPieceSyms = 8;  // codewords per piece: one decode chain
 constexpr int kPieceChains = (int)kPieceLaneChains;  // pieces per lane per round
-constexpr int kPieceHalf = kPieceChains / 2;          // a pair or a quad
-static_assert(kPieceChains == 4 || kPieceChains == 8, "two pairs or two quads");
+constexpr int kPieceGrp = kPieceChains == 8 ? 4 : 2;  // chains walked together: pairs, or quads for 8
+constexpr int kPieceNG = kPieceChains / kPieceGrp;     // groups of them per round (2 or 3)
+static_assert(kPieceChains == 4 || kPieceChains == 6 || kPieceChains == 8, "two or three pairs, or two quads");
 constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
 static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h output buffer");
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
@@ -3822,10 +3823,10 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
             for (int c = 0; c < kPieceChains; ++c) p1[c] = base - st0[c];
             PipeLane st[kPieceChains];
             uint32_t gv[kPieceChains];
-            auto issueh = [&](int c) {  // a half's LDS walk, then its global gathers
-                dec_pipe_ldsn<kPieceHalf>(d, lds, p1 + c, st + c);
+            auto issueh = [&](int c) {  // a pair's (quad's) LDS walk, then its global gathers
+                dec_pipe_ldsn<kPieceGrp>(d, lds, p1 + c, st + c);
 #pragma unroll
-                for (int u = 0; u < kPieceHalf; ++u) gv[c + u] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + u].gi, 0, 0);
+                for (int u = 0; u < kPieceGrp; ++u) gv[c + u] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + u].gi, 0, 0);
             };
 #if HZ_PIECE_DIRECT
             // symbols packed in registers (an even step keeps the entry, the odd one packs both symbols,
@@ -3846,15 +3847,19 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 obuf[t < cn[c] ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
             };
 #endif
+            // each group's gathers are consumed after the next group's walk has been issued
             issueh(0);
 #pragma unroll
             for (uint32_t t = 0; t < kPieceSyms; ++t) {
-                issueh(kPieceHalf);
 #pragma unroll
-                for (int u = 0; u < kPieceHalf; ++u) finish(u, t);
+                for (int gi = 1; gi < kPieceNG; ++gi) {
+                    issueh(gi * kPieceGrp);
+#pragma unroll
+                    for (int u = (gi - 1) * kPieceGrp; u < gi * kPieceGrp; ++u) finish(u, t);
+                }
                 if (t + 1 < kPieceSyms) issueh(0);
 #pragma unroll
-                for (int u = kPieceHalf; u < kPieceChains; ++u) finish(u, t);
+                for (int u = (kPieceNG - 1) * kPieceGrp; u < kPieceChains; ++u) finish(u, t);
             }
 #if HZ_PIECE_DIRECT
             // whole pieces: 16 bytes at output symbol F0 + o (2-byte aligned: the hardware takes unaligned
