@@ -471,13 +471,22 @@ struct PackIn {
     uint64_t bstart;
 };
 
+#ifndef HZ_PACK_NTLOAD
+#define HZ_PACK_NTLOAD 0
+#endif
 HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     const uint64_t ls = sym0 + kSPT <= a.nsym ? sym0 : 0;
     const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ls);
 #pragma unroll
     for (int q = 0; q < kSPT / 8; ++q) {
+#if HZ_PACK_NTLOAD
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v t = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p + q));  // streaming input:
+        const uint4 v = make_uint4(t.x, t.y, t.z, t.w);  // keep L2 for the escape table
+#else
         const uint4 v = p[q];
+#endif
         x.raw[4 * q] = v.x; x.raw[4 * q + 1] = v.y; x.raw[4 * q + 2] = v.z; x.raw[4 * q + 3] = v.w;
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
@@ -1902,6 +1911,9 @@ HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
 // exactly kStageUnroll loads per lane (static vmcnt for the pipelined waits):
 // chunks past the window or the payload read a clamped address and are fixed
 // up in registers. Requires nwords >= 4 (host check).
+#ifndef HZ_DEC_NTLOAD
+#define HZ_DEC_NTLOAD 0  // 1: staging loads non-temporal (keep L2 for the global LUT level)
+#endif
 HZ_DEV void dec_stage_prefetch(const DecArgs& a, const PipeMeta& m, int lane, uint4 (&v)[kStageUnroll]) {
     const uint64_t w0 = (((m.b0 + a.bit_adj) >> 5) & ~3ull) - 4;
 #pragma unroll
@@ -1909,7 +1921,13 @@ HZ_DEV void dec_stage_prefetch(const DecArgs& a, const PipeMeta& m, int lane, ui
         const uint64_t w = w0 + 4ull * ((uint32_t)lane + (uint32_t)u * kWave);
         const bool in = w < a.nwords;  // also false for a window that wrapped below word 0
         const uint64_t wl = !in ? 0 : (w + 4 <= a.nwords ? w : a.nwords - 4);
+#if HZ_DEC_NTLOAD
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v t = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(a.words + wl));
+        v[u] = make_uint4(t.x, t.y, t.z, t.w);
+#else
         v[u] = *reinterpret_cast<const uint4*>(a.words + wl);
+#endif
     }
 }
 
