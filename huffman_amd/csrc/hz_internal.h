@@ -138,28 +138,21 @@ constexpr int kDecMaxWaves = 16;
 #ifndef HZ_PIECE_CHAINS
 #define HZ_PIECE_CHAINS 4
 #endif
-// HZ_PIECE_DIRECT: whole pieces leave as 16-byte stores from registers (no LDS output buffer: its
-// room goes to the LUT's LDS heads, fewer global gathers); 0: through a per-round LDS buffer
-#ifndef HZ_PIECE_DIRECT
-#define HZ_PIECE_DIRECT 1
-#endif
 #ifndef HZ_PIECE_WAVES
 #define HZ_PIECE_WAVES (HZ_PIECE_CHAINS == 8 ? 8 : (HZ_PIECE_CHAINS == 6 ? 12 : 16))
 #endif
 constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
 constexpr uint32_t kPieceLaneChains = HZ_PIECE_CHAINS;
 constexpr uint32_t kPieceMaxGroup = HZ_PIECE_CHAINS == 8 ? 16 : 8;  // segments per group
-constexpr uint32_t kPieceObufSyms = 64 * kPieceLaneChains * 8 + 8;     // a round's pieces of 8, from an 8-aligned start
 struct PieceGeom {
     uint32_t gs;          // segments per group (<= kPieceMaxGroup)
     uint32_t rcap;        // piece records per segment (multiple of 16)
     uint32_t slot_words;  // payload staging words (multiple of 4)
     uint32_t wave_words;
 };
-// slot + output buffer (+ 64 per-lane dummy slots; none when HZ_PIECE_DIRECT) + the group's segment
-// table (3 u32 per segment) + its piece starts (u16, 2 KiB)
+// payload slot + the group's segment table (3 u32 per segment) + its piece starts (u16, 2 KiB)
 __host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
-    return slot_words + (HZ_PIECE_DIRECT ? 0u : (kPieceObufSyms + 64) / 2) + ((3 * kPieceMaxGroup + 3) & ~3u) + 512u;
+    return slot_words + ((3 * kPieceMaxGroup + 3) & ~3u) + 512u;
 }
 // avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
 // over the expected count of a segment (a segment past it sets error flag 64: the caller

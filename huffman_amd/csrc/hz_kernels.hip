@@ -210,16 +210,11 @@ HZ_DEV void hist_one(uint32_t* lds, unsigned long long* hist, uint32_t s, Rec re
 
 // The 8 symbols of a 16-byte vector: 8 LDS atomics; a fix-up is due exactly when the
 // incremented half was 0xffff (the half a symbol counts in is its bit 0, the shift 16 * bit 0).
-// HZ_HIST_PK: hist_word of both symbols of a dword at once (packed 16-bit shifts and multiply),
-// byte addresses from the table at LDS byte 0.
-#ifndef HZ_HIST_PK
-#define HZ_HIST_PK 1
-#endif
+// hist_word of both symbols of a dword at once (packed 16-bit shifts and multiply).
 template <typename Rec = NoRec>
 HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v, Rec rec = Rec()) {
     const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
     uint32_t old[8], sh[8];
-#if HZ_HIST_PK
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const hz_u16x2 w = __builtin_bit_cast(hz_u16x2, wd[j]);
@@ -230,14 +225,6 @@ HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v,
         old[2 * j] = atomicAdd(&lds[a & 0x7fffu], 1u << sh[2 * j]);
         old[2 * j + 1] = atomicAdd(&lds[a >> 16], 1u << sh[2 * j + 1]);
     }
-#else
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t s = (wd[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        sh[k] = (s << 4) & 16u;
-        old[k] = atomicAdd(&lds[hist_word(s)], 1u << sh[k]);
-    }
-#endif
     bool any = false;
 #pragma unroll
     for (int k = 0; k < 8; ++k) any |= __builtin_amdgcn_ubfe(old[k], sh[k], 16) == 0xffffu;
@@ -471,22 +458,13 @@ struct PackIn {
     uint64_t bstart;
 };
 
-#ifndef HZ_PACK_NTLOAD
-#define HZ_PACK_NTLOAD 0
-#endif
 HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
     const uint64_t ls = sym0 + kSPT <= a.nsym ? sym0 : 0;
     const uint4* p = reinterpret_cast<const uint4*>(a.in + 2 * ls);
 #pragma unroll
     for (int q = 0; q < kSPT / 8; ++q) {
-#if HZ_PACK_NTLOAD
-        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-        const u32x4v t = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p + q));  // streaming input:
-        const uint4 v = make_uint4(t.x, t.y, t.z, t.w);  // keep L2 for the escape table
-#else
         const uint4 v = p[q];
-#endif
         x.raw[4 * q] = v.x; x.raw[4 * q + 1] = v.y; x.raw[4 * q + 2] = v.z; x.raw[4 * q + 3] = v.w;
     }
     const uint64_t ps = blk ? blk * kBlockSyms - 32 + (uint64_t)(lane & 31) : 0;
@@ -1911,9 +1889,6 @@ HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
 // exactly kStageUnroll loads per lane (static vmcnt for the pipelined waits):
 // chunks past the window or the payload read a clamped address and are fixed
 // up in registers. Requires nwords >= 4 (host check).
-#ifndef HZ_DEC_NTLOAD
-#define HZ_DEC_NTLOAD 0  // 1: staging loads non-temporal (keep L2 for the global LUT level)
-#endif
 HZ_DEV void dec_stage_prefetch(const DecArgs& a, const PipeMeta& m, int lane, uint4 (&v)[kStageUnroll]) {
     const uint64_t w0 = (((m.b0 + a.bit_adj) >> 5) & ~3ull) - 4;
 #pragma unroll
@@ -1921,13 +1896,7 @@ HZ_DEV void dec_stage_prefetch(const DecArgs& a, const PipeMeta& m, int lane, ui
         const uint64_t w = w0 + 4ull * ((uint32_t)lane + (uint32_t)u * kWave);
         const bool in = w < a.nwords;  // also false for a window that wrapped below word 0
         const uint64_t wl = !in ? 0 : (w + 4 <= a.nwords ? w : a.nwords - 4);
-#if HZ_DEC_NTLOAD
-        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-        const u32x4v t = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(a.words + wl));
-        v[u] = make_uint4(t.x, t.y, t.z, t.w);
-#else
         v[u] = *reinterpret_cast<const uint4*>(a.words + wl);
-#endif
     }
 }
 
@@ -3386,34 +3355,6 @@ HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
     return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
 }
 
-// HZ_SEG_REGWIN (k_seg_walk): the window kept in registers -- two ring words at a funnel shift,
-// the next word read one step ahead -- so a step's critical path holds one LDS read (the length
-// table) instead of two. Valid for codes of <= 32 bits (the walker's <= 22).
-#ifndef HZ_SEG_REGWIN
-#define HZ_SEG_REGWIN 0
-#endif
-struct SegWin {
-    uint32_t w0, w1, sh, wn, nxt;
-    HZ_DEV void init(const uint32_t* ring, uint32_t p) {
-        const uint32_t q0 = (p - 1) >> 5;
-        w0 = ring[q0 & 15u];
-        w1 = ring[(q0 + 1) & 15u];
-        sh = (0u - p) & 31u;
-        wn = q0 + 2;
-    }
-    HZ_DEV uint32_t window() const { return __builtin_amdgcn_alignbit(w0, w1, sh); }
-    HZ_DEV void reload(const uint32_t* ring) { nxt = ring[wn & 15u]; }  // after the ring's refill
-    HZ_DEV void step(const uint32_t* ring, uint32_t L) {  // L <= 32
-        const int32_t r = (int32_t)sh - (int32_t)L;
-        const bool cr = r < 0;
-        w0 = cr ? w1 : w0;
-        w1 = cr ? nxt : w1;
-        sh = (uint32_t)(cr ? r + 32 : r);
-        wn += cr ? 1u : 0u;
-        nxt = ring[wn & 15u];
-    }
-};
-
 // Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
@@ -3499,9 +3440,6 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 7
     // codewords), held in rfl / roff until the half-round's end, then written to the lane's
     // 16-byte LDS record buffer (after the rings) and stored 8 records at a time.
-#ifndef HZ_EXP_REC
-#define HZ_EXP_REC 1  // timing builds only: 0 = no records (the decode is then wrong)
-#endif
     // A record is the distance in bits from the previous one (from the segment's entry for the
     // first): at most 8 codes of <= 22 bits, so one byte (the decoder rebuilds the offsets by a scan).
     constexpr uint32_t RG = 16;
@@ -3529,7 +3467,7 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     // after a codeword: its end p is the start of the segment's codeword cc; every 8th is a record
     // (one the crossing below turns into the next segment's entry is dropped there)
     auto note = [&](bool adv) {
-        const bool rn = HZ_EXP_REC & adv & ((cc & 7u) == 0u);
+        const bool rn = adv & ((cc & 7u) == 0u);
         roff = rn ? p : roff;
         rfl |= rn;
     };
@@ -3560,26 +3498,15 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     cross();  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
-#if HZ_SEG_REGWIN
-    SegWin wv;
-    wv.init(ring, p);
-#endif
     for (;;) {
         if (!__any(p < end)) break;
         const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
-#if HZ_SEG_REGWIN
-        wv.reload(ring);
-#endif
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
             for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (p < lim);
-#if HZ_SEG_REGWIN
-                const uint32_t W = wv.window();
-#else
                 const uint32_t W = seg_window(ring, p);
-#endif
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
                 HZ_WALK_FENCE();
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
@@ -3587,9 +3514,6 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
                 const uint32_t L = adv ? e + bias : 0u;
                 cc += adv ? 1u : 0u;
                 p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
                 pk |= park;
                 pW = park ? W : pW;
                 note(adv);
@@ -3599,9 +3523,6 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
             if (pk) {
                 const uint32_t L = a.esc[pW >> (32 - a.m)];
                 p += L;
-#if HZ_SEG_REGWIN
-                wv.step(ring, L);
-#endif
                 ++cc;
                 pk = false;
                 note(true);
@@ -3678,11 +3599,7 @@ constexpr int kPieceGrp = kPieceChains == 8 ? 4 : 2;  // chains walked together:
 constexpr int kPieceNG = kPieceChains / kPieceGrp;     // groups of them per round (2 or 3)
 static_assert(kPieceChains == 4 || kPieceChains == 6 || kPieceChains == 8, "two or three pairs, or two quads");
 constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
-static_assert(kPieceRound * kPieceSyms + 8 == kPieceObufSyms, "hz_internal.h output buffer");
 constexpr int kPieceWaves = HZ_PIECE_WAVES;
-#ifndef HZ_PIECE_EARLY
-#define HZ_PIECE_EARLY 0  // 1: the next group's loads issued at this group's start (their VGPRs live throughout)
-#endif
 static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
 
 
@@ -3731,17 +3648,13 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
     const uint32_t wid = wave_id();
     const uint32_t wave_words = piece_wave_words(y.slot_words);
     uint32_t* stg = lds + d.lds_words + wid * wave_words;
-    uint16_t* obuf = reinterpret_cast<uint16_t*>(stg + y.slot_words);  // 16-byte aligned (slot_words % 4 == 0)
-    uint32_t* sinfo = reinterpret_cast<uint32_t*>(obuf + (HZ_PIECE_DIRECT ? 0u : kPieceObufSyms + 64));  // cnt, entry, F
+    uint32_t* sinfo = stg + y.slot_words;  // per segment: cnt, entry, F (u32)
     uint16_t* rlds = reinterpret_cast<uint16_t*>(sinfo + ((3 * kPieceMaxGroup + 3) & ~3u));  // piece starts (from b0)
     const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
     const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
     const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
     const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
-#if !HZ_PIECE_DIRECT
-    const uint32_t dummy = kPieceObufSyms + (uint32_t)lane;  // the lane's slot for symbols nobody keeps
-#endif
     uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
     PieceIn cur, nxt;
     if (g < ngroups) piece_prefetch(d, y, g, lane, cur);
@@ -3802,16 +3715,12 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
         m.b1 = b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
         m.sub = 0;
         uint64_t w0;
-        __builtin_amdgcn_wave_barrier();  // the previous round's output copy has read the buffer
+        __builtin_amdgcn_wave_barrier();  // the previous group's steps have read the slot
         dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, cur.sv, w0);
         const uint32_t base = top * 32u - (uint32_t)(b0 + d.bit_adj - (w0 << 5));
         __builtin_amdgcn_wave_barrier();
-#if HZ_PIECE_EARLY
-        piece_prefetch(d, y, g + gstride, lane, nxt);  // the next group's loads, a whole group ahead
-#endif
         for (uint32_t r0 = 0; r0 < T; r0 += kPieceRound) {
-            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], st0[kPieceChains];
-            int32_t R0 = 0;  // the round's output run starts at F0 + R0, rounded down to 8 (from F0)
+            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], st0[kPieceChains];  // ob: from F0
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
                 const uint32_t q = r0 + 64u * (uint32_t)c + (uint32_t)lane;
@@ -3826,12 +3735,11 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 const bool valid = q < T;
                 const uint32_t i = valid ? q - qs : 0;
                 const uint32_t o = fs + kPieceSyms * i;  // from F0
-                if (c == 0) R0 = (int32_t)((readlane(o, 0) + (uint32_t)(F0 & 7)) & ~7u) - (int32_t)(F0 & 7);
                 uint32_t n = valid ? cs - kPieceSyms * i : 0;
                 n = n < kPieceSyms ? n : kPieceSyms;
                 n = o < lim ? (lim - o < n ? lim - o : n) : 0;
                 cn[c] = n;
-                ob[c] = (uint32_t)((int32_t)o - R0);
+                ob[c] = o;
                 // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
                 // segment's first bit, prefetched with the group into LDS)
                 const uint32_t rv = rlds[sg * y.rcap + (i ? i - 1 : 0)];
@@ -3846,7 +3754,6 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
 #pragma unroll
                 for (int u = 0; u < kPieceGrp; ++u) gv[c + u] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + u].gi, 0, 0);
             };
-#if HZ_PIECE_DIRECT
             // symbols packed in registers (an even step keeps the entry, the odd one packs both symbols,
             // leaf bytes 1-2, by one v_perm); a whole piece leaves as one 16-byte store at its place
             uint32_t pk[kPieceChains][kPieceSyms / 2];
@@ -3856,15 +3763,6 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                 if (t & 1) pk[c][t >> 1] = __builtin_amdgcn_perm(ee, pk[c][t >> 1], 0x06050201u);
                 else pk[c][t >> 1] = ee;
             };
-#else
-            // a symbol goes to the round's output buffer at its place (a piece's steps past its count to
-            // the lane's dummy slot)
-            auto finish = [&](int c, uint32_t t) {
-                const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : gv[c];
-                p1[c] -= lut_leaf_len(ee);
-                obuf[t < cn[c] ? ob[c] + t : dummy] = (uint16_t)lut_leaf_sym(ee);
-            };
-#endif
             // each group's gathers are consumed after the next group's walk has been issued
             issueh(0);
 #pragma unroll
@@ -3879,14 +3777,13 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
 #pragma unroll
                 for (int u = (kPieceNG - 1) * kPieceGrp; u < kPieceChains; ++u) finish(u, t);
             }
-#if HZ_PIECE_DIRECT
             // whole pieces: 16 bytes at output symbol F0 + o (2-byte aligned: the hardware takes unaligned
             // global stores; a lane's neighbours write the adjacent 16 bytes, so a store instruction covers
             // about 1 KiB); short pieces (a segment's last, the stream's end) symbol by symbol, so they
             // never touch the next piece's symbols
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
-                const uint64_t o = F0 + (uint64_t)(int64_t)((int32_t)ob[c] + R0);
+                const uint64_t o = F0 + ob[c];
                 if (cn[c] == kPieceSyms) {
                     *reinterpret_cast<u32x4a2*>(out16 + o) = u32x4a2{pk[c][0], pk[c][1], pk[c][2], pk[c][3]};
                 } else {
@@ -3898,11 +3795,10 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                     }
                 }
             }
-#endif
             // the stream's last codeword: its chain is decoded again, alone, for its end bit
 #pragma unroll
             for (int c = 0; c < kPieceChains; ++c) {
-                const bool is_end = cn[c] > 0 && (uint32_t)((int32_t)ob[c] + R0) + cn[c] == lim && lim == y.nsym - F0;
+                const bool is_end = cn[c] > 0 && ob[c] + cn[c] == lim && lim == y.nsym - F0;
                 if (__builtin_expect(is_end, 0)) {
                     uint32_t pp = base - st0[c];
                     for (uint32_t t = 0; t < cn[c]; ++t) {
@@ -3914,36 +3810,10 @@ __global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, Pi
                     *y.end = b0 + (uint64_t)(base - pp);
                 }
             }
-#if !HZ_PIECE_DIRECT
-            __builtin_amdgcn_wave_barrier();
-            // the round's run [Ra, Rb) (clamped to the stream): 16-byte stores of whole aligned groups
-            // of 8, single symbols at the two ends (the neighbouring runs own the rest); offsets from
-            // obuf slot 0 = output symbol Rz (a multiple of 8)
-            const uint32_t rl = (T - r0 < kPieceRound ? T - r0 : kPieceRound) - 1;  // the round's last piece
-            uint32_t obl = ob[0], cnl = cn[0];
-#pragma unroll
-            for (int c = 1; c < kPieceChains; ++c) {
-                obl = (rl >> 6) == (uint32_t)c ? ob[c] : obl;
-                cnl = (rl >> 6) == (uint32_t)c ? cn[c] : cnl;
-            }
-            const uint32_t a0 = readlane(ob[0], 0);
-            uint32_t b1 = readlane(obl, (int)(rl & 63)) + readlane(cnl, (int)(rl & 63));
-            b1 = b1 > a0 ? b1 : a0;
-            const uint32_t h1 = ((a0 + 7) & ~7u) < b1 ? ((a0 + 7) & ~7u) : b1;  // the first whole group
-            const uint32_t t0 = (b1 & ~7u) > h1 ? (b1 & ~7u) : h1;              // past the last one
-            uint16_t* orun = out16 + F0 + (uint64_t)(int64_t)R0;                   // output symbol Rz
-            if ((uint32_t)lane < h1 - a0) orun[a0 + lane] = obuf[a0 + lane];
-            uint4* o4 = reinterpret_cast<uint4*>(orun);
-            const uint4* b4 = reinterpret_cast<const uint4*>(obuf);
-            for (uint32_t cg = h1 / 8 + (uint32_t)lane; cg < t0 / 8; cg += 64) o4[cg] = b4[cg];
-            if ((uint32_t)lane < b1 - t0) orun[t0 + lane] = obuf[t0 + lane];
-#endif
         }
-#if !HZ_PIECE_EARLY
         // the next group's records and staging chunks (after the last round: their VGPRs beside the
         // chains' spill at 1024 threads)
         piece_prefetch(d, y, g + gstride, lane, nxt);
-#endif
         cur = nxt;
     }
 }
