@@ -132,3 +132,16 @@ def test_indexless_dense_run_takes_the_index_path(codec):
     # and the device context is clean afterwards (the overflow flag was cleared)
     ok2, end_ok2 = _check(codec, x, shift=3)
     assert ok2 and end_ok2
+
+
+def test_indexless_skewed_rounds(codec):
+    """90 % of the symbols one value (a 1-bit code): ~2 bits per codeword, ~250 pieces per 4096-bit
+    segment, so a decode group is one segment taking two rounds of 256 pieces, with records up to the
+    segment's last 8th codeword (hundreds per row). The output and end bit are exact."""
+    import torch
+    rng = np.random.default_rng(5)
+    nsym = (6 << 20) + 3
+    sym = np.where(rng.random(nsym) < 0.9, 0, rng.integers(1, 301, nsym)).astype("<u2")
+    x = torch.from_numpy(sym.view(np.uint8).copy()).cuda()
+    ok, end_ok = _check(codec, x)
+    assert ok and end_ok
