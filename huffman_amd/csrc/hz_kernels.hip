@@ -3414,6 +3414,15 @@ HZ_DEV void seg_feed(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint32_t p)
     }
 }
 
+// steps per round of the segment walk: two halves of 7 steps, so a half-round (plus its escape
+// gather) moves at most 8 codewords and takes at most one piece record. Zipf 16 GiB walk:
+// 10 / 12 / 14 steps 14.4 / 13.9 / 13.4 ms (A/B in one run, r04f); 3 parts of 6 steps 14.4 ms;
+// a second chunk fed per round (when no group load is pending) 15.2 ms
+#ifndef HZ_SEG_STEPS
+#define HZ_SEG_STEPS 14
+#endif
+constexpr int kSegSteps = HZ_SEG_STEPS;
+static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
 __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, SegArgs y) {
     // the length table at LDS address 0 (k_idx_walk's layout), the rings after it
     __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 8];
@@ -3437,7 +3446,7 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     uint32_t nb = p + (uint32_t)(cs - x0);         // the next segment start to cross
     uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
     uint32_t cc = 0;                               // codewords since the last crossing
-    // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 7
+    // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 8
     // codewords), held in rfl / roff until the half-round's end, then written to the lane's
     // 16-byte LDS record buffer (after the rings) and stored 8 records at a time.
     // A record is the distance in bits from the previous one (from the segment's entry for the
@@ -3504,7 +3513,7 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
 #pragma unroll
-            for (int t = 0; t < kWalkSteps / kWalkHalves; ++t) {
+            for (int t = 0; t < kSegSteps / kWalkHalves; ++t) {
                 const bool ok = !pk & (p < lim);
                 const uint32_t W = seg_window(ring, p);
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
