@@ -2619,8 +2619,12 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // (ent/dirty): k_sync_iter checks it against the bitmap, which lands at once
 // when the lead-in resynchronised.
 // ---------------------------------------------------------------------------
-// steps per round: u8 table 8: 25.5 ms, 10: 25.3 ms; 4-bit table 10/12/14: 24.7/24.4/24.6 ms
-constexpr int kWalkSteps = 12;
+// steps per round: u8 table 8: 25.5 ms, 10: 25.3 ms; 4-bit table 10/12/14: 24.7/24.4/24.6 ms;
+// round 4 (16 GiB Zipf, A/B in one run, k_idx_walk alone): 12 / 14 / 16 steps 17.32 / 17.11 / 17.44 ms
+#ifndef HZ_WALK_STEPS
+#define HZ_WALK_STEPS 14
+#endif
+constexpr int kWalkSteps = HZ_WALK_STEPS;
 // parked chains resume after each part of a round: 2 parts of 6 steps 23.6-23.9 ms, 1 part
 // 23.7-24.3, 2 x 8 23.4-23.9, 3 x 6 23.2-24.3, 3 x 4 24.8, 4 x 4 23.5-24.2 (A/B in one run);
 // round 3 (2.3 % escapes): 2 / 1 / 3 parts 22.1 / 22.1-22.3 / 23.4 ms
