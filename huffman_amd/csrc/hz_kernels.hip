@@ -3451,20 +3451,18 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
     uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
     uint32_t cc = 0;                               // codewords since the last crossing
     // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 8
-    // codewords), held in rfl / roff until the half-round's end, then written to the lane's
-    // 16-byte LDS record buffer (after the rings) and stored 8 records at a time.
+    // codewords), found at the half-round's end, written to the lane's 16-byte LDS record buffer
+    // (after the rings) and stored 16 records at a time.
     // A record is the distance in bits from the previous one (from the segment's entry for the
     // first): at most 8 codes of <= 22 bits, so one byte (the decoder rebuilds the offsets by a scan).
     constexpr uint32_t RG = 16;
     uint8_t* rbuf = reinterpret_cast<uint8_t*>(lds + kSegWalkWaves * 64 * kSegRing) + 16 * threadIdx.x;
-    uint32_t rj = 0, roff = 0, rprev = 0;
-    bool rfl = false;
-    // roff: the ring position of the pending record; rprev: the previous record's (or the entry's)
-    auto rec_put = [&]() {
+    uint32_t rj = 0, rprev = 0;
+    // roff: the ring position of a record; rprev: the previous record's (or the entry's)
+    auto rec_put = [&](uint32_t roff) {
         rbuf[rj & (RG - 1)] = (uint8_t)(roff - rprev);
         rprev = roff;
         ++rj;
-        rfl = false;
     };
     // segment sj - 1's record row, count and (segment sj's) entry: pointers advanced at each crossing
     uint8_t* rrow = y.rec + seg0 * y.rcap;
@@ -3477,38 +3475,24 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
         else
             atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
     };
-    // after a codeword: its end p is the start of the segment's codeword cc; every 8th is a record
-    // (one the crossing below turns into the next segment's entry is dropped there)
-    auto note = [&](bool adv) {
-        const bool rn = adv & ((cc & 7u) == 0u);
-        roff = rn ? p : roff;
-        rfl |= rn;
-    };
-    // p moved past nb: p is the first codeword start of segment sj (or the chain's exit)
     bool more = live;  // sj <= seg1 for a live chain: crossings still to record
-    auto cross = [&]() {
-        if (__builtin_expect(p >= nb, 0) && more) {
-            if (rfl && roff < nb) {  // a record inside the segment (not its successor's entry)
-                rec_put();
-                if ((rj & (RG - 1)) == 0u) rec_store();
-            }
-            rfl = false;
-            if (sj > seg0) {
-                *cntp++ = cc;
-                if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
-                rrow += y.rcap;
-            }
-            *(sj < seg1 ? entp : y.xit + ch) = abs0 + p;
-            ++entp;
-            cc = 0;
-            rj = 0;
-            rprev = p;  // the new segment's entry
-            ++sj;
-            more = sj <= seg1;
-            nb += kSegBits;
+    // Past nb (the half's codeword jx ends at px >= nb): segment sj - 1 ends with codeword jx (its
+    // count), px is segment sj's entry (or the chain's exit)
+    auto cross = [&](uint32_t px, uint32_t count) {
+        if (sj > seg0) {
+            *cntp++ = count;
+            if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
+            rrow += y.rcap;
         }
+        *(sj < seg1 ? entp : y.xit + ch) = abs0 + px;
+        ++entp;
+        rj = 0;
+        rprev = px;  // the new segment's entry
+        ++sj;
+        more = sj <= seg1;
+        nb += kSegBits;
     };
-    cross();  // a chain at the stream's start begins on its first segment's entry
+    if (more && p >= nb) cross(p, 0);  // a chain at the stream's start begins on its first segment's entry
     bool pk = false;
     uint32_t pW = 0;
     for (;;) {
@@ -3516,8 +3500,14 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
         const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
+            // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
+            // that parks or reaches lim stays put for the rest of the half), then at p for an escape;
+            // crossings and records are resolved once, at the half's end (at most one of each)
+            constexpr int S = kSegSteps / kWalkHalves;
+            uint32_t q[S];
+            uint32_t na = 0;
 #pragma unroll
-            for (int t = 0; t < kSegSteps / kWalkHalves; ++t) {
+            for (int t = 0; t < S; ++t) {
                 const bool ok = !pk & (p < lim);
                 const uint32_t W = seg_window(ring, p);
                 uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
@@ -3525,25 +3515,42 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
                 e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
                 const uint32_t L = adv ? e + bias : 0u;
-                cc += adv ? 1u : 0u;
+                na += adv ? 1u : 0u;
                 p += L;
                 pk |= park;
                 pW = park ? W : pW;
-                note(adv);
-                cross();
+                q[t] = p;
             }
-            // parked chains (codes longer than the table's k bits): one gather from the escape table
+            const uint32_t m = na + (pk ? 1u : 0u);
             if (pk) {
-                const uint32_t L = a.esc[pW >> (32 - a.m)];
-                p += L;
-                ++cc;
+                p += a.esc[pW >> (32 - a.m)];
                 pk = false;
-                note(true);
-                cross();
             }
-            if (rfl) {
-                rec_put();
-                if ((rj & (RG - 1)) == 0u) rec_store();
+            // the end of the half's codeword j (1-based, j <= m)
+            auto pos = [&](uint32_t j) {
+                const uint32_t jj = j <= na ? j : 0u;
+                uint32_t r = p;
+#pragma unroll
+                for (int t = 0; t < S; ++t) r = jj == (uint32_t)t + 1u ? q[t] : r;
+                return r;
+            };
+            const uint32_t j1 = 8u - (cc & 7u);  // the codeword that is a multiple of 8 in the segment
+            if (__builtin_expect(more && p >= nb, 0)) {
+                uint32_t jx = 1;  // the crossing codeword: the first that ends at or past nb
+#pragma unroll
+                for (int t = 0; t < S; ++t) jx += ((uint32_t)t < na && q[t] < nb) ? 1u : 0u;
+                if (j1 < jx) {  // a record inside the segment (not its successor's entry)
+                    rec_put(pos(j1));
+                    if ((rj & (RG - 1)) == 0u) rec_store();
+                }
+                cross(pos(jx), cc + jx);
+                cc = m - jx;  // < 8: no record of the new segment in this half
+            } else {
+                if (j1 <= m) {
+                    rec_put(pos(j1));
+                    if ((rj & (RG - 1)) == 0u) rec_store();
+                }
+                cc += m;
             }
         }
         seg_feed(a, ring, fd, p);
