@@ -239,7 +239,7 @@ def main():
 
     state = {}
 
-    def step():
+    def step(dropin=False):
         codec.histogram(x)
         if world > 1:
             hist_local.copy_(codec.hist)
@@ -257,9 +257,13 @@ def main():
                                last_byte=last, cb=cb)
         if "payload" not in state or state["payload"].numel() < plan.words * 4 + 16:
             state["payload"], state["index"] = codec.alloc_payload(plan, nsym)
-        codec.pack(x, plan, state["payload"], state["index"])
+        codec.pack(x, plan, state["payload"], None if dropin else state["index"])
         codec.upload_decode(plan)  # host builds the decode tables while pack runs
-        codec.decode(state["payload"], nsym, state["index"], out)
+        if dropin:
+            codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit, nsym,
+                                       out.data_ptr(), endb.data_ptr())
+        else:
+            codec.decode(state["payload"], nsym, state["index"], out)
         state["header"] = plan.header  # the .compressed header, written on the host while the GPU runs
         state["plan"] = plan
 
@@ -296,38 +300,61 @@ def main():
         return codec.make_plan(h, n_total, hist_local=hs[rank], first_shard=(rank == 0), shard_bit_offset=offset,
                                last_byte=0, cb=cb)  # N is even for every shard here
 
-    def run(steps):
+    def run(steps, dropin=False):
+        """dropin=False: pack writes its block index beside the payload and decode reads it (the
+        sidecar-index figure). dropin=True: what the reference's file path does, on the device --
+        pack writes NO index (a .compressed payload carries none, Compressor.cu:427-601) and the
+        decode is hz_decode_indexless of the bare payload (the `extract` path)."""
         hist_launch()
         plan = hist_plan()
         for i in range(steps):
             if "payload" not in state or state["payload"].numel() < plan.words * 4 + 16:
                 state["payload"], state["index"] = codec.alloc_payload(plan, nsym)
-            codec.pack(x, plan, state["payload"], state["index"])
+            codec.pack(x, plan, state["payload"], None if dropin else state["index"])
             if i + 1 < steps:
                 hist_launch()  # the next batch's histogram, between this batch's pack and decode
             codec.upload_decode(plan)  # host builds the decode tables while pack runs
-            codec.decode(state["payload"], nsym, state["index"], out)
+            if dropin:
+                codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit,
+                                           nsym, out.data_ptr(), endb.data_ptr())
+            else:
+                codec.decode(state["payload"], nsym, state["index"], out)
             state["header"] = plan.header  # the .compressed header, written on the host while the GPU runs
             state["plan"] = plan
             if i + 1 < steps:
                 plan = hist_plan()  # while this batch decodes
+
+    def timed(steps, dropin=False):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(steps, dropin)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    endb = torch.zeros(2, dtype=torch.int64, device=dev)
 
     log(f"rank {rank}: {N} bytes generated; {args.warmup} warmup steps")
     if args.warmup:
         run(args.warmup)
     codec.sync()
     log(f"rank {rank}: {args.steps} timed steps")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(args.steps)
     codec.sync()  # surfaces device-side errors (capacity, format)
     ok = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    # the drop-in file path, timed the same way: pack without an index, index-less decode
+    log(f"rank {rank}: drop-in path (no index): {args.warmup} warmup + {args.steps} timed steps")
+    out.fill_(0)
+    if args.warmup:
+        run(args.warmup, dropin=True)
+    codec.sync()
+    elapsed_dropin = timed(args.steps, dropin=True)
+    codec.sync()
+    ok_dropin = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    ok = ok and ok_dropin
     # Kernel times (HIP events) and host stage costs: two more steps, serialised, untimed.
     kms = {"hist": [], "pack": [], "decode": []}
     host_ms = []
@@ -340,6 +367,20 @@ def main():
         host_ms.append(codec.timings.get("codebook_ms", 0) + codec.timings.get("upload_ms", 0))
         host_dec_ms.append(codec.timings.get("upload_decode_ms", 0))
     ok = ok and bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    # the drop-in step's kernels (pack without an index; the index-less decode), serialised, untimed
+    from huffman_amd._lib import STAGE_EXTRACT
+    dk = {"hist": [], "pack": [], "extract": []}
+    for _ in range(2):
+        out.fill_(0)
+        step(dropin=True)
+        torch.cuda.synchronize()
+        km = codec.kernel_ms()
+        dk["hist"].append(km["hist"])
+        dk["pack"].append(km["pack"])
+        dk["extract"].append(codec.dev.kernel_ms(STAGE_EXTRACT))
+    ok = ok and bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    step()  # payload and index of the sidecar-index path again, for the checks below
+    torch.cuda.synchronize()
     plan = state["plan"]
     log(f"rank {rank}: {elapsed * 1e3 / args.steps:.3f} ms/step; index rebuild from the payload")
     # Index-less decode path (reference-produced files): rebuild the block index
@@ -354,10 +395,8 @@ def main():
     index_build = {"ms": round(codec.dev.kernel_ms(STAGE_INDEX), 3),
                    "matches_pack_index": bool(torch.equal(rebuilt[:nidx], state["index"][:nidx]))}
     del rebuilt
-    # `extract` of an index-less file on the device: hz_decode_indexless (no block index; two long-chain
-    # passes), its output checked against the input, its end bit against pack's index
-    from huffman_amd._lib import STAGE_EXTRACT
-    endb = torch.zeros(2, dtype=torch.int64, device=dev)
+    # `extract` of an index-less file on the device: hz_decode_indexless (no block index; chain walk,
+    # fix-ups, chain-block decode), its output checked against the input, its end bit against pack's index
     xms = []
     for _ in range(2):
         out.fill_(0)
@@ -375,12 +414,13 @@ def main():
         reassembly = reassemble(codec, plan, state["payload"], rank, world, n_total, kind, args, dev)
     C = plan.payload_bits // 8
     if world > 1:
-        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, elapsed_dropin, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
         all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, bad = float(t[0]), float(t[1])
+        elapsed, elapsed_dropin, bad = float(t[0]), float(t[1]), float(t[2])
         ok = bad == 0.0
     ms_step = elapsed / args.steps * 1e3
     value = n_total / (ms_step / 1e3) / 1e9
+    ms_dropin = elapsed_dropin / args.steps * 1e3
 
     if rank == 0:
         avg = {k: float(np.mean(v)) for k, v in kms.items()}
@@ -443,6 +483,32 @@ def main():
             "roundtrip_bit_exact": ok,
             "index_build_from_payload": index_build,
             "extract_indexless": extract,
+            # the drop-in file path timed like the headline (same --steps / --warmup, same clock): pack
+            # writes no block index (a .compressed payload has none) and the decode is the index-less
+            # extract of the bare payload
+            "dropin": {
+                "schedule": "pipelined like the headline: hist16_ranges -> host codebook -> pack_ranges "
+                            "(no index) -> hz_decode_indexless; the next batch's histogram between pack "
+                            "and decode",
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(ms_dropin, 3),
+                "value": round(n_total / (ms_dropin / 1e3) / 1e9, 2),
+                "unit": "GB/s",
+                "roundtrip_bit_exact": ok_dropin,
+                "kernel_ms": {k: round(float(np.mean(v)), 4) for k, v in dk.items()},
+                "roofline": {
+                    "kernel": "extract",
+                    "bound": "hbm",
+                    "achieved": round((C + 2 * nsym) / (float(np.mean(dk["extract"])) / 1e3) / 1e9, 1),
+                    "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s",
+                    "frac": round((C + 2 * nsym) / (float(np.mean(dk["extract"])) / 1e3) / 1e9 / HBM_PEAK_GBPS,
+                                  4),
+                    "traffic": pmc_traffic("extract"),
+                    "algorithmic_bytes_per_launch": C + 2 * nsym,
+                },
+            },
             # algorithmic HBM bytes of one step per GPU: hist N + pack (N + C) + decode (C + N)
             "step_algorithmic_GBps": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9, 1),
             "step_hbm_frac": round((3 * N + 2 * C) / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
@@ -490,7 +556,7 @@ def main():
             # `extract` of an index-less file: the payload read (twice: the length walk and the decode
             # pass) and the output written; algorithmic bytes C + N (payload in, symbols out)
             "extract_roofline": {
-                "kernels": ["seg_walk", "seg_fix", "scan", "piece_decode"],
+                "kernels": ["chain_walk", "chain_fix", "scan", "chain_meta", "chain_decode", "chain_tail"],
                 "bound": "hbm",
                 "ms": extract["ms"],
                 "achieved": round((C + 2 * nsym) / (extract["ms"] / 1e3) / 1e9, 1) if extract["ms"] else None,

@@ -555,8 +555,7 @@ static void add_lds_level(const hz_codebook* cb, std::vector<uint32_t>& img, con
 
 // LUT decode: level 1 (2^K1 u32) for the LDS, deeper levels (u32) for global
 // memory.
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl,
-                  std::vector<uint32_t>* seg_img) {
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl) {
     K1 = std::min<int>((int)cb->max_len, kDecLutMaxK1);
     if (K1 < 1) K1 = 1;
     std::vector<uint32_t> syms;
@@ -585,12 +584,6 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     for (uint32_t s = 0; s < HZ_NSYM; ++s)
         if (cb->len[s]) kbits += ldexp((double)cb->len[s], -(int)cb->len[s]);
     const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
-    if (seg_img) {  // the index-less decoder: heads in what its waves' slots and output buffers leave
-        *seg_img = img;
-        const PieceGeom pg = piece_geom(kbits, (int)cb->max_len);
-        add_lds_level(cb, *seg_img, l2, K1,
-                      (long)(kLdsBytes / 4) - (long)img.size() - (long)kPieceDecWaves * (long)pg.wave_words - 64);
-    }
     add_lds_level(cb, img, l2, K1,
                   (long)(kLdsBytes / 4) - (long)img.size() - (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64);
     return HZ_OK;

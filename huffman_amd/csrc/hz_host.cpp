@@ -36,8 +36,7 @@ std::vector<uint32_t> build_lenpair(const hz_codebook* cb);
 std::vector<uint64_t> build_enc_wide(const hz_codebook* cb);
 int select_dec_mode(const hz_codebook* cb);
 int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
-int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl,
-                  std::vector<uint32_t>* seg_img = nullptr);
+int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl);
 void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
                     int& bias);
 }  // namespace hz
@@ -85,7 +84,7 @@ struct hz_ctx {
     uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
-           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_seg_lds = 0;
+           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0;
     int last_pack_ranges = 0;       // the last hz_pack_ranges call took the range plan
 };
 
@@ -115,7 +114,6 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_len8);
     (void)hipFree(t.d_lenpair);
     (void)hipFree(t.d_dec_lds);
-    (void)hipFree(t.d_seg_lds);
     (void)hipFree(t.d_dec_l2);
     (void)hipFree(t.d_walk_lds);
     (void)hipFree(t.d_walk_esc);
@@ -195,6 +193,16 @@ extern "C" int hz_ctx_sync(hz_ctx* c) {
     return HZ_OK;
 }
 
+// Stage timing events: skipped while the stream is being captured into a graph (the stage calls
+// themselves are stream-ordered and capturable; hz_last_kernel_ms then reports the last eager call).
+static hipError_t stage_event(hz_ctx* c, int stage, int which) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing(c->stream, &st);
+    if (e != hipSuccess) return e;
+    if (st != hipStreamCaptureStatusNone) return hipSuccess;
+    return hipEventRecord(c->ev[stage][which], c->stream);
+}
+
 static int arm_err_check(hz_ctx* c) {
     HZ_TRY(hipMemcpyAsync(c->h_err, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     return HZ_OK;
@@ -211,9 +219,9 @@ extern "C" int hz_hist16(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t* d
     if (!c || !d_hist || (n && !d_in)) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
     if (!accumulate) HZ_TRY(hipMemsetAsync(d_hist, 0, HZ_NSYM * sizeof(uint64_t), c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_HIST, 0));
     HZ_TRY(launch_hist16(d_in, n, reinterpret_cast<unsigned long long*>(d_hist), c->ncu, c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_HIST, 1));
     c->ev_used[HZ_STAGE_HIST] = true;
     return HZ_OK;
 }
@@ -227,10 +235,10 @@ extern "C" int hz_hist16_ranges(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint
     if (!d_ranges || (((uintptr_t)d_in) & 15) || (((uintptr_t)d_ranges) & 15)) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
     if (!accumulate) HZ_TRY(hipMemsetAsync(d_hist, 0, HZ_NSYM * sizeof(uint64_t), c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_HIST, 0));
     HZ_TRY(launch_hist16_ranges(d_in, n, reinterpret_cast<unsigned long long*>(d_hist), d_ranges, c->d_err,
                                 c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_HIST][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_HIST, 1));
     c->ev_used[HZ_STAGE_HIST] = true;
     return arm_err_check(c);
 }
@@ -242,15 +250,6 @@ extern "C" int hz_codebook_build_device(hz_ctx* c, const uint64_t* d_hist, hz_co
     HZ_TRY(launch_codebook(reinterpret_cast<const unsigned long long*>(d_hist), d_cb, c->d_cbws, c->d_err, c->stream));
     return arm_err_check(c);
 }
-
-#ifdef HZ_SEG_DEBUG  // variant builds only: the context's scratch (tools/debug/seg_debug.py)
-extern "C" int hz_debug_scratch(hz_ctx* c, uint64_t* out, uint64_t words) {
-    HZ_TRY(hipStreamSynchronize(c->stream));
-    if (words > c->desc_cap) return HZ_EINVAL;
-    HZ_TRY(hipMemcpy(out, c->d_desc, words * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return HZ_OK;
-}
-#endif
 
 #ifdef HZ_CB_PROF  // variant builds only: k_cb_generate's phase timestamps (tools/debug/cb_prof.py)
 extern "C" int hz_debug_cb_prof(hz_ctx* c, uint64_t* out) {
@@ -384,16 +383,14 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.dec_max_len = (int)cb->max_len;
     t.dec_min_len = (int)cb->min_len;
     const int mode = select_dec_mode(cb);
-    std::vector<uint32_t> dimg, l2, wimg, wesc, simg;
+    std::vector<uint32_t> dimg, l2, wimg, wesc;
     if (mode == DEC_FIXED16) { dimg = build_dec_fixed16(cb); t.dec_k = 16; rc = HZ_OK; }
     else if (mode == DEC_DENSE) rc = build_dec_dense(cb, dimg, t.dec_k);
-    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, t.dec_level_bits, &simg);
+    else rc = build_dec_lut(cb, dimg, l2, t.dec_k, t.dec_level_bits);
     if (rc) return rc;
-    t.seg_lds_bytes = 0;
-    if (!simg.empty()) {
-        if ((rc = stage_copy(c, c->stage_dec, &t.d_seg_lds, &c->cap_seg_lds, simg))) return rc;
-        t.seg_lds_bytes = (uint32_t)(simg.size() * 4);
-    }
+    t.dec_avg_bits = 0.0;  // Kraft estimate of bits per codeword (sizes the index-less decoder's records)
+    for (uint32_t s = 0; s < HZ_NSYM; ++s)
+        if (cb->len[s]) t.dec_avg_bits += ldexp((double)cb->len[s], -(int)cb->len[s]);
     while (dimg.size() % 4) dimg.push_back(0);
     t.dec_lds_bytes = (uint32_t)(dimg.size() * 4);
     if (mode != DEC_FIXED16 && t.dec_lds_bytes + 4 * dec_slot_words_max(t.dec_max_len) > kLdsBytes)
@@ -457,11 +454,11 @@ static int pack_impl(hz_ctx* c, const uint8_t* d_in, uint64_t n, uint64_t start_
     HZ_TRY(hipSetDevice(c->device));
     int rc = ensure_scratch(c, pack_scratch_words(nsym));
     if (rc) return rc;
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_PACK, 0));
     HZ_TRY(launch_pack(c->t, d_in, nsym, start_bit, lead, reinterpret_cast<uint32_t*>(d_out), out_cap / 4, c->d_desc,
                        reinterpret_cast<unsigned long long*>(d_index), c->d_err, c->ncu, c->stream, d_ranges,
                        &c->last_pack_ranges));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_PACK][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_PACK, 1));
     c->ev_used[HZ_STAGE_PACK] = true;
     return arm_err_check(c);
 }
@@ -487,10 +484,10 @@ extern "C" int hz_decode(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_b
     if (!d_payload || !d_index || !d_out || (((uintptr_t)d_out) & 15)) return HZ_EINVAL;
     if (c->t.dec_mode < 0) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_DECODE][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_DECODE, 0));
     HZ_TRY(launch_decode(c->t, d_payload, payload_bytes, nsym, reinterpret_cast<const unsigned long long*>(d_index),
                          d_out, c->d_err, c->ncu, c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_DECODE][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_DECODE, 1));
     c->ev_used[HZ_STAGE_DECODE] = true;
     return arm_err_check(c);
 }
@@ -507,11 +504,11 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
     int rc = ensure_scratch(c, index_scratch_words(payload_bytes, start_bit));
     if (rc) return rc;
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_INDEX, 0));
     HZ_TRY(launch_index_build(c->t, d_payload, payload_bytes, start_bit, nsym,
                               reinterpret_cast<unsigned long long*>(d_index), c->d_desc, c->d_err, c->h_err + 2,
                               c->ncu, c->stream));
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_INDEX][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_INDEX, 1));
     c->ev_used[HZ_STAGE_INDEX] = true;
     return arm_err_check(c);
 }
@@ -529,7 +526,7 @@ static int hz_decode_indexless_via_index(hz_ctx* c, const uint8_t* d_payload, ui
         HZ_TRY(hipMalloc(&c->d_xidx, ib));
         c->xidx_cap = ib;
     }
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
     int rc = hz_index_build(c, d_payload, payload_bytes, start_bit, nsym, (uint64_t*)c->d_xidx);
     if (rc) return rc;
     const uint64_t* end = (const uint64_t*)c->d_xidx + index_blocks(nsym);
@@ -540,7 +537,7 @@ static int hz_decode_indexless_via_index(hz_ctx* c, const uint8_t* d_payload, ui
     if ((rc = hz_ctx_sync(c))) return rc;
     if (eb > payload_bytes * 8) return HZ_OK;  // the caller sees the end bit past the payload
     if ((rc = hz_decode(c, d_payload, payload_bytes, nsym, (const uint64_t*)c->d_xidx, d_out))) return rc;
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
     c->ev_used[HZ_STAGE_EXTRACT] = true;
     return arm_err_check(c);
 }
@@ -555,21 +552,19 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
     // nsym codewords end within nsym * max_len bits: the rest of a longer buffer is never walked
     const uint64_t reach = (start_bit + nsym * (uint64_t)std::max(c->t.dec_max_len, 1) + 7) / 8 + 8;
     if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
-    // codebooks the piece decoder does not take: block index, then the block decoder
+    // codebooks the chain decoder does not take (DENSE / FIXED16 tables, codes > 22 bits): block
+    // index, then the block decoder
     if (!seg_decode_supported(c->t) || payload_bytes < 16)
         return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
-    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit, nsym, c->t.dec_max_len));
+    // stream-ordered from here: walk, fix-ups, scans, block decode, tails (no host synchronisation
+    // unless the context's scratch has to grow)
+    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit, nsym, c->t, c->ncu));
     if (rc) return rc;
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][0], c->stream));
-    const hipError_t e = launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
-                                                 reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err,
-                                                 c->h_err + 2, c->ncu, c->stream);
-    if (e == hipErrorNotSupported) {  // more pieces in a segment than planned: through the block index
-        (void)hipGetLastError();
-        return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
-    }
-    HZ_TRY(e);
-    HZ_TRY(hipEventRecord(c->ev[HZ_STAGE_EXTRACT][1], c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
+    HZ_TRY(launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
+                                   reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err, c->ncu,
+                                   c->stream));
+    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
     c->ev_used[HZ_STAGE_EXTRACT] = true;
     return arm_err_check(c);
 }

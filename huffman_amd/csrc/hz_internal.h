@@ -129,48 +129,6 @@ __host__ __device__ inline uint32_t lut_leaf_entry(uint32_t L, uint32_t sym) {
 __host__ __device__ inline uint32_t lut_leaf_len(uint32_t e) { return (e >> 24) & 63u; }
 __host__ __device__ inline uint32_t lut_leaf_sym(uint32_t e) { return (e >> 8) & 0xffffu; }
 constexpr int kDecMaxWaves = 16;
-// Index-less decoder (k_piece_decode, hz_kernels.hip): waves per workgroup and the per-wave LDS
-// (a group of segments' payload slot + one round's output buffer). The walk records the start of
-// every 8th codeword of a 4096-bit segment (rcap records per segment); a wave decodes gs segments.
-// HZ_PIECE_CHAINS: pieces per lane per round, walked as pairs (4: two pairs, 6: three pairs) -- each
-// pair's global gathers land behind the other pairs' LDS walks -- or as two quads (8, like k_decode's
-// two blocks per wave)
-#ifndef HZ_PIECE_CHAINS
-#define HZ_PIECE_CHAINS 4
-#endif
-#ifndef HZ_PIECE_WAVES
-#define HZ_PIECE_WAVES (HZ_PIECE_CHAINS == 8 ? 8 : (HZ_PIECE_CHAINS == 6 ? 12 : 16))
-#endif
-constexpr int kPieceDecWaves = HZ_PIECE_WAVES;
-constexpr uint32_t kPieceLaneChains = HZ_PIECE_CHAINS;
-constexpr uint32_t kPieceMaxGroup = HZ_PIECE_CHAINS == 8 ? 16 : 8;  // segments per group
-struct PieceGeom {
-    uint32_t gs;          // segments per group (<= kPieceMaxGroup)
-    uint32_t rcap;        // piece records per segment (multiple of 16)
-    uint32_t slot_words;  // payload staging words (multiple of 4)
-    uint32_t wave_words;
-};
-// payload slot + the group's segment table (3 u32 per segment) + its piece starts (u16, 2 KiB)
-__host__ __device__ inline uint32_t piece_wave_words(uint32_t slot_words) {
-    return slot_words + ((3 * kPieceMaxGroup + 3) & ~3u) + 512u;
-}
-// avg_bits: payload bits per codeword (expected); rcap leaves 30 % + 32 codewords of headroom
-// over the expected count of a segment (a segment past it sets error flag 64: the caller
-// decodes through the block index instead).
-inline PieceGeom piece_geom(double avg_bits, int max_len) {
-    PieceGeom g;
-    const double per_seg = 4096.0 / (avg_bits > 1.0 ? avg_bits : 1.0);  // codewords per segment
-    const double recs = per_seg / 8.0;
-    uint32_t rcap = (uint32_t)((recs * 1.3 + 4.0 + 15.0) / 16.0) * 16u;
-    g.rcap = rcap < 16u ? 16u : (rcap > 1024u ? 1024u : rcap);
-    uint32_t gs = (uint32_t)(0.93 * 64.0 * kPieceLaneChains / (recs + 1.0));  // ~93 % of a round's pieces
-    g.gs = gs < 1u ? 1u : (gs > kPieceMaxGroup ? kPieceMaxGroup : gs);
-    if (g.gs * g.rcap > 1024u) g.gs = 1024u / g.rcap > 0u ? 1024u / g.rcap : 1u;  // a group's records <= 1 KiB
-    g.slot_words = ((g.gs * 128u + ((uint32_t)max_len * 8u + 31u) / 32u + 12u) + 3u) & ~3u;
-    g.wave_words = piece_wave_words(g.slot_words);
-    return g;
-}
-
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
 // beside a 4-bit code-length table of the top kWalkK window bits.
@@ -212,6 +170,7 @@ struct Tables {
     int dec_level_bits = 0;        // LUT: widest global subtable (kDecLevelBits unless reduced to fit kLutMaxL2)
     int dec_max_len = 0;           // of the codebook the decode tables were built for
     int dec_min_len = 0;
+    double dec_avg_bits = 0.0;     // Kraft estimate of bits per codeword of the decode codebook: sum 2^-L * L
     uint32_t enc_lds_bytes = 0;
     double enc_avg_bits = 16.0;    // Kraft estimate of bits per symbol: sum 2^-L * L
     uint32_t dec_lds_bytes = 0;
@@ -222,8 +181,6 @@ struct Tables {
     uint32_t* d_lenpair = nullptr; // range plan: u8 lengths of both symbols of every histogram word (u16 each)
     uint32_t hot_mask = 0x8000;    // HOT pairing: s and s ^ hot_mask share slot
     uint32_t* d_dec_lds = nullptr; // LDS image for the decode kernel
-    uint32_t* d_seg_lds = nullptr; // LUT: the index-less decoder's LDS image (level 1 + the heads beside its waves)
-    uint32_t seg_lds_bytes = 0;
     uint32_t* d_dec_l2 = nullptr;  // deeper LUT levels (shared by both images)
     uint64_t dec_l2_entries = 0;
     uint32_t* d_walk_lds = nullptr; // index walker: 4-bit code length - walk_bias per walk_k-bit window (0 = longer code)
@@ -262,15 +219,13 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
                               unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
                               hipStream_t s);  // synchronises the stream (iterates to a fixed point)
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
-// Index-less decode in two long-chain passes (no block index); d_end: the end bit of codeword nsym - 1.
+// Index-less decode in chain blocks (no block index, stream-ordered: no host synchronisation);
+// d_end: the end bit of codeword nsym - 1 (all ones when the payload holds fewer codewords).
 bool seg_decode_supported(const Tables& t);
 hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                                    uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
-                                   unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
-                                   hipStream_t s);  // synchronises the stream (fix-ups to a fixed point);
-                                                    // hipErrorNotSupported: a segment holds more pieces than
-                                                    // planned (nothing written; decode through the index)
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len);
+                                   unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, const Tables& t, int ncu);
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -7,6 +7,7 @@
 //   k_generate synthetic Zipf / uniform byte streams (this build's generator)
 //
 // Layout, roofline and design notes: DESIGN.md. All integer/bit work; no MFMA.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <mutex>
@@ -1204,14 +1205,15 @@ HZ_DEV uint64_t block_exclusive_scan(uint64_t v, uint64_t* sh, uint64_t& total) 
     return r;
 }
 
+// mask: the bits of each entry that are its count (the pack's block entries: the low 32; chain counts: all)
 __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const unsigned long long* blk, uint64_t nblocks,
-                                                              unsigned long long* tile_sum) {
+                                                              unsigned long long* tile_sum, uint64_t mask) {
     __shared__ uint64_t sh[17];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
     uint64_t s = 0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k)
-        if (base + k < nblocks) s += (uint32_t)blk[base + k];
+        if (base + k < nblocks) s += blk[base + k] & mask;
     uint64_t total;
     block_exclusive_scan(s, sh, total);
     if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
@@ -1233,14 +1235,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(unsigned long long*
 
 __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const unsigned long long* blk, uint64_t nblocks,
                                                              const unsigned long long* tile_off,
-                                                             unsigned long long* blk_start) {
+                                                             unsigned long long* blk_start, uint64_t mask) {
     __shared__ uint64_t sh[17];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
-    uint32_t c[kScanPer];
+    uint64_t c[kScanPer];
     uint64_t s = 0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-        c[k] = base + k < nblocks ? (uint32_t)blk[base + k] : 0u;
+        c[k] = base + k < nblocks ? blk[base + k] & mask : 0u;
         s += c[k];
     }
     uint64_t total;
@@ -1420,10 +1422,10 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
         hipLaunchKernelGGL(k_pack_count, dim3(cg), dim3(kCountThreads), kLen8LdsBytes, s, a);
     }
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
-                       nblocks, tiles);
+                       nblocks, tiles, 0xffffffffull);
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, start_bit);
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
-                       nblocks, (const unsigned long long*)tiles, blk_start);
+                       nblocks, (const unsigned long long*)tiles, blk_start, 0xffffffffull);
     switch (t.enc_mode) {
         case ENC_DENSE: hipLaunchKernelGGL((k_pack_write<ENC_DENSE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
         case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, false>), dim3(wgs), dim3(threads), lds, s, a); break;
@@ -3175,10 +3177,10 @@ static hipError_t finish_index(const DecArgs& a, SyncArgs y, unsigned long long*
     }
     const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       tiles);
+                       tiles, 0xffffffffull);
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       (const unsigned long long*)tiles, first);
+                       (const unsigned long long*)tiles, first, 0xffffffffull);
     uint16_t* subs = reinterpret_cast<uint16_t*>(d_index + index_sub_offset(a.nblocks));
     // end bit = all ones unless the payload holds nsym codewords (k_sync_select writes it then)
     hipError_t e = hipMemsetAsync(d_index + a.nblocks, 0xff, 8, s);
@@ -3312,45 +3314,72 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
 }
 
 // ===========================================================================
-// Index-less decode without a block index: the `extract` path of a reference
-// file (Decompressor.cu:259-291 decodes it serially). One pass of LONG chains
-// over the payload, then a block-parallel decode; no boundary bitmap, no select:
-//   k_seg_walk    : lengths only (k_idx_walk's table, payload ring and escape
-//                   parking); per 4096-bit segment its ENTRY (absolute bit of
-//                   the first codeword starting at or after the segment's first
-//                   bit), its COUNT (codewords starting in it) and the start of
-//                   every 8th codeword counted from its entry (a u16 offset from
-//                   the segment's first bit: the PIECE records); per chain its
-//                   EXIT (the first codeword start at or after the chain's end)
-//   k_seg_fix     : a chain whose lead-in had not resynchronised disagrees with
-//                   the previous chain's exit at its first entry: walk the true
-//                   path from that exit, rewriting entries, counts and records,
-//                   until it lands on a recorded entry (from there both paths
-//                   agree); host loop to a fixed point (typically one pass)
-//   k_scan_*      : counts -> F[k], the number of the first codeword of segment k
-//   k_piece_decode: one wave per group of segments; piece i of segment k is its
-//                   codewords [8 i, 8 i + 8) (F[k] + 8 i in the output), four
-//                   pieces per lane decoded like k_decode's chains (staged payload,
-//                   LDS tables, global gathers consumed a pair-walk later), the
-//                   group's symbols collected in LDS and stored contiguously
+// Index-less decode in CHAIN BLOCKS: the `extract` path of a reference file
+// (Decompressor.cu:259-291 decodes it serially; the format carries no index,
+// Compressor.cu:427-601). Stream-ordered end to end (no host synchronisation):
+//   k_chain_walk    : one walk CHAIN per lane over cbits payload bits (lengths
+//                     only: k_idx_walk's 4-bit table, payload ring, escape
+//                     parking), starting kWalkLead bits early so it has
+//                     resynchronised by its first bit. From its ENTRY (the first
+//                     codeword start at or after the chain's first bit) it
+//                     records the stream bit of every 8th codeword (u16 low
+//                     bits, the block index's sub[] format) and of every 2048th
+//                     (u64 checkpoint: a decode BLOCK of 256 records); per chain
+//                     its EXIT (the first codeword start at or after its end)
+//                     and codeword count
+//   k_chain_fix     : a chain whose entry disagrees with the previous chain's
+//                     exit walks the true path from that exit until it lands on
+//                     one of its own records: the codewords before it are the
+//                     chain's HEAD (decoded serially by k_chain_tail), the
+//                     records from it on are valid. One grid pass, then one
+//                     workgroup iterating on the chains whose exit moved
+//                     (rare: the lead-in resynchronises with P ~ 1 - 4e-4)
+//   k_scan_*        : output index of every chain, first decode block of every chain
+//   k_chain_meta    : block descriptors (start, end, records, output index)
+//   k_chain_decode  : k_decode's pipelined block decoder (two blocks per wave,
+//                     quad walks, hot heads, gathers consumed a quad later) over
+//                     the chain blocks, each written at its chain's output index
+//   k_chain_tail    : heads, records past a chain's capacity, the end bit
+// Records are chain-phased: every piece but a chain's last decodes exactly 8
+// codewords, so the decoder has no partial pieces at segment ends.
 // ===========================================================================
-struct SegArgs {
-    uint64_t nseg, spc, nchains;
-    unsigned long long* ent;    // [nseg] entry bit of every segment
-    unsigned long long* cnt;    // [nseg] codewords starting in it
-    unsigned long long* xit;    // [nchains] exit bit of every walk chain
-    unsigned long long* first;  // [nseg] F (k_scan_apply of cnt)
-    uint8_t* rec;               // [nseg][rcap] piece records: u8 deltas (16-byte aligned rows)
-    uint32_t rcap;              // records per segment (multiple of 16; more is an error, flag 64)
-    uint32_t* dirty[2];         // k_seg_fix: chains to check, ping-pong
-    uint32_t* changed;
+constexpr int kChainWalkWaves = 16;
+constexpr uint32_t kChainRecs = 256;  // records per decode block (2048 codewords)
+// Per-lane payload ring of k_chain_walk: 4 chunks of 4 words, then a copy of word 0 (so the window's two
+// words q, q + 1 never wrap), odd stride (lanes' rings start in distinct banks).
+constexpr uint32_t kSegRing = 16 + 1;
+
+struct ChainBlk {
+    unsigned long long b0, b1;  // stream bits of the block's first record and of the one after its last
+    unsigned long long rec;     // index of the block's first record in ChainArgs::rec
+    long long out;              // output index of the block's first record's first symbol
+    uint32_t lo, hi;            // valid records [lo, hi) of the block
+    uint32_t last, pad;         // symbols of record hi - 1 (8 unless it is the chain's last codewords)
+};
+static_assert(sizeof(ChainBlk) == 48, "ChainBlk");
+
+struct ChainArgs {
+    uint64_t nchains, cbits, pbits;  // chain c walks payload bits [c cbits, min((c + 1) cbits, pbits)) after start
+    uint64_t start;                  // stream bit of the first symbol
+    uint32_t bpc, cap;               // decode blocks per chain, records per chain (kChainRecs * bpc)
+    uint16_t* rec;                   // [nchains][cap] low 16 bits of the stream bit of chain codeword 8 r
+    unsigned long long* ckpt;        // [nchains][bpc + 1] stream bit of record 256 j; after the last block, the exit
+    unsigned long long* ent;         // [nchains] walked entry
+    unsigned long long* xit;         // [nchains] walked exit (first codeword start >= the chain's end)
+    unsigned long long* txit;        // [nchains] true exit (k_chain_fix): the next chain's true entry
+    unsigned long long* cnt;         // [nchains] codewords from the walked entry to the exit
+    unsigned long long* tcnt;        // [nchains] codewords of the chain on the true path
+    unsigned long long* nblk;        // [nchains] decode blocks of the chain
+    unsigned long long* first;       // [nchains] output index of the chain's first true codeword
+    unsigned long long* bbase;       // [nchains] the chain's first decode block
+    uint32_t* hd;                    // [nchains] head: true codewords before the first valid record
+    uint32_t* r0;                    // [nchains] first valid record (nrec: none)
+    uint32_t* list[2];               // k_chain_fix_loop: chains to check, ping-pong
+    uint32_t* lcnt;                  // [2] their counts
+    ChainBlk* blk;                   // [nchains * bpc] decode block descriptors
+    unsigned long long* info;        // [0] decode blocks, [1] largest block (bits), [2] end bit
     uint32_t* err;
 };
-
-constexpr int kSegWalkWaves = 16;
-// Per-lane payload ring of k_seg_walk / k_seg_decode: 4 chunks of 4 words, then a copy of word 0 (so the
-// window's two words q, q + 1 never wrap), odd stride (lanes' rings start in distinct banks).
-constexpr uint32_t kSegRing = 16 + 1;
 
 // The 32-bit window at ring bit position p (p >= 1; bit 0 of the ring = bit 0 of chunk 0): words
 // (p - 1) >> 5 and the next one, one ds_read2_b32.
@@ -3418,91 +3447,65 @@ HZ_DEV void seg_feed(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint32_t p)
     }
 }
 
-// steps per round of the segment walk: two halves of 7 steps, so a half-round (plus its escape
-// gather) moves at most 8 codewords and takes at most one piece record. Zipf 16 GiB walk:
-// 10 / 12 / 14 steps 14.4 / 13.9 / 13.4 ms (A/B in one run, r04f); 3 parts of 6 steps 14.4 ms;
-// a second chunk fed per round (when no group load is pending) 15.2 ms
-#ifndef HZ_SEG_STEPS
-#define HZ_SEG_STEPS 14
-#endif
-constexpr int kSegSteps = HZ_SEG_STEPS;
+// Steps per round of the walk: two halves of 7 steps, so a half-round (plus its escape gather) moves
+// at most 8 codewords and takes at most one record. (Segment walk, 16 GiB Zipf, round 4: 10 / 12 / 14
+// steps 14.4 / 13.9 / 13.4 ms; 3 parts of 6 steps 14.4 ms; a second chunk fed per round 15.2 ms.)
+constexpr int kSegSteps = 14;
 static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
-__global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, SegArgs y) {
-    // the length table at LDS address 0 (k_idx_walk's layout), the rings after it
+
+__global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a, ChainArgs y) {
+    // the length table at LDS address 0 (k_idx_walk's layout), the rings and record buffers after it
     __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 8];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(wtab, a.lds_img, a.lds_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
     const uint32_t k = (uint32_t)a.k, bias = (uint32_t)a.bias;
     uint32_t* ring = lds + threadIdx.x * kSegRing;
+    uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + blockDim.x * kSegRing) + 8 * threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = ch < y.nchains;
-    const uint64_t seg0 = (live ? ch : 0) * y.spc;
-    const uint64_t seg1 = seg0 + y.spc < y.nseg ? seg0 + y.spc : y.nseg;
-    const uint64_t cs = seg0 * kSegBits, ce = seg1 * kSegBits;
+    const uint64_t chc = live ? ch : 0;
+    const uint64_t cs = chc * y.cbits;
+    const uint64_t ce = cs + y.cbits < y.pbits ? cs + y.cbits : y.pbits;
     const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
-    const uint64_t P0 = a.start + a.bit_adj + x0;
+    const uint64_t P0 = y.start + a.bit_adj + x0;
     SegFeed fd;
     seg_feed_init(a, ring, fd, (P0 >> 7) - 1);  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
     uint32_t p = (uint32_t)(P0 - 128 * fd.bch);    // ring bit position of the walk (>= 128)
-    const uint64_t abs0 = a.start + x0 - p;        // absolute stream bit of ring position q: abs0 + q
+    const uint64_t abs0 = y.start + x0 - p;        // absolute stream bit of ring position q: abs0 + q
     const uint32_t end = live ? p + (uint32_t)(ce - x0) : p;
-    uint32_t nb = p + (uint32_t)(cs - x0);         // the next segment start to cross
-    uint64_t sj = seg0;                            // the segment that starts at nb (seg1: the chain's end)
-    uint32_t cc = 0;                               // codewords since the last crossing
-    // Piece records of segment sj - 1: at most one per half-round (a half-round moves <= 8
-    // codewords), found at the half-round's end, written to the lane's 16-byte LDS record buffer
-    // (after the rings) and stored 16 records at a time.
-    // A record is the distance in bits from the previous one (from the segment's entry for the
-    // first): at most 8 codes of <= 22 bits, so one byte (the decoder rebuilds the offsets by a scan).
-    constexpr uint32_t RG = 16;
-    uint8_t* rbuf = reinterpret_cast<uint8_t*>(lds + kSegWalkWaves * 64 * kSegRing) + 16 * threadIdx.x;
-    uint32_t rj = 0, rprev = 0;
-    // roff: the ring position of a record; rprev: the previous record's (or the entry's)
-    auto rec_put = [&](uint32_t roff) {
-        rbuf[rj & (RG - 1)] = (uint8_t)(roff - rprev);
-        rprev = roff;
+    const uint32_t csr = p + (uint32_t)(cs - x0);  // the chain's first bit
+    uint16_t* recp = y.rec + chc * y.cap;
+    unsigned long long* ckp = y.ckpt + chc * (y.bpc + 1);
+    uint32_t rj = 0;  // records so far (record r = chain codeword 8 r)
+    uint32_t cc = 0;  // codewords since the entry
+    // record r: the codeword's stream bit, low 16 bits, into the lane's 16-byte LDS buffer (stored 8 at
+    // a time); every 256th also as a u64 checkpoint (a decode block's start). Past the capacity
+    // nothing is stored (k_chain_tail decodes those codewords).
+    auto rec_put = [&](uint32_t rp) {
+        const uint64_t ab = abs0 + rp;
+        if (rj < y.cap) {
+            rbuf[rj & 7] = (uint16_t)ab;
+            if ((rj & (kChainRecs - 1)) == 0) ckp[rj / kChainRecs] = ab;
+            if ((rj & 7) == 7) *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
+        } else if (rj == y.cap) {
+            ckp[y.bpc] = ab;  // the first codeword past the capacity
+        }
         ++rj;
     };
-    // segment sj - 1's record row, count and (segment sj's) entry: pointers advanced at each crossing
-    uint8_t* rrow = y.rec + seg0 * y.rcap;
-    unsigned long long* cntp = y.cnt + seg0;
-    unsigned long long* entp = y.ent + seg0;
-    auto rec_store = [&]() {  // the group holding record rj - 1 (nothing in the lead-in before seg0)
-        if (sj == seg0) return;
-        if (rj <= y.rcap)
-            *reinterpret_cast<uint4*>(rrow + ((rj - 1) & ~(RG - 1))) = *reinterpret_cast<const uint4*>(rbuf);
-        else
-            atomicOr(y.err, 64u);  // more pieces than the host planned for: the caller takes the index path
-    };
-    bool more = live;  // sj <= seg1 for a live chain: crossings still to record
-    // Past nb (the half's codeword jx ends at px >= nb): segment sj - 1 ends with codeword jx (its
-    // count), px is segment sj's entry (or the chain's exit)
-    auto cross = [&](uint32_t px, uint32_t count) {
-        if (sj > seg0) {
-            *cntp++ = count;
-            if (rj & (RG - 1)) rec_store();  // the segment's last, partial group
-            rrow += y.rcap;
-        }
-        *(sj < seg1 ? entp : y.xit + ch) = abs0 + px;
-        ++entp;
-        rj = 0;
-        rprev = px;  // the new segment's entry
-        ++sj;
-        more = sj <= seg1;
-        nb += kSegBits;
-    };
-    if (more && p >= nb) cross(p, 0);  // a chain at the stream's start begins on its first segment's entry
+    bool on = p >= csr;  // past the lead-in: counting from the entry
+    uint32_t ent = p;
+    if (on && p < end) rec_put(p);
     bool pk = false;
     uint32_t pW = 0;
     for (;;) {
         if (!__any(p < end)) break;
-        const uint32_t lim = min(end, 128 * fd.f - 96);  // filled data: both window words lie below p + 64
+        const uint32_t fill = 128 * fd.f - 96;  // filled data: both window words lie below p + 64
+        const uint32_t lim = min(on ? end : csr, fill);
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
             // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
-            // that parks or reaches lim stays put for the rest of the half), then at p for an escape;
-            // crossings and records are resolved once, at the half's end (at most one of each)
+            // that parks or reaches lim stays put for the rest of the half), then at p for an escape
             constexpr int S = kSegSteps / kWalkHalves;
             uint32_t q[S];
             uint32_t na = 0;
@@ -3526,442 +3529,571 @@ __global__ __launch_bounds__(kSegWalkWaves * 64) void k_seg_walk(WalkArgs a, Seg
                 p += a.esc[pW >> (32 - a.m)];
                 pk = false;
             }
-            // the end of the half's codeword j (1-based, j <= m)
-            auto pos = [&](uint32_t j) {
-                const uint32_t jj = j <= na ? j : 0u;
-                uint32_t r = p;
-#pragma unroll
-                for (int t = 0; t < S; ++t) r = jj == (uint32_t)t + 1u ? q[t] : r;
-                return r;
-            };
-            const uint32_t j1 = 8u - (cc & 7u);  // the codeword that is a multiple of 8 in the segment
-            if (__builtin_expect(more && p >= nb, 0)) {
-                uint32_t jx = 1;  // the crossing codeword: the first that ends at or past nb
-#pragma unroll
-                for (int t = 0; t < S; ++t) jx += ((uint32_t)t < na && q[t] < nb) ? 1u : 0u;
-                if (j1 < jx) {  // a record inside the segment (not its successor's entry)
-                    rec_put(pos(j1));
-                    if ((rj & (RG - 1)) == 0u) rec_store();
-                }
-                cross(pos(jx), cc + jx);
-                cc = m - jx;  // < 8: no record of the new segment in this half
-            } else {
+            if (on) {
+                // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based)
+                const uint32_t j1 = 8u - (cc & 7u);
                 if (j1 <= m) {
-                    rec_put(pos(j1));
-                    if ((rj & (RG - 1)) == 0u) rec_store();
+                    const uint32_t jj = j1 <= na ? j1 : 0u;
+                    uint32_t rp = p;
+#pragma unroll
+                    for (int t = 0; t < S; ++t) rp = jj == (uint32_t)t + 1u ? q[t] : rp;
+                    if (rp < end) rec_put(rp);  // (a codeword starting at the end is the next chain's)
                 }
                 cc += m;
+            } else if (p >= csr) {  // the lead-in's last step lands on the entry
+                on = true;
+                ent = p;
+                cc = 0;
+                if (p < end) rec_put(p);
             }
         }
         seg_feed(a, ring, fd, p);
     }
+    if (!live) return;
+    if ((rj & 7u) && (rj & ~7u) < y.cap)  // the last, partial group of records
+        *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
+    if (rj <= y.cap) ckp[(rj + kChainRecs - 1) / kChainRecs] = abs0 + p;  // after the last block: the exit
+    y.ent[ch] = abs0 + (on ? ent : p);
+    y.xit[ch] = abs0 + p;
+    y.txit[ch] = abs0 + p;
+    y.cnt[ch] = cc;
 }
 
-// Chain i (>= 1) against chain i - 1's exit: the true path enters segment seg0(i) at xit[i - 1].
-// When that is not the recorded entry, walk the true path segment by segment (entries, counts
-// and piece records rewritten) until a segment's true entry equals its recorded one; a walk that
-// leaves the chain hands its exit to chain i + 1 for the next iteration. it == 0 checks every chain.
+// Stream bit of record r (< cap) of chain c.
+HZ_DEV uint64_t chain_rec_pos(const ChainArgs& y, uint64_t c, uint32_t r) {
+    const uint64_t ck = y.ckpt[c * (y.bpc + 1) + r / kChainRecs];
+    return ck + (uint16_t)(y.rec[c * y.cap + r] - (uint16_t)ck);
+}
+
+HZ_DEV uint32_t chain_nrec(uint64_t n) { return (uint32_t)((n + 7) / 8); }
+HZ_DEV uint64_t chain_blocks(uint32_t navail, uint32_t r0) {
+    const uint32_t nb = (navail + kChainRecs - 1) / kChainRecs, j0 = r0 / kChainRecs;
+    return r0 < navail ? nb - j0 : 0;
+}
+
+// Chain i (>= 1) against chain i - 1's true exit (its true entry). When that is not the walked entry,
+// walk the true path until it lands on one of the chain's records (from there both paths agree):
+// head, first valid record, true count and decode blocks follow. The chain's true exit is its walked
+// exit when a record was met, else where the true path left the chain (the whole chain is head).
+// Returns true when the true exit changed (the next chain must be checked again). Idempotent: a chain
+// checked against a stale entry (another chain's exit moving concurrently) is checked again.
 template <int MODE>
-__global__ __launch_bounds__(kSyncThreads) void k_seg_fix(DecArgs a, SegArgs y, uint64_t start, int it) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, a.lds_img, a.lds_words);
-    const uint32_t* dr = y.dirty[it & 1];
-    uint32_t* dw = y.dirty[(it + 1) & 1];
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < y.nchains; i += stride) {
-        if (it > 0 && !dr[i]) continue;
-        uint64_t s = i * y.spc;
-        const uint64_t s1 = s + y.spc < y.nseg ? s + y.spc : y.nseg;
-        uint64_t p = y.xit[i - 1];
-        if (p == y.ent[s]) continue;
+HZ_DEV bool chain_fix_one(const DecArgs& a, const ChainArgs& y, const uint32_t* lds, uint64_t i) {
+    uint64_t p = y.txit[i - 1];
+    const uint64_t n = y.cnt[i];
+    const uint32_t nrec = chain_nrec(n), navail = nrec < y.cap ? nrec : y.cap;
+    uint32_t rr = 0;
+    uint64_t h = 0;
+    bool met = p == y.ent[i];
+    if (!met) {
+        const uint64_t cend = (i + 1) * y.cbits < y.pbits ? (i + 1) * y.cbits : y.pbits;
+        const uint64_t ce = y.start + cend;
         BitReader r;
         br_init(r, a, p + a.bit_adj);
-        bool met = false;
-        for (; s < s1; ++s) {
-            if (p == y.ent[s]) { met = true; break; }
-            y.ent[s] = p;
-            const uint64_t sb = start + (s + 1) * kSegBits;
-            uint64_t n = 0, pprev = p;
-            while (p < sb) {
-                uint32_t sym;
-                const uint32_t L = br_next<MODE>(r, a, lds, sym);
-                if (L == 0) { atomicOr(a.err, 2u); p = sb; break; }
-                p += L;
-                ++n;
-                if ((n & 7u) == 0 && p < sb) {
-                    const uint64_t j = (n >> 3) - 1;
-                    if (j < y.rcap) y.rec[s * y.rcap + j] = (uint8_t)(p - pprev);
-                    else atomicOr(y.err, 64u);
-                    pprev = p;
-                }
+        uint64_t R = navail ? chain_rec_pos(y, i, 0) : ~0ull;
+        for (;;) {
+            while (rr < navail && R < p) {
+                ++rr;
+                R = rr < navail ? chain_rec_pos(y, i, rr) : ~0ull;
             }
-            y.cnt[s] = n;
+            if (rr < navail && R == p) { met = true; break; }
+            if (p >= ce) break;
+            uint32_t sym;
+            const uint32_t L = br_next<MODE>(r, a, lds, sym);
+            if (L == 0) { atomicOr(a.err, 2u); break; }
+            p += L;
+            ++h;
         }
-        if (!met) {  // the exit moved: chain i + 1 checks it next iteration
-            y.xit[i] = p;
-            if (i + 1 < y.nchains) dw[i + 1] = 1u;
-            atomicAdd(y.changed, 1u);
+    }
+    y.hd[i] = (uint32_t)h;
+    y.r0[i] = met ? rr : nrec;
+    y.tcnt[i] = met ? h + n - 8ull * rr : h;
+    y.nblk[i] = met ? chain_blocks(navail, rr) : 0;
+    const uint64_t tx = met ? y.xit[i] : p;
+    if (tx != y.txit[i]) {
+        y.txit[i] = tx;
+        return true;
+    }
+    return false;
+}
+
+// Every chain once (chain 0 starts on its entry); chains whose predecessor's exit moved go on a list.
+template <int MODE>
+__global__ __launch_bounds__(kSyncThreads) void k_chain_fix(DecArgs a, ChainArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < y.nchains; i += stride) {
+        if (i == 0) {
+            const uint64_t n = y.cnt[0];
+            const uint32_t nrec = chain_nrec(n);
+            y.hd[0] = 0;
+            y.r0[0] = 0;
+            y.tcnt[0] = n;
+            y.nblk[0] = chain_blocks(nrec < y.cap ? nrec : y.cap, 0);
+            continue;
+        }
+        if (chain_fix_one<MODE>(a, y, lds, i) && i + 1 < y.nchains) {
+            const uint32_t s = atomicAdd(y.lcnt, 1u);
+            y.list[0][s] = (uint32_t)(i + 1);
         }
     }
 }
 
-// Block-parallel decode of groups of y.gs segments (k_decode's chain machinery): the
-// group's payload bits [start + 4096 k0, + 4096 gs + 8 max_len) staged (descending) in the
-// wave's slot; rounds of 64 * kPieceChains pieces, lane l taking pieces 64 c + l as two halves
-// (pairs or quads) whose global gathers land behind the other half's LDS walk; a round's symbols (one
-// contiguous output run: its pieces are consecutive) go to the wave's LDS output buffer at
-// their place (slot 0 = the run's first symbol rounded down to 8) and leave as 16-byte
-// stores (2-byte stores at the run's two ends). A group's segment records and staging
-// loads are issued together (one memory round trip), its piece records in a second.
-constexpr uint32_t kPieceSyms = 8;  // codewords per piece: one decode chain
-constexpr int kPieceChains = (int)kPieceLaneChains;  // pieces per lane per round
-constexpr int kPieceGrp = kPieceChains == 8 ? 4 : 2;  // chains walked together: pairs, or quads for 8
-constexpr int kPieceNG = kPieceChains / kPieceGrp;     // groups of them per round (2 or 3)
-static_assert(kPieceChains == 4 || kPieceChains == 6 || kPieceChains == 8, "two or three pairs, or two quads");
-constexpr uint32_t kPieceRound = 64 * kPieceChains;  // pieces per round
-constexpr int kPieceWaves = HZ_PIECE_WAVES;
-static_assert(kPieceWaves == kPieceDecWaves, "hz_internal.h kPieceDecWaves");
-
-
-struct PieceArgs {
-    const unsigned long long* ent;
-    const unsigned long long* cnt;
-    const unsigned long long* first;
-    const uint8_t* rec;
-    uint32_t rcap, gs;
-    uint32_t slot_words;   // staging words per wave (multiple of 4)
-    uint64_t nseg, start, nsym;
-    unsigned long long* end;  // bit after codeword nsym - 1
-};
-
-HZ_DEV uint64_t readlane64(uint64_t v, int l) {
-    return ((uint64_t)readlane((uint32_t)(v >> 32), l) << 32) | readlane((uint32_t)v, l);
-}
-
-// A group's segment records (lanes < ns) and staging chunks, issued together.
-struct PieceIn {
-    uint64_t c, e, f;
-    uint4 sv[kStageUnroll];
-    uint4 rr;  // 16 bytes of the group's record rows (1 KiB per wave: all of them, host geometry)
-};
-HZ_DEV void piece_prefetch(const DecArgs& d, const PieceArgs& y, uint64_t g, int lane, PieceIn& x) {
-    const uint64_t gg = g * y.gs < y.nseg ? g : 0;  // past the end: any group, never used
-    const uint64_t k0 = gg * y.gs;
-    const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
-    const uint64_t kk = k0 + ((uint32_t)lane < ns ? (uint32_t)lane : 0u);
-    x.c = y.cnt[kk];
-    x.e = y.ent[kk];
-    x.f = y.first[kk];
-    const uint32_t rbytes = ns * y.rcap, ro = 16u * (uint32_t)lane;
-    x.rr = *reinterpret_cast<const uint4*>(y.rec + k0 * y.rcap + (ro < rbytes ? ro : 0u));
-    PipeMeta m;
-    m.b0 = y.start + k0 * kSegBits;
-    m.b1 = m.b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
-    m.sub = 0;
-    dec_stage_prefetch(d, m, lane, x.sv);
-}
-
-__global__ __launch_bounds__(kPieceWaves * 64) void k_piece_decode(DecArgs d, PieceArgs y) {
+// The listed chains again, one workgroup, until no exit moves: each pass moves the frontier of a run
+// of unsynchronised chains by one chain (bounded by nchains passes).
+template <int MODE>
+__global__ __launch_bounds__(kSyncThreads) void k_chain_fix_loop(DecArgs a, ChainArgs y) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(lds, d.lds_img, d.lds_words);
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    for (uint64_t it = 0; it <= y.nchains; ++it) {
+        const uint32_t cur = (uint32_t)(it & 1);
+        const uint32_t n = __hip_atomic_load(y.lcnt + cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n == 0) break;  // every thread read the same count (the adds happened before the barrier)
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint64_t i = y.list[cur][j];
+            if (chain_fix_one<MODE>(a, y, lds, i) && i + 1 < y.nchains) {
+                const uint32_t s = atomicAdd(y.lcnt + (cur ^ 1u), 1u);
+                y.list[cur ^ 1u][s] = (uint32_t)(i + 1);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(y.lcnt + cur, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+}
+
+// Decode block descriptors of every chain (after the scans of tcnt -> first and nblk -> bbase), the
+// largest block and the number of blocks.
+__global__ __launch_bounds__(256) void k_chain_meta(ChainArgs y) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t maxb = 0;
+    if (c < y.nchains) {
+        const uint64_t nb = y.nblk[c];
+        if (c + 1 == y.nchains) y.info[0] = y.bbase[c] + nb;
+        if (nb) {
+            const uint64_t n = y.cnt[c];
+            const uint32_t nrec = chain_nrec(n), navail = nrec < y.cap ? nrec : y.cap;
+            const uint32_t r0 = y.r0[c], j0 = r0 / kChainRecs;
+            const long long out0 = (long long)(y.first[c] + y.hd[c]) - 8ll * r0;  // output index of record 0
+            const unsigned long long* ckp = y.ckpt + c * (y.bpc + 1);
+            ChainBlk* bk = y.blk + y.bbase[c];
+            for (uint32_t j = j0; j < j0 + (uint32_t)nb; ++j) {
+                ChainBlk d;
+                d.b0 = ckp[j];
+                d.b1 = ckp[j + 1];
+                d.rec = c * y.cap + (uint64_t)kChainRecs * j;
+                d.out = out0 + 8ll * kChainRecs * j;
+                d.lo = r0 > kChainRecs * j ? r0 - kChainRecs * j : 0u;
+                const uint32_t hi = navail - kChainRecs * j;
+                d.hi = hi < kChainRecs ? hi : kChainRecs;
+                // the chain's last record (not cut by the capacity) holds n - 8 (nrec - 1) codewords
+                d.last = nrec <= y.cap && kChainRecs * j + d.hi == nrec ? (uint32_t)(n - 8ull * (nrec - 1)) : 8u;
+                d.pad = 0;
+                bk[j - j0] = d;
+                maxb = d.b1 - d.b0 > maxb ? d.b1 - d.b0 : maxb;
+            }
+        }
+    }
+    // one atomic per wave
+#pragma unroll
+    for (int mm = 1; mm < 64; mm <<= 1) {
+        const uint64_t o = ((uint64_t)shfl_xor_u32((uint32_t)(maxb >> 32), mm) << 32) | shfl_xor_u32((uint32_t)maxb, mm);
+        maxb = o > maxb ? o : maxb;
+    }
+    if ((threadIdx.x & 63) == 0 && maxb) atomicMax(y.info + 1, (unsigned long long)maxb);
+}
+
+// Block metadata of the chain decoder: the descriptor's stream bits (for the staging), the lane's
+// four record low bits (chain slots 64 k + lane; invalid records read as the block start, decoded and
+// never stored), output index, valid range.
+struct ChainMeta {
+    uint64_t b0, b1, sub;
+    long long out;
+    uint32_t lo, hi, last;
+};
+
+HZ_DEV void chain_meta_load(const ChainArgs& y, uint64_t b, uint64_t nb, int lane, ChainMeta& m) {
+    const uint64_t bb = b < nb ? b : (nb ? nb - 1 : 0);  // past the end: any block, never stored
+    // the descriptor through the scalar cache (6 u64: b0, b1, rec, out, lo | hi << 32, last)
+    typedef const __attribute__((address_space(4))) unsigned long long* cu64p;
+    const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bb >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bb);
+    const cu64p d = (cu64p)y.blk + 6 * bu;
+    m.b0 = d[0];
+    m.b1 = d[1];
+    const uint64_t rec = d[2];
+    m.out = (long long)d[3];
+    const uint64_t lohi = d[4];
+    m.lo = (uint32_t)lohi;
+    m.hi = b < nb ? (uint32_t)(lohi >> 32) : 0u;
+    m.last = (uint32_t)d[5];
+    const uint16_t* s16 = y.rec + rec + (uint32_t)lane;
+    uint64_t sub = 0;
+#pragma unroll
+    for (int c = 0; c < kChainsPerLane; ++c) {
+        const uint32_t t = 64u * c + (uint32_t)lane;
+        const uint16_t v = s16[t < m.hi ? 64 * c : 0];  // one load per slot, always issued
+        sub |= (uint64_t)(t < m.hi ? v : (uint16_t)m.b0) << (16 * c);
+    }
+    m.sub = sub;
+}
+
+// A chain block's symbols: record t = 64 c + lane of the block, 8 symbols at output index out + 8 t
+// (2-byte aligned: the 16-byte stores of adjacent lanes are adjacent), the last record's and the
+// stream end's symbol by symbol.
+HZ_DEV void chain_store(const DecArgs& a, const ChainMeta& m, int lane, const uint32_t* pk) {
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(a.out);
+    const bool full = m.lo == 0 && m.hi == kChainRecs && m.last == 8 && m.out >= 0 &&
+                      (uint64_t)m.out + (uint64_t)kBlockSyms <= a.nsym;
+    if (full) {
+#pragma unroll
+        for (int c = 0; c < kChainsPerLane; ++c) {
+            uint32_t* q = reinterpret_cast<uint32_t*>(out16 + m.out + 8 * (64 * c + lane));
+            u32x4a2 v = u32x4a2{pk[4 * c], pk[4 * c + 1], pk[4 * c + 2], pk[4 * c + 3]};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4a2*>(q));
+        }
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < kChainsPerLane; ++c) {
+        const uint32_t t = 64u * c + (uint32_t)lane;
+        if (t < m.lo || t >= m.hi) continue;
+        const long long o = m.out + 8ll * t;
+        if (o < 0 || (uint64_t)o >= a.nsym) continue;
+        uint32_t cn = t + 1 == m.hi ? m.last : 8u;
+        cn = a.nsym - (uint64_t)o < cn ? (uint32_t)(a.nsym - (uint64_t)o) : cn;
+        if (cn == 8) {
+            *reinterpret_cast<u32x4a2*>(out16 + o) = u32x4a2{pk[4 * c], pk[4 * c + 1], pk[4 * c + 2], pk[4 * c + 3]};
+        } else {
+            for (uint32_t q = 0; q < cn; ++q) out16[o + q] = (uint16_t)(pk[4 * c + (q >> 1)] >> (16 * (q & 1)));
+        }
+    }
+}
+
+// k_decode's two-blocks-per-wave pipelined walk (dec_wave_pipe2) over chain blocks b, b + 1, then
+// b + stride, ...: the same staging, quad walks and deferred gathers; block metadata from the
+// descriptors, output at each block's chain position.
+HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, const uint32_t* lds, uint32_t* stg,
+                           uint32_t slot, uint64_t b, uint64_t stride, int lane) {
+    constexpr int C = 2 * kChainsPerLane;
+    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(a.l2);
+    ChainMeta mc[2], mn[2], mn2[2];
+    uint4 sc[2][kStageUnroll], sn[2][kStageUnroll];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        chain_meta_load(y, b + j, nb, lane, mc[j]);
+        chain_meta_load(y, b + stride + j, nb, lane, mn[j]);
+    }
+    auto as_pipe = [](const ChainMeta& m) { PipeMeta p; p.b0 = m.b0; p.b1 = m.b1; p.sub = m.sub; return p; };
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, as_pipe(mc[j]), lane, sc[j]);
+    for (; b < nb; b += stride) {
+        uint32_t p1[C];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            uint64_t w0;
+            dec_stage_commit<true>(a, as_pipe(mc[j]), slot >> 2, stg + j * slot, lane, sc[j], w0);
+            uint32_t off[kChainsPerLane];
+            dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
+            const uint32_t top = (uint32_t)(stg - lds) + (uint32_t)(j + 1) * slot - 1u;
+            const uint32_t base = top * 32u - (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5));
+#pragma unroll
+            for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base - off[c];
+        }
+        __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+        uint32_t pk[2][kSPT / 2];
+        PipeLane st[C];
+        uint32_t g[C];
+        auto finish = [&](int c, int q) {
+            const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
+            p1[c] -= lut_leaf_len(ee);
+            const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
+            if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x06050201u);
+            else pk[c / kChainsPerLane][i] = ee;
+        };
+        auto issue4 = [&](int c) {
+            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
+        };
+        issue4(0);
+#pragma unroll
+        for (int q = 0; q < kChainSyms; ++q) {
+            issue4(4);
+            if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
+#pragma unroll
+                for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, as_pipe(mn[j]), lane, sn[j]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) chain_meta_load(y, b + 2 * stride + j, nb, lane, mn2[j]);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) finish(c, q);
+            if (q + 1 < kChainSyms) issue4(0);
+#pragma unroll
+            for (int c = 4; c < 8; ++c) finish(c, q);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (b + j < nb) chain_store(a, mc[j], lane, pk[j]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            mc[j] = mn[j];
+            mn[j] = mn2[j];
+#pragma unroll
+            for (int u = 0; u < kStageUnroll; ++u) sc[j][u] = sn[j][u];
+        }
+    }
+}
+
+// Persistent: the block count and the largest block come from the device (k_chain_meta); slots are
+// sized in-kernel from the largest block, waves without a slot pair idle (k_decode's rule).
+__global__ __launch_bounds__(kDecPipe2Threads) void k_chain_decode(DecArgs a, ChainArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
     const uint32_t wid = wave_id();
-    const uint32_t wave_words = piece_wave_words(y.slot_words);
-    uint32_t* stg = lds + d.lds_words + wid * wave_words;
-    uint32_t* sinfo = stg + y.slot_words;  // per segment: cnt, entry, F (u32)
-    uint16_t* rlds = reinterpret_cast<uint16_t*>(sinfo + ((3 * kPieceMaxGroup + 3) & ~3u));  // piece starts (from b0)
-    const __amdgpu_buffer_rsrc_t l2r = lut_l2_rsrc(d.l2);
-    const uint32_t top = (uint32_t)(stg - lds) + y.slot_words - 1u;  // the slot's top word (descending staging)
-    const uint64_t ngroups = (y.nseg + y.gs - 1) / y.gs;
-    const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint16_t* out16 = reinterpret_cast<uint16_t*>(d.out);
-    uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
-    PieceIn cur, nxt;
-    if (g < ngroups) piece_prefetch(d, y, g, lane, cur);
-    for (; g < ngroups; g += gstride) {
-        const uint64_t k0 = g * y.gs;
-        const uint32_t ns = (uint32_t)(y.nseg - k0 < y.gs ? y.nseg - k0 : y.gs);
-        const uint64_t b0 = y.start + k0 * kSegBits;  // the group's first bit
-        // the group's segments in lanes 0 .. ns - 1: pieces per segment and their exclusive prefix;
-        // counts, entries (from b0) and F (from F0) as u32 in the wave's LDS table
-        const bool sl = (uint32_t)lane < ns;
-        const uint64_t sc = sl ? cur.c : 0;
-        const uint32_t np = (uint32_t)((sc + kPieceSyms - 1) / kPieceSyms);
-        const uint32_t incl = wave_incl_sum(np);
-        const uint32_t T = readlane(incl, (int)ns - 1);
-        const uint64_t F0 = readlane64(cur.f, 0);
-        // output symbols [F0, F0 + lim) exist (u32: a group holds < 2^32 symbols)
-        const uint32_t lim = y.nsym > F0 ? (y.nsym - F0 < 0xffffffffull ? (uint32_t)(y.nsym - F0) : 0xffffffffu) : 0u;
-        uint32_t Qs[kPieceMaxGroup];
-#pragma unroll
-        for (uint32_t t = 0; t < kPieceMaxGroup; ++t) Qs[t] = t < ns ? readlane(incl - np, (int)t) : 0xffffffffu;
-        if (sl) {
-            sinfo[3 * lane] = (uint32_t)sc;
-            sinfo[3 * lane + 1] = (uint32_t)(cur.e - b0);
-            sinfo[3 * lane + 2] = (uint32_t)(cur.f - F0);
-        }
-        // the group's piece starts from its records: lane l holds records 16 l .. 16 l + 15 (one row
-        // never splits a lane: rcap % 16 == 0); in-lane prefix, then a scan across the lanes of a row
-        // (segmented at row starts), plus the row's entry; u16 offsets from b0 into LDS
-        {
-            const uint32_t w[4] = {cur.rr.x, cur.rr.y, cur.rr.z, cur.rr.w};
-            uint32_t pre[16], acc = 0;
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                acc += (w[t >> 2] >> (8 * (t & 3))) & 0xffu;
-                pre[t] = acc;
+    typedef const __attribute__((address_space(4))) unsigned long long* cu64p;
+    const uint64_t nb = ((cu64p)y.info)[0];
+    if (nb == 0) return;  // no chain has a block (every codeword in heads / tails)
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)dec_slot_words(((cu64p)y.info)[1], a.max_len));
+    const uint32_t nwave = blockDim.x >> 6;
+    uint32_t nw2 = a.region_words / (2 * slot);
+    nw2 = nw2 < nwave ? nw2 : nwave;
+    if (nw2 == 0) {  // a block larger than the region (cannot happen: the host sizes it for 2048 x max_len)
+        if (threadIdx.x == 0) atomicOr(a.err, 128u);
+        return;
+    }
+    if (wid >= nw2) return;
+    const uint64_t b = 2 * ((uint64_t)blockIdx.x * nw2 + wid), stride = 2 * (uint64_t)gridDim.x * nw2;
+    dec_wave_chain(a, y, nb, lds, lds + a.lds_words + wid * 2 * slot, slot, b, stride, lane);
+}
+
+// One thread per chain: its head (true codewords before its first valid record), the codewords past
+// its record capacity, and the end bit of codeword nsym - 1, decoded serially (rare, short).
+template <int MODE>
+__global__ __launch_bounds__(kSyncThreads) void k_chain_tail(DecArgs a, ChainArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(a.out);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t last = a.nsym - 1;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < y.nchains; c += stride) {
+        const uint64_t F = y.first[c], T = y.tcnt[c], n = y.cnt[c];
+        const uint32_t h = y.hd[c], r0 = y.r0[c], nrec = chain_nrec(n);
+        const bool has_end = a.nsym > 0 && F <= last && last < F + T;
+        // serial decode of k codewords from stream bit p into output index o, noting the end bit
+        auto serial = [&](uint64_t p, uint64_t o, uint64_t k) {
+            BitReader r;
+            br_init(r, a, p + a.bit_adj);
+            for (uint64_t t = 0; t < k; ++t) {
+                uint32_t sym;
+                const uint32_t L = br_next<MODE>(r, a, lds, sym);
+                if (L == 0) { atomicOr(a.err, 2u); return; }
+                p += L;
+                if (o + t < a.nsym) out16[o + t] = (uint16_t)sym;
+                if (o + t == last) y.info[2] = p;
             }
-            const uint32_t row = 16u * (uint32_t)lane / y.rcap;                // the lane's segment in the group
-            const bool head = (16u * (uint32_t)lane) % y.rcap == 0u;
-            uint32_t v = acc;                                                  // segmented inclusive scan
-            bool f = head;
-#pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1) {
-                const uint32_t ov = shfl_up_u32(v, dd);
-                const uint32_t of = shfl_up_u32(f ? 1u : 0u, dd);
-                if (lane >= dd && !f) { v += ov; f = of != 0u; }
-            }
-            const uint32_t base0 = (row < ns ? sinfo[3 * row + 1] : 0u) + v - acc;  // entry + records before the lane
-            uint32_t o2[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) o2[t] = ((base0 + pre[2 * t]) & 0xffffu) | ((base0 + pre[2 * t + 1]) << 16);
-            uint4* r4 = reinterpret_cast<uint4*>(rlds) + 2 * lane;
-            r4[0] = make_uint4(o2[0], o2[1], o2[2], o2[3]);
-            r4[1] = make_uint4(o2[4], o2[5], o2[6], o2[7]);
-        }
-        // the group's payload bits, staged descending (k_decode's layout)
-        PipeMeta m;
-        m.b0 = b0;
-        m.b1 = b0 + (uint64_t)ns * kSegBits + kPieceSyms * (uint32_t)d.max_len;
-        m.sub = 0;
-        uint64_t w0;
-        __builtin_amdgcn_wave_barrier();  // the previous group's steps have read the slot
-        dec_stage_commit<true>(d, m, y.slot_words >> 2, stg, lane, cur.sv, w0);
-        const uint32_t base = top * 32u - (uint32_t)(b0 + d.bit_adj - (w0 << 5));
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t r0 = 0; r0 < T; r0 += kPieceRound) {
-            uint32_t p1[kPieceChains], cn[kPieceChains], ob[kPieceChains], st0[kPieceChains];  // ob: from F0
-#pragma unroll
-            for (int c = 0; c < kPieceChains; ++c) {
-                const uint32_t q = r0 + 64u * (uint32_t)c + (uint32_t)lane;
-                uint32_t sg = 0, qs = 0;
-#pragma unroll
-                for (uint32_t t = 1; t < kPieceMaxGroup; ++t) {
-                    const bool in = q >= Qs[t];
-                    sg = in ? t : sg;
-                    qs = in ? Qs[t] : qs;
+        };
+        if (h) serial(y.txit[c - 1], F, h);  // chain 0 starts on its entry: never a head
+        if (r0 < nrec && nrec > y.cap)      // records past the capacity: the rest of the chain
+            serial(y.ckpt[c * (y.bpc + 1) + y.bpc], F + h + 8ull * (y.cap - r0), n - 8ull * y.cap);
+        if (has_end && last >= F + h) {     // the end bit inside a piece: walk that piece up to it
+            const uint64_t q = last - (F + h);
+            const uint64_t m = r0 + q / 8;
+            if (m < y.cap) {
+                BitReader r;
+                uint64_t p = chain_rec_pos(y, c, (uint32_t)m);
+                br_init(r, a, p + a.bit_adj);
+                for (uint32_t t = 0; t <= (uint32_t)(q % 8); ++t) {
+                    uint32_t sym;
+                    const uint32_t L = br_next<MODE>(r, a, lds, sym);
+                    if (L == 0) { atomicOr(a.err, 2u); break; }
+                    p += L;
                 }
-                const uint32_t cs = sinfo[3 * sg], es = sinfo[3 * sg + 1], fs = sinfo[3 * sg + 2];
-                const bool valid = q < T;
-                const uint32_t i = valid ? q - qs : 0;
-                const uint32_t o = fs + kPieceSyms * i;  // from F0
-                uint32_t n = valid ? cs - kPieceSyms * i : 0;
-                n = n < kPieceSyms ? n : kPieceSyms;
-                n = o < lim ? (lim - o < n ? lim - o : n) : 0;
-                cn[c] = n;
-                ob[c] = o;
-                // piece 0 starts at the segment's entry, piece i >= 1 at its record (an offset from the
-                // segment's first bit, prefetched with the group into LDS)
-                const uint32_t rv = rlds[sg * y.rcap + (i ? i - 1 : 0)];
-                st0[c] = i ? rv : es;  // from b0
-            }
-#pragma unroll
-            for (int c = 0; c < kPieceChains; ++c) p1[c] = base - st0[c];
-            PipeLane st[kPieceChains];
-            uint32_t gv[kPieceChains];
-            auto issueh = [&](int c) {  // a pair's (quad's) LDS walk, then its global gathers
-                dec_pipe_ldsn<kPieceGrp>(d, lds, p1 + c, st + c);
-#pragma unroll
-                for (int u = 0; u < kPieceGrp; ++u) gv[c + u] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + u].gi, 0, 0);
-            };
-            // symbols packed in registers (an even step keeps the entry, the odd one packs both symbols,
-            // leaf bytes 1-2, by one v_perm); a whole piece leaves as one 16-byte store at its place
-            uint32_t pk[kPieceChains][kPieceSyms / 2];
-            auto finish = [&](int c, uint32_t t) {
-                const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : gv[c];
-                p1[c] -= lut_leaf_len(ee);
-                if (t & 1) pk[c][t >> 1] = __builtin_amdgcn_perm(ee, pk[c][t >> 1], 0x06050201u);
-                else pk[c][t >> 1] = ee;
-            };
-            // each group's gathers are consumed after the next group's walk has been issued
-            issueh(0);
-#pragma unroll
-            for (uint32_t t = 0; t < kPieceSyms; ++t) {
-#pragma unroll
-                for (int gi = 1; gi < kPieceNG; ++gi) {
-                    issueh(gi * kPieceGrp);
-#pragma unroll
-                    for (int u = (gi - 1) * kPieceGrp; u < gi * kPieceGrp; ++u) finish(u, t);
-                }
-                if (t + 1 < kPieceSyms) issueh(0);
-#pragma unroll
-                for (int u = (kPieceNG - 1) * kPieceGrp; u < kPieceChains; ++u) finish(u, t);
-            }
-            // whole pieces: 16 bytes at output symbol F0 + o (2-byte aligned: the hardware takes unaligned
-            // global stores; a lane's neighbours write the adjacent 16 bytes, so a store instruction covers
-            // about 1 KiB); short pieces (a segment's last, the stream's end) symbol by symbol, so they
-            // never touch the next piece's symbols
-#pragma unroll
-            for (int c = 0; c < kPieceChains; ++c) {
-                const uint64_t o = F0 + ob[c];
-                if (cn[c] == kPieceSyms) {
-                    *reinterpret_cast<u32x4a2*>(out16 + o) = u32x4a2{pk[c][0], pk[c][1], pk[c][2], pk[c][3]};
-                } else {
-                    for (uint32_t t = 0; t < cn[c]; ++t) {
-                        uint32_t w = pk[c][0];
-#pragma unroll
-                        for (uint32_t u = 1; u < kPieceSyms / 2; ++u) w = (t >> 1) == u ? pk[c][u] : w;
-                        out16[o + t] = (uint16_t)(w >> (16 * (t & 1)));
-                    }
-                }
-            }
-            // the stream's last codeword: its chain is decoded again, alone, for its end bit
-#pragma unroll
-            for (int c = 0; c < kPieceChains; ++c) {
-                const bool is_end = cn[c] > 0 && ob[c] + cn[c] == lim && lim == y.nsym - F0;
-                if (__builtin_expect(is_end, 0)) {
-                    uint32_t pp = base - st0[c];
-                    for (uint32_t t = 0; t < cn[c]; ++t) {
-                        PipeLane one;
-                        dec_pipe_ldsn<1>(d, lds, &pp, &one);
-                        const uint32_t ee = lut_leaf(one.e) ? one.e : __builtin_amdgcn_raw_buffer_load_b32(l2r, one.gi, 0, 0);
-                        pp -= lut_leaf_len(ee);
-                    }
-                    *y.end = b0 + (uint64_t)(base - pp);
-                }
+                y.info[2] = p;
             }
         }
-        // the next group's records and staging chunks (after the last round: their VGPRs beside the
-        // chains' spill at 1024 threads)
-        piece_prefetch(d, y, g + gstride, lane, nxt);
-        cur = nxt;
     }
 }
 
-// The piece geometry of a payload: expected bits per codeword from its size.
-static PieceGeom seg_piece_geom(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len) {
-    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
-    return piece_geom(nsym ? (double)bits / (double)nsym : 16.0, max_len);
+// ---- host side -----------------------------------------------------------------------------
+// Chain geometry: chains of cbits payload bits, about one per walk lane of the device (16 waves per
+// CU), but at least kChainMinBlocks decode blocks long; each chain's record capacity holds its
+// expected records with 25 % headroom (more go to k_chain_tail, serially).
+constexpr uint64_t kChainMinBlocks = 4;
+struct ChainGeom {
+    uint64_t nchains = 0, cbits = 0, pbits = 0;
+    uint32_t bpc = 0, cap = 0;
+    uint64_t off_rec, off_ckpt, off_arr, off_u32, off_list, off_info, off_tiles, off_blk, words;
+};
+
+static ChainGeom chain_geom(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, double kraft_bits, int ncu) {
+    ChainGeom g;
+    g.pbits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    if (g.pbits == 0 || nsym == 0) return g;
+    double avg = (double)g.pbits / (double)nsym;  // payload bits per codeword
+    if (kraft_bits > 0.5 && kraft_bits < avg) avg = kraft_bits;  // the lower (more records) of the two
+    if (avg < 1.0) avg = 1.0;
+    const uint64_t lanes = (uint64_t)kChainWalkWaves * 64 * (uint64_t)(ncu > 0 ? ncu : 1);
+    const uint64_t minbits = (uint64_t)(kChainMinBlocks * kBlockSyms * avg);
+    uint64_t cb = (g.pbits + lanes - 1) / lanes;
+    cb = cb > minbits ? cb : minbits;
+    cb = (cb + 127) & ~127ull;
+    g.cbits = cb;
+    g.nchains = (g.pbits + cb - 1) / cb;
+    const double recs = (double)cb / avg / 8.0 * 1.25 + 64.0;
+    g.bpc = (uint32_t)((recs + kChainRecs - 1) / kChainRecs);
+    g.cap = g.bpc * kChainRecs;
+    const uint64_t nc = g.nchains;
+    const uint64_t ntiles = (nc + kScanTile - 1) / kScanTile;
+    uint64_t w = 0;
+    g.off_rec = w;   w += (nc * g.cap * 2 + 15) / 16 * 2;       // u16 records (16-byte rows)
+    g.off_ckpt = w;  w += nc * (g.bpc + 1);                     // u64 checkpoints
+    g.off_arr = w;   w += 8 * nc;                               // ent, xit, txit, cnt, tcnt, nblk, first, bbase
+    g.off_u32 = w;   w += nc;                                   // hd, r0 (u32)
+    g.off_list = w;  w += nc + 1;                               // list[2] (u32), lcnt
+    g.off_info = w;  w += 4;
+    g.off_tiles = w; w += ntiles + 2;
+    g.off_blk = w;   w += nc * g.bpc * (sizeof(ChainBlk) / 8);
+    g.words = w + 8;
+    return g;
 }
 
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, int max_len) {
-    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
-    const uint64_t nseg = (bits + kSegBits - 1) / kSegBits;
-    const uint64_t ntiles = (nseg + kScanTile - 1) / kScanTile;
-    const PieceGeom pg = seg_piece_geom(payload_bytes, start_bit, nsym, max_len);
-    // records (u16, 16-byte rows); ent, cnt, first, xit (<= nseg chains) (u64); dirty[2] (u32); changed,
-    // end; tiles
-    return (nseg * pg.rcap + 7) / 8 + 2 + 4 * nseg + nseg + 4 + ntiles + 24;
+uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, const Tables& t, int ncu) {
+    return chain_geom(payload_bytes, start_bit, nsym, t.dec_avg_bits, ncu).words;
 }
 
 bool seg_decode_supported(const Tables& t) {
-    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.seg_lds_bytes > 0 && t.dec_max_len <= 32 &&
+    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.dec_max_len <= 32 &&
            t.dec_max_len <= t.dec_k + t.dec_level_bits;
+}
+
+// HZ_CAPTURE_DEBUG=1 (debug): the stream's capture status after each step of the launcher.
+static void cap_check(hipStream_t s, const char* tag) {
+    static const bool on = getenv("HZ_CAPTURE_DEBUG") != nullptr;
+    if (!on) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    const hipError_t e = hipStreamGetCaptureInfo(s, &st, &id);
+    fprintf(stderr, "[hz capture] %-12s status %d (err %d)\n", tag, (int)st, (int)e);
+}
+
+static hipError_t scan_u64(const unsigned long long* v, uint64_t n, unsigned long long* tiles, unsigned long long* out,
+                           hipStream_t s) {
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, v, n, tiles, ~0ull);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
+    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, v, n, (const unsigned long long*)tiles,
+                       out, ~0ull);
+    return hipGetLastError();
 }
 
 hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                                    uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
-                                   unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
-                                   hipStream_t s) {
+                                   unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s) {
     if (nsym == 0) return hipSuccess;
     if (!seg_decode_supported(t)) return hipErrorInvalidValue;
     DecArgs d;
     fill_dec_args(d, t, d_payload, payload_bytes, nsym);
     d.starts = nullptr; d.subs = nullptr; d.out = d_out; d.err = d_err;
     if (d.nwords < 4) return hipErrorInvalidValue;
-    const uint64_t bits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
-    const PieceGeom pg = seg_piece_geom(payload_bytes, start_bit, nsym, t.dec_max_len);
-    // the decoder's waves: as many as its LDS image leaves room for (the image was sized for the
-    // codebook's Kraft estimate, the geometry here for the payload's own bits per codeword)
-    int waves = (int)((kLdsBytes / 4 - t.seg_lds_bytes / 4) / pg.wave_words);
-    waves = waves > kPieceWaves ? kPieceWaves : waves;
-    if (waves < 1) return hipErrorNotSupported;
-    SegArgs y;
-    y.nseg = (bits + kSegBits - 1) / kSegBits;
-    if (y.nseg == 0) return hipErrorInvalidValue;
-    y.rcap = pg.rcap;
+    const ChainGeom g = chain_geom(payload_bytes, start_bit, nsym, t.dec_avg_bits, ncu);
+    if (g.nchains == 0 || g.nchains >= (1ull << 32)) return hipErrorInvalidValue;
+    ChainArgs y;
+    y.nchains = g.nchains; y.cbits = g.cbits; y.pbits = g.pbits; y.start = start_bit;
+    y.bpc = g.bpc; y.cap = g.cap;
+    unsigned long long* sc = d_scratch;
+    y.rec = reinterpret_cast<uint16_t*>(sc + g.off_rec);
+    y.ckpt = sc + g.off_ckpt;
+    unsigned long long* arr = sc + g.off_arr;
+    y.ent = arr; y.xit = arr + g.nchains; y.txit = arr + 2 * g.nchains; y.cnt = arr + 3 * g.nchains;
+    y.tcnt = arr + 4 * g.nchains; y.nblk = arr + 5 * g.nchains; y.first = arr + 6 * g.nchains;
+    y.bbase = arr + 7 * g.nchains;
+    y.hd = reinterpret_cast<uint32_t*>(sc + g.off_u32);
+    y.r0 = y.hd + g.nchains;
+    y.list[0] = reinterpret_cast<uint32_t*>(sc + g.off_list);
+    y.list[1] = y.list[0] + g.nchains;
+    y.lcnt = y.list[1] + g.nchains;
+    y.info = sc + g.off_info;
+    unsigned long long* tiles = sc + g.off_tiles;
+    y.blk = reinterpret_cast<ChainBlk*>(sc + g.off_blk);
     y.err = d_err;
-    unsigned long long* p = d_scratch;
-    y.rec = reinterpret_cast<uint8_t*>(p); p += (y.nseg * y.rcap + 7) / 8 + 2;
-    y.ent = p; p += y.nseg;
-    y.cnt = p; p += y.nseg;
-    y.first = p; p += y.nseg;
-    y.xit = p; p += y.nseg;
-    y.dirty[0] = reinterpret_cast<uint32_t*>(p);
-    y.dirty[1] = y.dirty[0] + y.nseg;
-    p += y.nseg;
-    y.changed = reinterpret_cast<uint32_t*>(p); p += 2;
-    unsigned long long* endw = p; p += 2;
-    unsigned long long* tiles = p;
+    hipError_t e;
+    // lcnt[0..1] = 0; info: blocks 0, largest block 0, end bit ~0
+    if ((e = hipMemsetAsync(y.lcnt, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(y.info, 0, 16, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(y.info + 2, 0xff, 8, s)) != hipSuccess) return e;
+    cap_check(s, "memsets");
     WalkArgs w;
     w.words = d.words; w.nwords = d.nwords; w.bit_adj = d.bit_adj;
-    w.start = start_bit; w.nseg = y.nseg;
+    w.start = start_bit; w.nseg = 0;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
     w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
     w.bmp = nullptr; w.cnt = nullptr; w.ent = nullptr; w.dirty = nullptr;
     // test hook: HZ_SEG_LEAD=<bits> (0: no lead-in, so nearly every chain takes the fix-up path)
     static const uint32_t lead = [] { const char* v = getenv("HZ_SEG_LEAD"); return v ? (uint32_t)atoi(v) : kWalkLead; }();
     w.lead = lead;
-    // 1. walk: chains of spc segments, one per lane
+    // 1. the walk: one chain per lane; small chain counts spread over every CU (fewer waves per workgroup)
     {
-        const uint32_t ring_bytes = kSegWalkWaves * 64 * (kSegRing * 4 + 16);  // rings, record buffers
-        hipError_t e = ensure_lds_limit((const void*)k_seg_walk, (int)ring_bytes);
-        if (e != hipSuccess) return e;
-        const uint64_t target = (uint64_t)kSegWalkWaves * 64 * (uint64_t)ncu;
-        y.spc = (y.nseg + target - 1) / target;
-        y.nchains = (y.nseg + y.spc - 1) / y.spc;
-        const uint64_t wgs = (y.nchains + kSegWalkWaves * 64 - 1) / (kSegWalkWaves * 64);
-        hipLaunchKernelGGL(k_seg_walk, dim3(wgs), dim3(kSegWalkWaves * 64), ring_bytes, s, w, y);
+        uint64_t wpg = (g.nchains + 64ull * ncu - 1) / (64ull * ncu);
+        wpg = wpg < 1 ? 1 : (wpg > (uint64_t)kChainWalkWaves ? (uint64_t)kChainWalkWaves : wpg);
+        const uint32_t threads = (uint32_t)(64 * wpg);
+        const uint32_t ring_bytes = threads * (kSegRing * 4 + 16);  // rings, record buffers
+        if ((e = ensure_lds_limit((const void*)k_chain_walk, (int)(kChainWalkWaves * 64 * (kSegRing * 4 + 16)))) !=
+            hipSuccess)
+            return e;
+        const uint64_t wgs = (g.nchains + threads - 1) / threads;
+        hipLaunchKernelGGL(k_chain_walk, dim3(wgs), dim3(threads), ring_bytes, s, w, y);
+        cap_check(s, "walk");
     }
-    // 2. fix-ups to a fixed point (host loop); then the records' overflow flag
+    // 2. fix-ups: every chain once, then the chains whose predecessor's exit moved, on the device
     {
-        hipError_t e = ensure_lds_limit((const void*)k_seg_fix<DEC_LUT>, kLdsBytes);
-        if (e != hipSuccess) return e;
-        uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
+        if ((e = ensure_lds_limit((const void*)k_chain_fix<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
+        if ((e = ensure_lds_limit((const void*)k_chain_fix_loop<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
+        uint64_t wgs = (g.nchains + kSyncThreads - 1) / kSyncThreads;
         wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
-        for (int it = 0;; ++it) {
-            if ((e = hipMemsetAsync(y.changed, 0, 4, s)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(y.dirty[(it + 1) & 1], 0, 4 * y.nchains, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_seg_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y, start_bit,
-                               it);
-            if ((e = hipMemcpyAsync(h_scratch, y.changed, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-            if ((e = hipMemcpyAsync(h_scratch + 1, d_err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-            if (h_scratch[0] == 0 || it > (int)y.nchains || (h_scratch[1] & 64u)) break;
-        }
-        if (h_scratch[1] & 64u) {  // a segment with more pieces than planned: the caller takes the index path
-            h_scratch[1] &= ~64u;
-            if ((e = hipMemcpyAsync(d_err, h_scratch + 1, 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-            return hipErrorNotSupported;
-        }
+        hipLaunchKernelGGL(k_chain_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
+        hipLaunchKernelGGL(k_chain_fix_loop<DEC_LUT>, dim3(1), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
+        cap_check(s, "fix");
     }
-    // 3. F = exclusive scan of the counts
-    const uint64_t ntiles = (y.nseg + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       tiles);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, 0ull);
-    hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)y.cnt, y.nseg,
-                       (const unsigned long long*)tiles, y.first);
-    // 4. the piece decoder: groups of gs segments, one wave each (persistent)
+    // 3. output index and first decode block of every chain; 4. block descriptors
+    if ((e = scan_u64(y.tcnt, g.nchains, tiles, y.first, s)) != hipSuccess) return e;
+    if ((e = scan_u64(y.nblk, g.nchains, tiles, y.bbase, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_chain_meta, dim3((g.nchains + 255) / 256), dim3(256), 0, s, y);
+    cap_check(s, "scan+meta");
+    // 5. the block decoder: k_decode's slot sizing, two slots per wave, persistent over every CU
     {
-        hipError_t e = ensure_lds_limit((const void*)k_piece_decode, kLdsBytes);
-        if (e != hipSuccess) return e;
-        if ((e = hipMemsetAsync(endw, 0xff, 8, s)) != hipSuccess) return e;
-        PieceArgs z;
-        z.ent = y.ent; z.cnt = y.cnt; z.first = y.first; z.rec = y.rec;
-        z.rcap = pg.rcap; z.gs = pg.gs; z.slot_words = pg.slot_words;
-        z.nseg = y.nseg; z.start = start_bit; z.nsym = nsym; z.end = endw;
-        d.lds_img = t.d_seg_lds;
-        d.lds_words = t.seg_lds_bytes / 4;
-        const uint64_t ngroups = (y.nseg + pg.gs - 1) / pg.gs;
-        uint64_t wgs = (ngroups + waves - 1) / waves;
-        wgs = wgs < (uint64_t)ncu ? wgs : (uint64_t)ncu;
-        const uint32_t lds = 4 * (d.lds_words + (uint32_t)waves * pg.wave_words);
-        hipLaunchKernelGGL(k_piece_decode, dim3(wgs), dim3(waves * 64), lds, s, d, z);
-        if (d_end) {
-            if ((e = hipMemcpyAsync(d_end, endw, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-        }
+        if ((e = ensure_lds_limit((const void*)k_chain_decode, kLdsBytes)) != hipSuccess) return e;
+        const uint64_t nbe = (nsym + kBlockSyms - 1) / kBlockSyms + 1;
+        uint64_t avg = (g.pbits + nbe - 1) / nbe;
+        avg = avg < (uint64_t)kBlockSyms * (uint32_t)d.max_len ? avg : (uint64_t)kBlockSyms * (uint32_t)d.max_len;
+        const uint32_t worst = dec_slot_words_max(d.max_len);
+        uint32_t est = dec_slot_words(avg + avg / 16 + 256, d.max_len);
+        est = est < worst ? est : worst;
+        const uint32_t table = d.lds_words;
+        if (table + worst > kLdsBytes / 4) return hipErrorInvalidValue;
+        uint32_t nslot = (kLdsBytes / 4 - table) / est;
+        nslot = nslot > 2 * kDecPipe2Threads / 64 ? 2 * kDecPipe2Threads / 64 : nslot;
+        nslot &= ~1u;
+        DecArgs b = d;
+        b.region_words = nslot * est;
+        if (b.region_words < 2 * worst && table + 2 * worst <= kLdsBytes / 4) b.region_words = 2 * worst;
+        const int threads = 64 * (int)((nslot / 2) ? nslot / 2 : 1);
+        const uint32_t lds = 4 * (table + b.region_words);
+        hipLaunchKernelGGL(k_chain_decode, dim3(ncu), dim3(threads), lds, s, b, y);
+        cap_check(s, "decode");
+    }
+    // 6. heads, records past the capacity, the end bit
+    {
+        if ((e = ensure_lds_limit((const void*)k_chain_tail<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
+        uint64_t wgs = (g.nchains + kSyncThreads - 1) / kSyncThreads;
+        wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
+        hipLaunchKernelGGL(k_chain_tail<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
+        if (d_end && (e = hipMemcpyAsync(d_end, y.info + 2, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        cap_check(s, "tail+end");
     }
     return hipGetLastError();
 }

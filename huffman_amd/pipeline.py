@@ -13,6 +13,7 @@ PyTorch provides device memory and the stream; every compute stage is a
 gfx950 kernel of libhuffman_amd.so.
 """
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -54,6 +55,22 @@ class Plan:
         return self._header
 
 
+class _PlanKey:
+    """Identity of a histogram's input for its range plan: the very tensor object (a weak
+    reference: a freed tensor whose address the caching allocator hands out again never matches),
+    its view and its in-place version counter."""
+
+    def __init__(self, x):
+        self.ref = weakref.ref(x)
+        self.key = (x.data_ptr(), x.numel(), x._version)
+
+    def __eq__(self, other):
+        if not isinstance(other, _PlanKey):
+            return NotImplemented
+        a, b = self.ref(), other.ref()
+        return a is not None and a is b and self.key == other.key
+
+
 class StreamCodec:
     def __init__(self, device_index=0, use_ranges=True):
         self.device = torch.device("cuda", device_index)
@@ -73,16 +90,25 @@ class StreamCodec:
     # -- stages ---------------------------------------------------------------
     def histogram(self, x, accumulate=False):
         n = x.numel()
-        rb = self.dev.ranges_bytes(n) if self.use_ranges and not accumulate else 0
+        # the range plan needs a 16-byte aligned input (hz_hist16_ranges); offset views take hz_hist16
+        aligned = x.data_ptr() % 16 == 0
+        rb = self.dev.ranges_bytes(n) if self.use_ranges and not accumulate and aligned else 0
         if rb:
             if self.ranges is None or self.ranges.numel() < rb:
                 self.ranges = torch.empty(rb, dtype=torch.uint8, device=self.device)
             self.dev.hist16_ranges(x.data_ptr(), n, self.hist.data_ptr(), self.ranges.data_ptr(), accumulate)
-            self._ranges_of = (x.data_ptr(), n)
+            self._ranges_of = self._ident(x)
         else:
             self.dev.hist16(x.data_ptr(), n, self.hist.data_ptr(), accumulate)
             self._ranges_of = None
         return self.hist
+
+    @staticmethod
+    def _ident(x):
+        """What a range plan is valid for: the same tensor's storage, view and contents (its
+        in-place version counter), so a reused address or an in-place change falls back to
+        count + scan + write instead of packing with stale range starts."""
+        return _PlanKey(x)
 
     def make_plan(self, hist_host, n_total, hist_local=None, first_shard=True, shard_bit_offset=0, last_byte=0,
                   cb=None):
@@ -110,13 +136,15 @@ class StreamCodec:
 
     def pack(self, x, plan, out, index):
         """Pack x; with the range plan of x's histogram (the last histogram() call, same tensor,
-        unchanged since: stream order) in one pass over x, else count + scan + write."""
-        if self._ranges_of == (x.data_ptr(), x.numel()):
+        unchanged since: stream order) in one pass over x, else count + scan + write. A plan is
+        used once. index may be None: no block index is written (the drop-in file path)."""
+        iptr = index.data_ptr() if index is not None else 0
+        if self._ranges_of is not None and self._ranges_of == self._ident(x):
+            self._ranges_of = None
             self.dev.pack_ranges(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
-                                 index.data_ptr(), self.ranges.data_ptr())
+                                 iptr, self.ranges.data_ptr())
         else:
-            self.dev.pack(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),
-                          index.data_ptr())
+            self.dev.pack(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(), iptr)
         return out
 
     def decode(self, payload, nsym, index, out):

@@ -1,7 +1,7 @@
 """The `extract` path without a block index (include/huffman_amd.h
-hz_decode_indexless: a length walk with per-segment entries and counts, the
-segment fix-ups, a count scan and the long-chain decoder) against the inputs it
-must restore and against hz_pack's own index (its end bit). The reference's
+hz_decode_indexless: a length walk of long chains recording every 8th codeword,
+the chain fix-ups, the count scans and the chain-block decoder, all stream-ordered)
+against the inputs it must restore and against hz_pack's own index (its end bit). The reference's
 decoder (Decompressor.cu:259-291) is serial; the CPU oracle pins the same
 streams in test_gpu.py / test_oracle.py, and the golden reference-encoder files
 go through this path via hz.decode (test_gpu.py::test_decode_golden_and_baseline_files).
@@ -109,18 +109,19 @@ print("ok")
 @pytest.mark.parametrize("lead", ["0", "64"])
 def test_indexless_fixups_without_lead_in(built_lib, lead):
     """HZ_SEG_LEAD (test hook) shortens the walk chains' lead-in, so chains start unsynchronised and
-    the segment fix-ups (k_seg_fix) repair them: the file still decodes bit-exact."""
+    the chain fix-ups (k_chain_fix: heads decoded by k_chain_tail) repair them: the file still decodes
+    bit-exact."""
     code = _NO_LEAD.format(root=ROOT, tests=os.path.join(ROOT, "tests"), n=(24 << 20) + 1)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, HZ_SEG_LEAD=lead))
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
-def test_indexless_dense_run_takes_the_index_path(codec):
-    """A long run of the most frequent symbol packs ~1800 codewords into a 4096-bit segment, far
-    more piece records than planned from the stream's average code length: the walk flags it
-    (error bit 64) and hz_decode_indexless decodes through hz_index_build + hz_decode instead;
-    the output and the end bit are the same."""
+def test_indexless_dense_run_past_record_capacity(codec):
+    """A long run of the most frequent symbol (~2 bits per codeword against ~12.5 on average) gives
+    the chains inside it about 5x more records than their capacity (sized from the average code
+    length): the walk stops storing records there and k_chain_tail decodes the rest of each such
+    chain serially. The output and the end bit are exact, and nothing is left on the context."""
     import torch
     rng = np.random.default_rng(11)
     nsym = 8 << 20
@@ -129,15 +130,14 @@ def test_indexless_dense_run_takes_the_index_path(codec):
     x = torch.from_numpy(sym.view(np.uint8).copy()).cuda()
     ok, end_ok = _check(codec, x)
     assert ok and end_ok
-    # and the device context is clean afterwards (the overflow flag was cleared)
+    # and again, moved 3 bytes into a buffer
     ok2, end_ok2 = _check(codec, x, shift=3)
     assert ok2 and end_ok2
 
 
 def test_indexless_skewed_rounds(codec):
-    """90 % of the symbols one value (a 1-bit code): ~2 bits per codeword, ~250 pieces per 4096-bit
-    segment, so a decode group is one segment taking two rounds of 256 pieces, with records up to the
-    segment's last 8th codeword (hundreds per row). The output and end bit are exact."""
+    """90 % of the symbols one value (a 1-bit code): ~2 bits per codeword, so the chains are short in
+    bits and long in codewords (many decode blocks per chain). The output and end bit are exact."""
     import torch
     rng = np.random.default_rng(5)
     nsym = (6 << 20) + 3
@@ -145,3 +145,43 @@ def test_indexless_skewed_rounds(codec):
     x = torch.from_numpy(sym.view(np.uint8).copy()).cuda()
     ok, end_ok = _check(codec, x)
     assert ok and end_ok
+
+
+def test_indexless_graph_capture(codec):
+    """hz_decode_indexless is stream-ordered (no host synchronisation inside, fix-ups iterated on the
+    device): captured into a HIP graph on the context's stream and replayed, it decodes bit-exact. A
+    host sync inside the call would break the capture."""
+    import torch
+    from huffman_amd import index_starts
+    n = (48 << 20) + 2
+    nsym = n // 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=21)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    end_pack = int(index_starts(index.cpu().numpy(), nsym)[-1])
+    out = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    end = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+
+    def call():
+        codec.dev.decode_indexless(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, out.data_ptr(),
+                                   end.data_ptr())
+
+    call()  # eager first: the context's scratch is sized outside the capture
+    codec.sync()
+    assert torch.equal(out[:n], x)
+    out.zero_()
+    end.fill_(-1)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=codec.stream):
+        call()
+    torch.cuda.synchronize()
+    assert not torch.equal(out[:n], x)  # captured, not run
+    for _ in range(2):
+        out.zero_()
+        end.fill_(-1)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[:n], x)
+        assert int(end[0].item()) == end_pack

@@ -29,8 +29,9 @@ from collections import defaultdict
 
 # stage -> (kernels of the stage, kernels that mark one launch of the stage)
 # k_scan_* (count scans) are shared by the three-pass pack, the index builder and the index-less
-# extract: they count toward "extract" (the stage whose dedicated run, tools/debug/extract_loop.py
-# --only-indexless, launches them alone); the range-plan pack has its own k_range_* kernels.
+# extract: they are attributed by launch order, to the stage of the kernel launched before them
+# (SHARED below), not to a fixed stage.
+SHARED = ("k_scan_reduce", "k_scan_tiles", "k_scan_apply")
 STAGES = {
     "hist": (("k_hist16", "k_hist16_rng"), ("k_hist16", "k_hist16_rng")),
     "pack": (("k_pack_count", "k_range_dot", "k_range_scan", "k_pack_write", "k_pack_fixed16", "k_pack_fixed16_blk"),
@@ -39,15 +40,15 @@ STAGES = {
     "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
                "k_sync_subs"),
               ("k_sync_subs", "k_idx_fixed16")),
-    "extract": (("k_seg_walk", "k_seg_fix", "k_piece_decode", "k_scan_reduce", "k_scan_tiles", "k_scan_apply"),
-                ("k_piece_decode",)),
+    "extract": (("k_chain_walk", "k_chain_fix", "k_chain_fix_loop", "k_chain_meta", "k_chain_decode", "k_chain_tail"),
+                ("k_chain_decode",)),
 }
 
 
 # kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
 WIDE_READ = ("k_hist16", "k_hist16_rng", "k_range_dot", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16",
-             "k_pack_fixed16_blk", "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk", "k_seg_walk",
-             "k_piece_decode")
+             "k_pack_fixed16_blk", "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk", "k_chain_walk",
+             "k_chain_decode")
 
 
 def _is(name, k):
@@ -69,10 +70,16 @@ def read_counter(d, counter):
     fixed = defaultdict(set)
     calls = defaultdict(set)
     with open(path) as f:
-        for row in csv.DictReader(f):
-            if row["Counter_Name"] != counter:
-                continue
-            st = stage_of(row["Kernel_Name"])
+        rows = [r for r in csv.DictReader(f) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    last_stage = None
+    for row in rows:
+        if True:
+            if any(_is(row["Kernel_Name"], k) for k in SHARED):
+                st = last_stage  # a count scan belongs to the stage that launched it
+            else:
+                st = stage_of(row["Kernel_Name"])
+                last_stage = st if st is not None else last_stage
             if st is None:
                 continue
             v = float(row["Counter_Value"]) * 1024.0
