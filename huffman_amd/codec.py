@@ -227,6 +227,19 @@ class Device:
         check(self.lib.hz_decode_indexless(self.h, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit),
               "hz_decode_indexless")
 
+    # -- one index-less stream in parts (one per rank; huffman_amd/dist.py decode_indexless_split) -----
+    def indexless_scan(self, d_payload, payload_bytes, start_bit, part_begin, part_end, entry_bit, d_summary):
+        """Walk + fix-ups of payload bits [part_begin, part_end) after start_bit; entry_bit: the part's true
+        entry or 2**64 - 1 (its walked entry). d_summary (device, 3 x u64): codewords, true exit, walked entry."""
+        check(self.lib.hz_indexless_scan(self.h, d_payload, payload_bytes, start_bit, part_begin, part_end,
+                                         entry_bit, d_summary), "hz_indexless_scan")
+
+    def indexless_refix(self, entry_bit, d_summary):
+        check(self.lib.hz_indexless_refix(self.h, entry_bit, d_summary), "hz_indexless_refix")
+
+    def indexless_decode(self, nsym, d_out, d_end_bit=None):
+        check(self.lib.hz_indexless_decode(self.h, nsym, d_out, d_end_bit), "hz_indexless_decode")
+
     def generate(self, d_out, n, offset=0, kind=1, alpha=1.1, seed=42):
         check(self.lib.hz_generate(self.h, d_out, n, offset, kind, alpha, seed), "hz_generate")
 

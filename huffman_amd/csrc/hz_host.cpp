@@ -68,6 +68,7 @@ struct Staging {
 struct hz_ctx {
     int device = 0;
     int ncu = 0;
+    ChainState* chain = nullptr;    // the index-less decoder's phases (hz_decode_indexless, hz_indexless_*)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     Tables t;
@@ -130,6 +131,7 @@ extern "C" int hz_ctx_create(int device, void* stream, hz_ctx** out) {
     std::unique_ptr<hz_ctx> c(new hz_ctx());
     c->device = device;
     c->ncu = prop.multiProcessorCount;
+    c->chain = chain_state_create();
     HZ_TRY(hipSetDevice(device));
     if (stream) {
         c->stream = (hipStream_t)stream;
@@ -156,6 +158,7 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
         if (st->done) (void)hipEventDestroy(st->done);
         (void)hipHostFree(st->p);
     }
+    chain_state_destroy(c->chain);
     (void)hipFree(c->d_desc);
     (void)hipFree(c->d_err);
     (void)hipFree(c->d_thr);
@@ -558,14 +561,57 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
         return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
     // stream-ordered from here: walk, fix-ups, scans, block decode, tails (no host synchronisation
     // unless the context's scratch has to grow)
-    int rc = ensure_scratch(c, seg_scratch_words(payload_bytes, start_bit, nsym, c->t, c->ncu));
+    const uint64_t pbits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
+    int rc = ensure_scratch(c, chain_scratch_words(0, pbits, nsym, c->t, c->ncu));
     if (rc) return rc;
     HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
-    HZ_TRY(launch_decode_indexless(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
-                                   reinterpret_cast<unsigned long long*>(d_end_bit), c->d_desc, c->d_err, c->ncu,
-                                   c->stream));
+    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, start_bit, nsym, 0, pbits, ~0ull, c->d_desc, c->d_err,
+                      c->ncu, c->stream));
+    HZ_TRY(chain_decode(c->chain, c->t, nsym, d_out, reinterpret_cast<unsigned long long*>(d_end_bit), c->ncu,
+                        c->stream));
     HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
     c->ev_used[HZ_STAGE_EXTRACT] = true;
+    return arm_err_check(c);
+}
+
+// ---- one stream over several devices: the index-less decode in parts -----------------
+static int part_summary(hz_ctx* c, uint64_t* d_summary) {
+    if (!d_summary) return HZ_OK;
+    const unsigned long long* info = chain_info(c->chain);
+    if (!info) return HZ_EINVAL;
+    HZ_TRY(hipMemcpyAsync(d_summary, info + 3, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
+    return HZ_OK;
+}
+
+extern "C" int hz_indexless_scan(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                                 uint64_t part_begin, uint64_t part_end, uint64_t entry_bit, uint64_t* d_summary) {
+    if (!c || !d_payload || part_end <= part_begin) return HZ_EINVAL;
+    if (c->t.dec_mode < 0 || !seg_decode_supported(c->t)) return HZ_EINVAL;
+    if (start_bit + part_end > payload_bytes * 8) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    int rc = ensure_scratch(c, chain_scratch_words(part_begin, part_end, 0, c->t, c->ncu));
+    if (rc) return rc;
+    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, start_bit, 0, part_begin, part_end, entry_bit,
+                      c->d_desc, c->d_err, c->ncu, c->stream));
+    if ((rc = part_summary(c, d_summary))) return rc;
+    return arm_err_check(c);
+}
+
+extern "C" int hz_indexless_refix(hz_ctx* c, uint64_t entry_bit, uint64_t* d_summary) {
+    if (!c || !chain_info(c->chain)) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(chain_refix(c->chain, c->t, entry_bit, c->ncu, c->stream));
+    int rc = part_summary(c, d_summary);
+    if (rc) return rc;
+    return arm_err_check(c);
+}
+
+extern "C" int hz_indexless_decode(hz_ctx* c, uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
+    if (!c || !chain_info(c->chain)) return HZ_EINVAL;
+    if (nsym && (!d_out || (((uintptr_t)d_out) & 15))) return HZ_EINVAL;
+    HZ_TRY(hipSetDevice(c->device));
+    HZ_TRY(chain_decode(c->chain, c->t, nsym, d_out, reinterpret_cast<unsigned long long*>(d_end_bit), c->ncu,
+                        c->stream));
     return arm_err_check(c);
 }
 

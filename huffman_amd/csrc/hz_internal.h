@@ -219,13 +219,27 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
                               unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,
                               hipStream_t s);  // synchronises the stream (iterates to a fixed point)
 uint64_t index_scratch_words(uint64_t payload_bytes, uint64_t start_bit);  // u64 words hz_index_build needs
-// Index-less decode in chain blocks (no block index, stream-ordered: no host synchronisation);
-// d_end: the end bit of codeword nsym - 1 (all ones when the payload holds fewer codewords).
+// Index-less decode in chain blocks (hz_kernels.hip; no block index, stream-ordered: no host
+// synchronisation). Phases over a PART of the payload (bits [part_begin, part_end) after start_bit; the
+// whole payload for one device, a slice per rank for one stream split over ranks):
+//   chain_scan   : walk, fix-ups, scans, block descriptors; summary in chain_info (device u64):
+//                  [3] codewords of the part, [4] its true exit bit, [5] its entry bit in use.
+//                  entry0: the part's true entry bit (~0: its walked entry, e.g. the stream's start)
+//   chain_refix  : the fix-ups again from a new true entry (another rank's exit), summary updated
+//   chain_decode : the part's first nsym codewords (nsym: the stream's symbols after the part's first)
+//                  into d_out; d_end: end bit of its codeword nsym - 1 (all ones: not in this part)
+struct ChainState;
+ChainState* chain_state_create();
+void chain_state_destroy(ChainState* st);
 bool seg_decode_supported(const Tables& t);
-hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                                   uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
-                                   unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, const Tables& t, int ncu);
+uint64_t chain_scratch_words(uint64_t part_begin, uint64_t part_end, uint64_t nsym, const Tables& t, int ncu);
+hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                      uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end, uint64_t entry0,
+                      unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
+hipError_t chain_refix(ChainState* st, const Tables& t, uint64_t entry0, int ncu, hipStream_t s);
+hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
+                        int ncu, hipStream_t s);
+const unsigned long long* chain_info(const ChainState* st);
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -3359,8 +3359,10 @@ struct ChainBlk {
 static_assert(sizeof(ChainBlk) == 48, "ChainBlk");
 
 struct ChainArgs {
-    uint64_t nchains, cbits, pbits;  // chain c walks payload bits [c cbits, min((c + 1) cbits, pbits)) after start
+    uint64_t nchains, cbits;         // chain c walks payload bits [pbeg + c cbits, min(pbeg + (c + 1) cbits, pend))
+    uint64_t pbeg, pend;             // the part of the payload (bits after start) these chains cover
     uint64_t start;                  // stream bit of the first symbol
+    uint64_t entry0;                 // true entry of chain 0 (~0: its walked entry -- the stream's start)
     uint32_t bpc, cap;               // decode blocks per chain, records per chain (kChainRecs * bpc)
     uint16_t* rec;                   // [nchains][cap] low 16 bits of the stream bit of chain codeword 8 r
     unsigned long long* ckpt;        // [nchains][bpc + 1] stream bit of record 256 j; after the last block, the exit
@@ -3377,7 +3379,8 @@ struct ChainArgs {
     uint32_t* list[2];               // k_chain_fix_loop: chains to check, ping-pong
     uint32_t* lcnt;                  // [2] their counts
     ChainBlk* blk;                   // [nchains * bpc] decode block descriptors
-    unsigned long long* info;        // [0] decode blocks, [1] largest block (bits), [2] end bit
+    unsigned long long* info;        // [0] decode blocks, [1] largest block (bits), [2] end bit, [3] codewords,
+                                     // [4] true exit of the last chain, [5] entry of chain 0 in use
     uint32_t* err;
 };
 
@@ -3465,8 +3468,8 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = ch < y.nchains;
     const uint64_t chc = live ? ch : 0;
-    const uint64_t cs = chc * y.cbits;
-    const uint64_t ce = cs + y.cbits < y.pbits ? cs + y.cbits : y.pbits;
+    const uint64_t cs = y.pbeg + chc * y.cbits;
+    const uint64_t ce = cs + y.cbits < y.pend ? cs + y.cbits : y.pend;
     const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
     const uint64_t P0 = y.start + a.bit_adj + x0;
     SegFeed fd;
@@ -3571,7 +3574,7 @@ HZ_DEV uint64_t chain_blocks(uint32_t navail, uint32_t r0) {
     return r0 < navail ? nb - j0 : 0;
 }
 
-// Chain i (>= 1) against chain i - 1's true exit (its true entry). When that is not the walked entry,
+// Chain i against chain i - 1's true exit (its true entry; chain 0: entry0). When that is not the walked entry,
 // walk the true path until it lands on one of the chain's records (from there both paths agree):
 // head, first valid record, true count and decode blocks follow. The chain's true exit is its walked
 // exit when a record was met, else where the true path left the chain (the whole chain is head).
@@ -3579,15 +3582,15 @@ HZ_DEV uint64_t chain_blocks(uint32_t navail, uint32_t r0) {
 // checked against a stale entry (another chain's exit moving concurrently) is checked again.
 template <int MODE>
 HZ_DEV bool chain_fix_one(const DecArgs& a, const ChainArgs& y, const uint32_t* lds, uint64_t i) {
-    uint64_t p = y.txit[i - 1];
+    uint64_t p = i ? y.txit[i - 1] : y.entry0;
     const uint64_t n = y.cnt[i];
     const uint32_t nrec = chain_nrec(n), navail = nrec < y.cap ? nrec : y.cap;
     uint32_t rr = 0;
     uint64_t h = 0;
     bool met = p == y.ent[i];
     if (!met) {
-        const uint64_t cend = (i + 1) * y.cbits < y.pbits ? (i + 1) * y.cbits : y.pbits;
-        const uint64_t ce = y.start + cend;
+        const uint64_t cend = y.pbeg + (i + 1) * y.cbits;
+        const uint64_t ce = y.start + (cend < y.pend ? cend : y.pend);
         BitReader r;
         br_init(r, a, p + a.bit_adj);
         uint64_t R = navail ? chain_rec_pos(y, i, 0) : ~0ull;
@@ -3617,20 +3620,22 @@ HZ_DEV bool chain_fix_one(const DecArgs& a, const ChainArgs& y, const uint32_t* 
     return false;
 }
 
-// Every chain once (chain 0 starts on its entry); chains whose predecessor's exit moved go on a list.
+// Every chain once (chain 0 starts on its walked entry unless entry0 says otherwise); chains whose
+// predecessor's exit moved go on a list.
 template <int MODE>
 __global__ __launch_bounds__(kSyncThreads) void k_chain_fix(DecArgs a, ChainArgs y) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < y.nchains; i += stride) {
-        if (i == 0) {
+        if (i == 0 && y.entry0 == ~0ull) {
             const uint64_t n = y.cnt[0];
             const uint32_t nrec = chain_nrec(n);
             y.hd[0] = 0;
             y.r0[0] = 0;
             y.tcnt[0] = n;
             y.nblk[0] = chain_blocks(nrec < y.cap ? nrec : y.cap, 0);
+            y.txit[0] = y.xit[0];
             continue;
         }
         if (chain_fix_one<MODE>(a, y, lds, i) && i + 1 < y.nchains) {
@@ -3670,7 +3675,12 @@ __global__ __launch_bounds__(256) void k_chain_meta(ChainArgs y) {
     uint64_t maxb = 0;
     if (c < y.nchains) {
         const uint64_t nb = y.nblk[c];
-        if (c + 1 == y.nchains) y.info[0] = y.bbase[c] + nb;
+        if (c + 1 == y.nchains) {  // the part's summary
+            y.info[0] = y.bbase[c] + nb;
+            y.info[3] = y.first[c] + y.tcnt[c];
+            y.info[4] = y.txit[c];
+            y.info[5] = y.entry0 != ~0ull ? y.entry0 : y.ent[0];  // the entry in use
+        }
         if (nb) {
             const uint64_t n = y.cnt[c];
             const uint32_t nrec = chain_nrec(n), navail = nrec < y.cap ? nrec : y.cap;
@@ -3897,7 +3907,7 @@ __global__ __launch_bounds__(kSyncThreads) void k_chain_tail(DecArgs a, ChainArg
                 if (o + t == last) y.info[2] = p;
             }
         };
-        if (h) serial(y.txit[c - 1], F, h);  // chain 0 starts on its entry: never a head
+        if (h) serial(c ? y.txit[c - 1] : y.entry0, F, h);
         if (r0 < nrec && nrec > y.cap)      // records past the capacity: the rest of the chain
             serial(y.ckpt[c * (y.bpc + 1) + y.bpc], F + h + 8ull * (y.cap - r0), n - 8ull * y.cap);
         if (has_end && last >= F + h) {     // the end bit inside a piece: walk that piece up to it
@@ -3920,30 +3930,32 @@ __global__ __launch_bounds__(kSyncThreads) void k_chain_tail(DecArgs a, ChainArg
 }
 
 // ---- host side -----------------------------------------------------------------------------
-// Chain geometry: chains of cbits payload bits, about one per walk lane of the device (16 waves per
-// CU), but at least kChainMinBlocks decode blocks long; each chain's record capacity holds its
-// expected records with 25 % headroom (more go to k_chain_tail, serially).
+// Chain geometry of a part of the payload (bits [pbeg, pend) after start): chains of cbits bits, about
+// one per walk lane of the device (16 waves per CU), but at least kChainMinBlocks decode blocks long;
+// each chain's record capacity holds its expected records with 25 % headroom (more go to
+// k_chain_tail, serially). avg: expected payload bits per codeword (the lower of the payload's own
+// and the codebook's Kraft estimate: more records, more headroom).
 constexpr uint64_t kChainMinBlocks = 4;
 struct ChainGeom {
-    uint64_t nchains = 0, cbits = 0, pbits = 0;
+    uint64_t nchains = 0, cbits = 0, pbeg = 0, pend = 0;
     uint32_t bpc = 0, cap = 0;
     uint64_t off_rec, off_ckpt, off_arr, off_u32, off_list, off_info, off_tiles, off_blk, words;
 };
 
-static ChainGeom chain_geom(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, double kraft_bits, int ncu) {
+static ChainGeom chain_geom(uint64_t pbeg, uint64_t pend, double avg, int ncu) {
     ChainGeom g;
-    g.pbits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;
-    if (g.pbits == 0 || nsym == 0) return g;
-    double avg = (double)g.pbits / (double)nsym;  // payload bits per codeword
-    if (kraft_bits > 0.5 && kraft_bits < avg) avg = kraft_bits;  // the lower (more records) of the two
-    if (avg < 1.0) avg = 1.0;
+    g.pbeg = pbeg;
+    g.pend = pend;
+    const uint64_t bits = pend > pbeg ? pend - pbeg : 0;
+    if (bits == 0) return g;
+    if (!(avg >= 1.0)) avg = 1.0;
     const uint64_t lanes = (uint64_t)kChainWalkWaves * 64 * (uint64_t)(ncu > 0 ? ncu : 1);
     const uint64_t minbits = (uint64_t)(kChainMinBlocks * kBlockSyms * avg);
-    uint64_t cb = (g.pbits + lanes - 1) / lanes;
+    uint64_t cb = (bits + lanes - 1) / lanes;
     cb = cb > minbits ? cb : minbits;
     cb = (cb + 127) & ~127ull;
     g.cbits = cb;
-    g.nchains = (g.pbits + cb - 1) / cb;
+    g.nchains = (bits + cb - 1) / cb;
     const double recs = (double)cb / avg / 8.0 * 1.25 + 64.0;
     g.bpc = (uint32_t)((recs + kChainRecs - 1) / kChainRecs);
     g.cap = g.bpc * kChainRecs;
@@ -3955,15 +3967,22 @@ static ChainGeom chain_geom(uint64_t payload_bytes, uint64_t start_bit, uint64_t
     g.off_arr = w;   w += 8 * nc;                               // ent, xit, txit, cnt, tcnt, nblk, first, bbase
     g.off_u32 = w;   w += nc;                                   // hd, r0 (u32)
     g.off_list = w;  w += nc + 1;                               // list[2] (u32), lcnt
-    g.off_info = w;  w += 4;
+    g.off_info = w;  w += 8;
     g.off_tiles = w; w += ntiles + 2;
     g.off_blk = w;   w += nc * g.bpc * (sizeof(ChainBlk) / 8);
     g.words = w + 8;
     return g;
 }
 
-uint64_t seg_scratch_words(uint64_t payload_bytes, uint64_t start_bit, uint64_t nsym, const Tables& t, int ncu) {
-    return chain_geom(payload_bytes, start_bit, nsym, t.dec_avg_bits, ncu).words;
+static double chain_avg(const Tables& t, uint64_t bits, uint64_t nsym) {
+    double avg = nsym ? (double)bits / (double)nsym : t.dec_avg_bits;
+    if (t.dec_avg_bits > 0.5 && t.dec_avg_bits < avg) avg = t.dec_avg_bits;
+    return avg;
+}
+
+uint64_t chain_scratch_words(uint64_t part_begin, uint64_t part_end, uint64_t nsym, const Tables& t, int ncu) {
+    return chain_geom(part_begin, part_end, chain_avg(t, part_end > part_begin ? part_end - part_begin : 0, nsym), ncu)
+        .words;
 }
 
 bool seg_decode_supported(const Tables& t) {
@@ -3971,7 +3990,7 @@ bool seg_decode_supported(const Tables& t) {
            t.dec_max_len <= t.dec_k + t.dec_level_bits;
 }
 
-// HZ_CAPTURE_DEBUG=1 (debug): the stream's capture status after each step of the launcher.
+// HZ_CAPTURE_DEBUG=1 (debug): the stream's capture status after each step of the launchers.
 static void cap_check(hipStream_t s, const char* tag) {
     static const bool on = getenv("HZ_CAPTURE_DEBUG") != nullptr;
     if (!on) return;
@@ -3991,19 +4010,55 @@ static hipError_t scan_u64(const unsigned long long* v, uint64_t n, unsigned lon
     return hipGetLastError();
 }
 
-hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                                   uint64_t start_bit, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
-                                   unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s) {
-    if (nsym == 0) return hipSuccess;
-    if (!seg_decode_supported(t)) return hipErrorInvalidValue;
-    DecArgs d;
-    fill_dec_args(d, t, d_payload, payload_bytes, nsym);
-    d.starts = nullptr; d.subs = nullptr; d.out = d_out; d.err = d_err;
-    if (d.nwords < 4) return hipErrorInvalidValue;
-    const ChainGeom g = chain_geom(payload_bytes, start_bit, nsym, t.dec_avg_bits, ncu);
-    if (g.nchains == 0 || g.nchains >= (1ull << 32)) return hipErrorInvalidValue;
+// The state a chain decode keeps between its phases (scan, refix, decode): geometry, kernel arguments
+// (device pointers into the context's scratch and tables), the part's summary in y.info.
+struct ChainState {
+    ChainGeom g;
     ChainArgs y;
-    y.nchains = g.nchains; y.cbits = g.cbits; y.pbits = g.pbits; y.start = start_bit;
+    DecArgs d;
+    WalkArgs w;
+    unsigned long long* tiles = nullptr;  // scan scratch
+    bool valid = false;
+};
+ChainState* chain_state_create() { return new ChainState(); }
+void chain_state_destroy(ChainState* st) { delete st; }
+const unsigned long long* chain_info(const ChainState* st) { return st->valid ? st->y.info : nullptr; }
+
+// fix-ups (every chain once, then the listed ones on one workgroup), the scans and the descriptors
+static hipError_t chain_fix_and_meta(ChainState* st, const Tables& t, int ncu, hipStream_t s) {
+    ChainArgs& y = st->y;
+    hipError_t e;
+    if ((e = hipMemsetAsync(y.lcnt, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(y.info, 0, 16, s)) != hipSuccess) return e;  // blocks, largest block (atomicMax)
+    if ((e = ensure_lds_limit((const void*)k_chain_fix<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
+    if ((e = ensure_lds_limit((const void*)k_chain_fix_loop<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
+    uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
+    wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
+    hipLaunchKernelGGL(k_chain_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, st->d, y);
+    hipLaunchKernelGGL(k_chain_fix_loop<DEC_LUT>, dim3(1), dim3(kSyncThreads), t.dec_lds_bytes, s, st->d, y);
+    cap_check(s, "fix");
+    if ((e = scan_u64(y.tcnt, y.nchains, st->tiles, y.first, s)) != hipSuccess) return e;
+    if ((e = scan_u64(y.nblk, y.nchains, st->tiles, y.bbase, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_chain_meta, dim3((y.nchains + 255) / 256), dim3(256), 0, s, y);
+    cap_check(s, "scan+meta");
+    return hipGetLastError();
+}
+
+hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                      uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end, uint64_t entry0,
+                      unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s) {
+    st->valid = false;
+    if (!seg_decode_supported(t)) return hipErrorInvalidValue;
+    DecArgs& d = st->d;
+    fill_dec_args(d, t, d_payload, payload_bytes, nsym);
+    d.starts = nullptr; d.subs = nullptr; d.out = nullptr; d.err = d_err;
+    if (d.nwords < 4) return hipErrorInvalidValue;
+    const ChainGeom& g = st->g = chain_geom(part_begin, part_end,
+                                             chain_avg(t, part_end > part_begin ? part_end - part_begin : 0, nsym), ncu);
+    if (g.nchains == 0 || g.nchains >= (1ull << 32)) return hipErrorInvalidValue;
+    ChainArgs& y = st->y;
+    y.nchains = g.nchains; y.cbits = g.cbits; y.pbeg = g.pbeg; y.pend = g.pend; y.start = start_bit;
+    y.entry0 = entry0;
     y.bpc = g.bpc; y.cap = g.cap;
     unsigned long long* sc = d_scratch;
     y.rec = reinterpret_cast<uint16_t*>(sc + g.off_rec);
@@ -4018,16 +4073,10 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     y.list[1] = y.list[0] + g.nchains;
     y.lcnt = y.list[1] + g.nchains;
     y.info = sc + g.off_info;
-    unsigned long long* tiles = sc + g.off_tiles;
     y.blk = reinterpret_cast<ChainBlk*>(sc + g.off_blk);
     y.err = d_err;
-    hipError_t e;
-    // lcnt[0..1] = 0; info: blocks 0, largest block 0, end bit ~0
-    if ((e = hipMemsetAsync(y.lcnt, 0, 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(y.info, 0, 16, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(y.info + 2, 0xff, 8, s)) != hipSuccess) return e;
-    cap_check(s, "memsets");
-    WalkArgs w;
+    st->tiles = sc + g.off_tiles;
+    WalkArgs& w = st->w;
     w.words = d.words; w.nwords = d.nwords; w.bit_adj = d.bit_adj;
     w.start = start_bit; w.nseg = 0;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
@@ -4036,6 +4085,7 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
     // test hook: HZ_SEG_LEAD=<bits> (0: no lead-in, so nearly every chain takes the fix-up path)
     static const uint32_t lead = [] { const char* v = getenv("HZ_SEG_LEAD"); return v ? (uint32_t)atoi(v) : kWalkLead; }();
     w.lead = lead;
+    hipError_t e;
     // 1. the walk: one chain per lane; small chain counts spread over every CU (fewer waves per workgroup)
     {
         uint64_t wpg = (g.nchains + 64ull * ncu - 1) / (64ull * ncu);
@@ -4049,26 +4099,32 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
         hipLaunchKernelGGL(k_chain_walk, dim3(wgs), dim3(threads), ring_bytes, s, w, y);
         cap_check(s, "walk");
     }
-    // 2. fix-ups: every chain once, then the chains whose predecessor's exit moved, on the device
-    {
-        if ((e = ensure_lds_limit((const void*)k_chain_fix<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
-        if ((e = ensure_lds_limit((const void*)k_chain_fix_loop<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
-        uint64_t wgs = (g.nchains + kSyncThreads - 1) / kSyncThreads;
-        wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
-        hipLaunchKernelGGL(k_chain_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
-        hipLaunchKernelGGL(k_chain_fix_loop<DEC_LUT>, dim3(1), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
-        cap_check(s, "fix");
-    }
-    // 3. output index and first decode block of every chain; 4. block descriptors
-    if ((e = scan_u64(y.tcnt, g.nchains, tiles, y.first, s)) != hipSuccess) return e;
-    if ((e = scan_u64(y.nblk, g.nchains, tiles, y.bbase, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_chain_meta, dim3((g.nchains + 255) / 256), dim3(256), 0, s, y);
-    cap_check(s, "scan+meta");
-    // 5. the block decoder: k_decode's slot sizing, two slots per wave, persistent over every CU
-    {
+    // 2.-4. fix-ups, scans, block descriptors and the part's summary
+    if ((e = chain_fix_and_meta(st, t, ncu, s)) != hipSuccess) return e;
+    st->valid = true;
+    return hipSuccess;
+}
+
+hipError_t chain_refix(ChainState* st, const Tables& t, uint64_t entry0, int ncu, hipStream_t s) {
+    if (!st->valid) return hipErrorInvalidValue;
+    st->y.entry0 = entry0;
+    return chain_fix_and_meta(st, t, ncu, s);
+}
+
+hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
+                        int ncu, hipStream_t s) {
+    if (!st->valid) return hipErrorInvalidValue;
+    DecArgs d = st->d;
+    const ChainArgs& y = st->y;
+    d.out = d_out;
+    d.nsym = nsym;
+    hipError_t e;
+    if ((e = hipMemsetAsync(y.info + 2, 0xff, 8, s)) != hipSuccess) return e;  // end bit: not found
+    if (nsym) {
+        // 5. the block decoder: k_decode's slot sizing, two slots per wave, persistent over every CU
         if ((e = ensure_lds_limit((const void*)k_chain_decode, kLdsBytes)) != hipSuccess) return e;
-        const uint64_t nbe = (nsym + kBlockSyms - 1) / kBlockSyms + 1;
-        uint64_t avg = (g.pbits + nbe - 1) / nbe;
+        const uint64_t bits = st->g.pend - st->g.pbeg;
+        uint64_t avg = (uint64_t)(chain_avg(t, bits, nsym) * kBlockSyms);  // expected block bits
         avg = avg < (uint64_t)kBlockSyms * (uint32_t)d.max_len ? avg : (uint64_t)kBlockSyms * (uint32_t)d.max_len;
         const uint32_t worst = dec_slot_words_max(d.max_len);
         uint32_t est = dec_slot_words(avg + avg / 16 + 256, d.max_len);
@@ -4085,16 +4141,14 @@ hipError_t launch_decode_indexless(const Tables& t, const uint8_t* d_payload, ui
         const uint32_t lds = 4 * (table + b.region_words);
         hipLaunchKernelGGL(k_chain_decode, dim3(ncu), dim3(threads), lds, s, b, y);
         cap_check(s, "decode");
-    }
-    // 6. heads, records past the capacity, the end bit
-    {
+        // 6. heads, records past the capacity, the end bit
         if ((e = ensure_lds_limit((const void*)k_chain_tail<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
-        uint64_t wgs = (g.nchains + kSyncThreads - 1) / kSyncThreads;
+        uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
         wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
         hipLaunchKernelGGL(k_chain_tail<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
-        if (d_end && (e = hipMemcpyAsync(d_end, y.info + 2, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-        cap_check(s, "tail+end");
     }
+    if (d_end && (e = hipMemcpyAsync(d_end, y.info + 2, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    cap_check(s, "tail+end");
     return hipGetLastError();
 }
 

@@ -201,3 +201,61 @@ def reassemble_on_device(payload, local_bytes, word0, dst=0, group=None, via_hos
             seg = out[4 * w0[r]:4 * w0[r] + head_n[r]]
             seg.bitwise_or_(heads[r, :head_n[r]])
     return out, total
+
+
+# ---- one index-less stream decoded by every rank ----------------------------------
+# A reference `.compressed` payload carries no index (Compressor.cu:427-601) and the reference decodes
+# it serially (Decompressor.cu:259-291). Split over ranks, every rank decodes one PART of the payload
+# bits, found by self-synchronisation: rank r walks its part from 1024 bits before it (its walked
+# entry is the first codeword start on that path at or after the part's first bit), counts its
+# codewords and finds its exit (the first codeword start at or after its end). The true entry of
+# rank r is rank r - 1's true exit: one all-gather of (codewords, exit, entry used) per round; a rank
+# whose entry disagrees walks again from the true one (its exit may move, so rounds repeat: at most
+# world - 1, typically none). Rank r's first output symbol is the sum of the codewords before it.
+
+UNKNOWN_ENTRY = (1 << 64) - 1
+
+
+def part_range(payload_bits, world, rank, align=128):
+    """Payload bits [begin, end) (after the stream's first bit) of rank `rank`'s part: equal parts,
+    boundaries on `align` bits, the last part takes the rest."""
+    per = (payload_bits // world) // align * align
+    beg = per * rank
+    end = payload_bits if rank == world - 1 else beg + per
+    return beg, end
+
+
+def decode_indexless_split(scan, refix, decode, nsym, device, group=None):
+    """The exchange of a split index-less decode. Per-rank engines (every bit a stream bit, the same
+    coordinates on every rank):
+      scan() -> (codewords, exit, walked entry) of this rank's part (rank 0: from the stream's start)
+      refix(entry) -> (codewords, exit, entry) of the part walked from a given true entry
+      decode(first, nsym_from_first) -> decodes the part's codewords (at most nsym_from_first)
+    On the GPU these are hz_indexless_scan / hz_indexless_refix / hz_indexless_decode (bench.py,
+    tests/test_gpu_dist.py); tests/test_dist.py drives the same exchange with the CPU oracle's walk.
+    Returns (first symbol of this rank, its codewords, rounds of refixes)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    count, exit_, entry = scan()
+    rounds = 0
+    while True:
+        mine = torch.tensor([count, exit_ & ((1 << 63) - 1), exit_ >> 63, entry & ((1 << 63) - 1), entry >> 63],
+                            dtype=torch.int64, device=device)
+        allv = torch.zeros(world * 5, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(allv, mine, group=group)
+        v = allv.view(world, 5).cpu().tolist()
+        counts = [int(x[0]) for x in v]
+        exits = [int(x[1]) | (int(x[2]) << 63) for x in v]
+        entries = [int(x[3]) | (int(x[4]) << 63) for x in v]
+        stale = [r for r in range(1, world) if entries[r] != exits[r - 1]]
+        if not stale:
+            break
+        if rounds >= world:  # a change moves one part per round: cannot happen
+            raise RuntimeError("decode_indexless_split: exits did not settle")
+        rounds += 1
+        if rank in stale:
+            count, exit_, entry = refix(exits[rank - 1])
+    first = sum(counts[:rank])
+    take = max(0, min(count, nsym - first))
+    decode(first, take)
+    return first, count, rounds

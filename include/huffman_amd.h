@@ -215,18 +215,44 @@ int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes
 /* Decode the first nsym codewords of an index-less stream (a .compressed file
  * from the reference encoder; Decompressor.cu:259-291 decodes it serially) into
  * d_out (2*nsym bytes, 16-byte aligned) with no block index: a length walk of
- * long chains over the payload (per 4096-bit segment: its first codeword start,
- * its codeword count and the start of every 8th codeword), then a block-parallel
- * decode of 8-codeword pieces placed by the scanned counts. *d_end_bit (device
- * u64, optional) receives the end bit of codeword nsym - 1, counted from byte 0
- * of d_payload; a payload with fewer than nsym codewords leaves it at UINT64_MAX
- * (past payload_bytes * 8) with undefined output (the caller checks, as
- * `extract` does). Codebooks the piece decoder does not take (codes longer than
- * 22 bits, DENSE / FIXED16 tables), and payloads whose segments hold more
- * codewords than it planned for, go through hz_index_build + hz_decode, with the
- * same result. Synchronises the stream. */
+ * long chains over the payload (one chain per lane, recording the start of every
+ * 8th codeword of the chain), device-side fix-ups of chains whose lead-in had not
+ * resynchronised, then k_decode's block decoder over the chains' 2048-codeword
+ * blocks placed by the scanned counts. *d_end_bit (device u64, optional)
+ * receives the end bit of codeword nsym - 1, counted from byte 0 of d_payload; a
+ * payload with fewer than nsym codewords leaves it at UINT64_MAX (past
+ * payload_bytes * 8) with undefined output (the caller checks, as `extract`
+ * does). Stream-ordered: no host synchronisation (a HIP graph can capture it)
+ * unless the context's scratch grows. Codebooks the chain decoder does not take
+ * (codes longer than 22 bits, DENSE / FIXED16 tables) go through hz_index_build
+ * + hz_decode, with the same result (that path synchronises). */
 int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                         uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
+
+/* ---- one index-less stream over several devices ------------
+ * The same decode in PARTS: every device (rank) decodes the payload bits
+ * [part_begin, part_end) (counted after start_bit) of one stream, found by
+ * self-synchronisation; the parts then exchange three numbers (huffman_amd/
+ * dist.py decode_indexless_split):
+ *   hz_indexless_scan : walk and fix-ups of the part's chains. entry_bit: the
+ *       part's true first codeword start if known, else UINT64_MAX (its walked
+ *       entry: right for the stream's first part, and for every part whose
+ *       lead-in resynchronised). d_summary (device, 3 x u64): codewords of the
+ *       part, its true exit bit (the next part's true entry), the entry bit in
+ *       use (entry_bit, or the walked entry for UINT64_MAX). Bits are stream bits from byte 0 of d_payload, which must hold the
+ *       part plus 1024 bits before it and max_len bits after it.
+ *   hz_indexless_refix : the part again from its true entry (the previous
+ *       part's exit, when it differs from the walked entry); d_summary updated.
+ *   hz_indexless_decode : the part's codewords into d_out (2 bytes each, from
+ *       the part's first codeword), at most nsym of them (the stream's symbols
+ *       from the part's first on); *d_end_bit as hz_decode_indexless when the
+ *       stream's last codeword falls in this part.
+ * The three calls use the context's scratch: one part per context at a time.
+ * Codebooks as hz_decode_indexless's chain path only (HZ_EINVAL otherwise). */
+int hz_indexless_scan(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                      uint64_t part_begin, uint64_t part_end, uint64_t entry_bit, uint64_t *d_summary);
+int hz_indexless_refix(hz_ctx *ctx, uint64_t entry_bit, uint64_t *d_summary);
+int hz_indexless_decode(hz_ctx *ctx, uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
 
 /* Kernel timings of the last hz_hist16 / hz_pack / hz_decode / hz_index_build /
  * hz_decode_indexless call on this context, in milliseconds (HIP events on the

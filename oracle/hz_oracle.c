@@ -415,3 +415,48 @@ void hzo_gen(uint8_t *out, uint64_t n, uint64_t offset, int kind, uint64_t seed,
         out[j] = (uint8_t)lo;
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* The serial codeword walk of translateFile (Decompressor.cu:262-284) over a bare payload, started at
+ * any stream bit: codewords are decoded from bit `pos` (a trie of the codebook, MSB-first bits of
+ * payload byte 0 onwards) while the position is below `end` and fewer than max_count were taken;
+ * symbols go to out (2 bytes LE each) when out is not NULL. Returns the number of codewords and sets
+ * *exit to the bit after the last one (a walk started mid-codeword follows whatever path the bits
+ * give: Huffman codes resynchronise). The checker of the per-part index-less decode
+ * (huffman_amd/dist.py decode_indexless_split, tests/test_dist.py). -1: allocation failed or a code
+ * the trie does not hold. */
+int64_t hzo_walk(const uint8_t *payload, uint64_t nbytes, const uint8_t *len, const uint64_t *code, uint64_t pos,
+                 uint64_t end, uint64_t max_count, uint8_t *out, uint64_t *exit)
+{
+    uint64_t maxn = 1 + 65536ull * HZO_MAXLEN;
+    int32_t *child = (int32_t *)malloc(sizeof(int32_t) * 2 * maxn);
+    int32_t *sym = (int32_t *)malloc(sizeof(int32_t) * maxn);
+    if (!child || !sym) { free(child); free(sym); return -1; }
+    memset(child, 0xff, sizeof(int32_t) * 2 * maxn);
+    uint64_t nn = 1;
+    for (uint32_t s = 0; s < 65536; ++s) {
+        if (!len[s]) continue;
+        uint64_t v = 0;
+        for (int b = len[s] - 1; b >= 0; --b) {
+            uint32_t bit = (uint32_t)((code[s] >> b) & 1);
+            if (child[2 * v + bit] < 0) { child[2 * v + bit] = (int32_t)nn; nn++; }
+            v = (uint64_t)child[2 * v + bit];
+        }
+        sym[v] = (int32_t)s;
+    }
+    hzo_br r = {payload, nbytes, pos, 0};
+    int64_t n = 0;
+    while (r.bit < end && (uint64_t)n < max_count) {
+        uint64_t v = 0;
+        while (child[2 * v] >= 0 || child[2 * v + 1] >= 0) {
+            uint32_t bit = br_bit(&r);             /* past the payload: zeros */
+            if (child[2 * v + bit] < 0) { free(child); free(sym); return -1; }
+            v = (uint64_t)child[2 * v + bit];
+        }
+        if (out) { out[2 * n] = (uint8_t)(sym[v] & 0xff); out[2 * n + 1] = (uint8_t)((sym[v] >> 8) & 0xff); }
+        ++n;
+    }
+    *exit = r.bit;
+    free(child); free(sym);
+    return n;
+}

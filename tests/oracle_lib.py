@@ -35,6 +35,8 @@ def load():
     lib.hzo_encoded_bits.argtypes = [U64, ctypes.c_uint32, P, P, ctypes.POINTER(U64)]
     lib.hzo_encoded_bits.restype = U64
     lib.hzo_zipf_thresholds.argtypes = [ctypes.c_double, P]
+    lib.hzo_walk.argtypes = [P, U64, P, P, U64, U64, U64, P, ctypes.POINTER(U64)]
+    lib.hzo_walk.restype = ctypes.c_int64
     lib.hzo_gen.argtypes = [P, U64, U64, ctypes.c_int, U64, P]
     I64 = ctypes.c_int64
     lib.hzl_archive.argtypes = [P, U64, P, ctypes.c_uint32, P, P, P, U64, P, ctypes.POINTER(I64), ctypes.POINTER(I64)]
@@ -171,3 +173,18 @@ def generate(n, offset=0, kind=1, seed=42, alpha=1.1):
 def ref_binary(name):
     p = os.path.join(REF_DIR, name)
     return p if os.path.exists(p) else None
+
+
+def walk(payload, ln, code, pos, end, max_count=(1 << 63), decode=False):
+    """hzo_walk: codewords from stream bit pos (any bit) while below end; (count, exit bit, symbols or None)."""
+    lib = load()
+    p = as_u8(payload)
+    ln = np.ascontiguousarray(ln, dtype=np.uint8)
+    code = np.ascontiguousarray(code, dtype=np.uint64)
+    cap = min(max_count, (max(end - pos, 0) + 1))
+    out = np.zeros(2 * cap + 2, dtype=np.uint8) if decode else None
+    ex = ctypes.c_uint64()
+    n = lib.hzo_walk(_p(p), p.size, _p(ln), _p(code), pos, end, max_count, _p(out) if decode else None, ctypes.byref(ex))
+    if n < 0:
+        raise RuntimeError("hzo_walk failed")
+    return n, ex.value, (out[:2 * n] if decode else None)

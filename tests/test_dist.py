@@ -142,3 +142,64 @@ def test_subgroups_use_global_ranks(tmp_path):
                        start_method="spawn")
     for k in (0, 1):
         assert (tmp_path / f"g{k}.txt").read_text() == "ok"
+
+
+def _split_worker(rank, world, port, n_total, kind, lead, result_path):
+    """One index-less stream (the oracle's encoding: no index, reference format) decoded in parts, one
+    per rank (huffman_amd/dist.py decode_indexless_split). The per-part engine here is the oracle's
+    serial walk (no GPU); on the GPU the same exchange drives hz_indexless_scan/refix/decode
+    (tests/test_gpu_dist.py). `lead`: lead-in bits before a part (0: every rank but 0 starts
+    mid-codeword, so the refix rounds run)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from huffman_amd import dist as hd
+        data = oracle_lib.generate(n_total, offset=0, kind=kind, seed=23)
+        blob = oracle_lib.encode(data)
+        _, ln, code, info = oracle_lib.parse_header(blob)
+        nsym = info[0] // 2
+        pay = np.frombuffer(blob, dtype=np.uint8)[info[1]:]
+        start = info[2]
+        beg, end = hd.part_range(pay.size * 8 - start, world, rank)
+        st = {}
+
+        def scan():
+            e = start + beg
+            if rank > 0:  # the lead-in walk lands on the first codeword start >= the part's first bit
+                _, e, _ = oracle_lib.walk(pay, ln, code, start + beg - min(lead, beg), start + beg)
+            n, x, _ = oracle_lib.walk(pay, ln, code, e, start + end)
+            st["entry"] = e
+            return n, x, e
+
+        def refix(entry):
+            n, x, _ = oracle_lib.walk(pay, ln, code, entry, start + end)
+            st["entry"] = entry
+            return n, x, entry
+
+        def decode(first, take):
+            _, _, syms = oracle_lib.walk(pay, ln, code, st["entry"], start + end, max_count=max(take, 0), decode=True)
+            st["out"] = (first, syms[:2 * take].tobytes())
+
+        first, count, rounds = hd.decode_indexless_split(scan, refix, decode, nsym, torch.device("cpu"))
+        parts = [None] * world
+        dist.all_gather_object(parts, (st["out"][0], st["out"][1], rounds))
+        if rank == 0:
+            got = b"".join(p[1] for p in sorted(parts, key=lambda p: p[0]))
+            ok = got == data[:2 * nsym].tobytes() and all(p[2] == parts[0][2] for p in parts)
+            if lead == 0 and world > 1:
+                ok = ok and parts[0][2] >= 1  # the refix rounds ran
+            with open(result_path, "w") as f:
+                f.write("ok" if ok else f"mismatch rounds={parts[0][2]} len={len(got)}/{2 * nsym}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,kind,lead", [(2, 300001, 1, 1024), (3, 1 << 20, 1, 1024), (3, 200000, 1, 0),
+                                                     (8, (1 << 20) + 7, 1, 1024), (8, 1 << 19, 0, 0),
+                                                     (8, 400002, 1, 0)])
+def test_indexless_split_over_ranks(tmp_path, world, n_total, kind, lead):
+    result = str(tmp_path / "result.txt")
+    mp.start_processes(_split_worker, args=(world, _free_port(), n_total, kind, lead, result), nprocs=world, join=True,
+                       start_method="spawn")
+    assert open(result).read() == "ok"

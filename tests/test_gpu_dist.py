@@ -157,3 +157,78 @@ def test_bench_rehearsal_eight_ranks_1gib_shards(tmp_path, dist_kind):
     assert re["whole_stream_decoded_bit_exact"]
     if dist_kind == "uniform":
         assert line["config"]["payload_bytes_rank0"] > (1 << 30) + 4  # a shard body spans two messages
+
+
+def _split_worker(rank, world, port, n_total, lead, result_dir):
+    """One index-less stream decoded by `world` ranks on one GPU, one part each, through
+    hz_indexless_scan / hz_indexless_refix / hz_indexless_decode and the exchange of
+    huffman_amd/dist.py decode_indexless_split (gloo here; RCCL on a multi-GPU node)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if lead is not None:
+        os.environ["HZ_SEG_LEAD"] = str(lead)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    status = "error"
+    try:
+        from huffman_amd import dist as hd
+        from huffman_amd.pipeline import StreamCodec
+        codec = StreamCodec(0)
+        dev = codec.device
+        x = torch.empty(n_total, dtype=torch.uint8, device=dev)
+        codec.dev.generate(x.data_ptr(), n_total, offset=0, kind=1, alpha=1.1, seed=7)
+        plan, payload, _ = codec.encode(x)  # every rank holds the whole stream (as read from one file)
+        codec.sync()
+        nsym = n_total // 2
+        pbits = payload.numel() * 8 - plan.start_bit
+        beg, end = hd.part_range(pbits, world, rank)
+        summ = torch.zeros(4, dtype=torch.int64, device=dev)
+
+        def read():
+            codec.sync()
+            v = [int(t) & ((1 << 64) - 1) for t in summ[:3].cpu().tolist()]
+            return v[0], v[1], v[2]
+
+        def scan():
+            entry = plan.start_bit if rank == 0 else hd.UNKNOWN_ENTRY
+            codec.dev.indexless_scan(payload.data_ptr(), payload.numel(), plan.start_bit, beg, end, entry,
+                                     summ.data_ptr())
+            return read()
+
+        def refix(entry):
+            codec.dev.indexless_refix(entry, summ.data_ptr())
+            return read()
+
+        out = torch.zeros(2 * nsym + 16, dtype=torch.uint8, device=dev)
+        endb = torch.zeros(2, dtype=torch.int64, device=dev)
+
+        def decode(first, take):
+            codec.dev.indexless_decode(take, out.data_ptr(), endb.data_ptr())
+            codec.sync()
+
+        first, count, rounds = hd.decode_indexless_split(scan, refix, decode, nsym, torch.device("cpu"))
+        take = max(0, min(count, nsym - first))
+        ok = torch.equal(out[:2 * take], x[2 * first:2 * (first + take)])
+        flags = torch.tensor([0 if ok else 1, rounds, take], dtype=torch.int64)
+        allf = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allf, flags)
+        total = sum(int(f[2]) for f in allf)
+        status = "ok" if all(int(f[0]) == 0 for f in allf) and total == nsym else f"bad {[f.tolist() for f in allf]}"
+        if lead == 0 and rank == 0:
+            status += f" rounds={rounds}"
+    finally:
+        with open(os.path.join(result_dir, f"r{rank}.txt"), "w") as f:
+            f.write(status)
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n_total,lead", [(2, (8 << 20) + 2, None), (3, (24 << 20) + 6, None),
+                                                (8, (64 << 20) + 2, None), (4, (16 << 20) + 2, 0)])
+def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead):
+    mp.start_processes(_split_worker, args=(world, _free_port(), n_total, lead, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        assert open(tmp_path / f"r{r}.txt").read().startswith("ok"), open(tmp_path / f"r{r}.txt").read()
