@@ -74,19 +74,7 @@ HZ_DEV uint32_t dpp0(uint32_t v) {
 }
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
 constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
-#ifndef HZ_DEC_HOT_OOB
-#define HZ_DEC_HOT_OOB 1  // 10.30-10.32 vs 10.38-10.43 ms at 16 GiB Zipf (round 3 A/B)
-#endif
-#ifndef HZ_DEC_SMEM
-#define HZ_DEC_SMEM 1  // decode: block bounds through the scalar cache (10.04-10.23 vs 10.27-10.33 ms, round 3)
-#endif
-#ifndef HZ_UNIFORM_WID
-#define HZ_UNIFORM_WID 1
-#endif
-#ifndef HZ_FIXED16_BLK
-#define HZ_FIXED16_BLK 1
-#endif
-constexpr bool kFixed16Blk = HZ_FIXED16_BLK;  // FIXED16 streams: the 1 KiB-coalesced full-block kernels
+constexpr bool kFixed16Blk = true;  // FIXED16 streams: the 1 KiB-coalesced full-block kernels
 
 // Inclusive prefix sum over the 64 lanes.
 HZ_DEV uint32_t wave_incl_sum(uint32_t v) {
@@ -108,11 +96,7 @@ HZ_DEV uint32_t lds_at(uint32_t byte) { return *reinterpret_cast<lds_cu32*>(byte
 // The wave's index in its workgroup as a wave-uniform (SGPR) value: block numbers derived from it,
 // and the index / start loads they address, stay on the scalar unit.
 HZ_DEV uint32_t wave_id() {
-#if HZ_UNIFORM_WID
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#else
-    return threadIdx.x >> 6;
-#endif
 }
 
 HZ_DEV uint64_t wave_sum_u64(uint64_t v) {
@@ -238,17 +222,15 @@ HZ_DEV void hist_count8(uint32_t* lds, unsigned long long* hist, const uint4& v,
 }
 
 // Vectors [i0, end) of in4 with stride `step` from this thread's i0: software pipelined over
-// HZ_HIST_DEPTH register buffers (no copies). One workgroup per CU leaves 16 waves to cover
+// kHistDepth register buffers (no copies). One workgroup per CU leaves 16 waves to cover
 // HBM latency, so each lane keeps DEPTH - 1 loads in flight while one vector's LDS atomics
 // run (loads and LDS ops use separate counters). Refills past the end re-read the last
 // vector (branch-free, so the waits stay vmcnt(DEPTH - 1)); the tail counts what is left.
-#ifndef HZ_HIST_DEPTH
-#define HZ_HIST_DEPTH 8
-#endif
+constexpr int kHistDepth = 8;
 template <typename Rec = NoRec>
 HZ_DEV void hist_sweep(uint32_t* lds, unsigned long long* hist, const uint4* in4, uint64_t i, uint64_t end,
                        uint64_t step, Rec rec = Rec()) {
-    constexpr int D = HZ_HIST_DEPTH;
+    constexpr int D = kHistDepth;
     if (i >= end) return;
     const uint64_t last = end - 1;
     uint4 v[D];
@@ -704,15 +686,11 @@ HZ_DEV void pack_emit_lds(const typename PackEnt<MODE>::T (&e)[kSPT], uint64_t& 
     }
 }
 
-#ifndef HZ_PACK_MAXW
-#define HZ_PACK_MAXW 8
-#endif
-#ifndef HZ_PACK_MARGIN
-#define HZ_PACK_MARGIN 1.12
-#endif
 // <= 8 waves: room for a block of registers in flight per lane (16 GiB Zipf, round 3: 9 / 10 waves under a
 // 168-VGPR cap 11.7 / 11.0 ms vs 8 waves 9.6 ms for k_pack_write)
-constexpr int kPackWriteThreads = 64 * HZ_PACK_MAXW;
+constexpr int kPackMaxWaves = 8;
+constexpr double kPackSlotMargin = 1.12;  // LDS output slot: the Kraft-estimated block bits x this
+constexpr int kPackWriteThreads = 64 * kPackMaxWaves;
 constexpr int kPackCopyIters = 16;       // slot copy-out covers 16 x 64 words: a 1024-word slot
 
 // One block of a wave between its lookup and its emit: the lane's 32 entries,
@@ -949,10 +927,6 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     }
 }
 
-#ifndef HZ_PACK_DEFER
-#define HZ_PACK_DEFER 1
-#endif
-constexpr bool kPackDefer = HZ_PACK_DEFER;
 
 // Pack of blocks whose start bits are known: the three-pass pack (after
 // k_pack_count + k_scan_*; wave w packs blocks w, w + W, ...) or, RNG, the
@@ -1004,7 +978,7 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
         // next block's loads: after this block's escapes, so no wait covers them early
         pack_prefetch(a, nb < a.nblocks ? nb : blk, lane, nx);
         pack_block_count<MODE>(lane, b);
-        pack_block_emit<MODE>(a, slot, blk, lane, b, RNG ? run : cur.bstart, max_bits, kPackDefer ? &po : nullptr);
+        pack_block_emit<MODE>(a, slot, blk, lane, b, RNG ? run : cur.bstart, max_bits, &po);
         if (RNG) run = newr ? nrun : run + b.bits;
         blk = nb;
     }
@@ -1368,7 +1342,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     const uint32_t table_words = t.enc_mode == ENC_WIDE ? 0 : t.enc_lds_bytes / 4;
     a.lds_words = table_words;
     const uint32_t free_words = kLdsBytes / 4 - table_words;
-    const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * HZ_PACK_MARGIN / 32.0) + 4;
+    const uint32_t est_words = (uint32_t)(t.enc_avg_bits * kBlockSyms * kPackSlotMargin / 32.0) + 4;
     constexpr uint32_t kMaxWaves = kPackWriteThreads / 64;
     uint32_t waves = free_words / est_words;
     waves = waves > kMaxWaves ? kMaxWaves : waves;
@@ -1450,12 +1424,6 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 // Every code 16 bits (FIXED16): symbol i sits at bit start + 16 i, so that
 // decoder needs no index and no staging (k_decode_fixed16).
 // ===========================================================================
-#ifndef HZ_DEC_DESC
-#define HZ_DEC_DESC 1
-#endif
-#ifndef HZ_DEC_PERM
-#define HZ_DEC_PERM 1  // pipelined decoder: two symbols packed by one v_perm (A/B switch)
-#endif
 struct DecArgs {
     const uint32_t* words;   // payload view, 64-byte aligned
     uint64_t nwords;
@@ -1827,15 +1795,10 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
     bool h[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-#if HZ_DEC_DESC
         // descending slot (dec_stage_commit<true>): p1 holds m, stream word t + 1 at byte (m >> 3) & ~3,
         // word t just above it, and m & 31 is the funnel shift (no v_not per step)
         const uint32_t wb = (p1[c] >> 3) & ~3u;
         W[c] = __builtin_amdgcn_alignbit(lds_at(wb + 4), lds_at(wb), p1[c]);
-#else
-        const uint32_t wb = (p1[c] >> 3) & ~3u;
-        W[c] = __builtin_amdgcn_alignbit(lds_at(wb), lds_at(wb + 4), ~p1[c]);
-#endif
     }
     HZ_WALK_FENCE();
 #pragma unroll
@@ -1845,13 +1808,9 @@ HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t*
     for (int c = 0; c < NC; ++c) {
         h[c] = lut_lds_link(e[c]);
         const uint32_t byte = ((e[c] >> 10) + __builtin_amdgcn_ubfe(W[c], e[c], e[c] >> 5)) << 2;
-#if HZ_DEC_HOT_OOB
         // a leaf's or a global link's byte address is >= 256 KiB, past the workgroup's LDS: that
         // read returns nothing anyone uses (the select below keeps e), so no address select
         x[c] = lds_at(byte);
-#else
-        x[c] = lds_at(h[c] ? byte : 0u);
-#endif
     }
     HZ_WALK_FENCE();
 #pragma unroll
@@ -1872,7 +1831,6 @@ struct PipeMeta {
 
 HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
     const uint64_t bb = b < a.nblocks ? b : a.nblocks - 1;  // past the end: any block, never used
-#if HZ_DEC_SMEM
     // the block's bounds through the scalar cache (the index is read-only here): the window
     // arithmetic that follows stays on the scalar unit
     typedef const __attribute__((address_space(4))) unsigned long long* cu64p;
@@ -1880,10 +1838,6 @@ HZ_DEV void dec_meta_load(const DecArgs& a, uint64_t b, int lane, PipeMeta& m) {
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bb);
     m.b0 = ((cu64p)a.starts)[bu];
     m.b1 = ((cu64p)a.starts)[bu + 1];
-#else
-    m.b0 = a.starts[bb];
-    m.b1 = a.starts[bb + 1];
-#endif
     m.sub = dec_sub_load(a, bb, lane);
 }
 
@@ -2035,21 +1989,15 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint64_t w0;
-            dec_stage_commit<HZ_DEC_DESC>(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
+            dec_stage_commit<true>(a, mc[j], slot >> 2, stg + j * slot, lane, sc[j], w0);
             uint32_t off[kChainsPerLane];
             dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
-#if HZ_DEC_DESC
             // m = (E - 1) * 32 + 31 - r for the slot's top word E and r = the chain's next bit - 1,
             // relative to stream word w0; a step of L bits subtracts L
             const uint32_t top = (uint32_t)(stg - lds) + (uint32_t)(j + 1) * slot - 1u;
             const uint32_t base = top * 32u - (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5));
 #pragma unroll
             for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base - off[c];
-#else
-            const uint32_t base = (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5)) + (uint32_t)j * slot * 32u + stg_bit;
-#pragma unroll
-            for (int c = 0; c < kChainsPerLane; ++c) p1[j * kChainsPerLane + c] = base + off[c];
-#endif
         }
         __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
         uint32_t pk[2][kSPT / 2];
@@ -2057,20 +2005,11 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         uint32_t g[C];
         auto finish = [&](int c, int q) {
             const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
-#if HZ_DEC_DESC
             p1[c] -= lut_leaf_len(ee);
-#else
-            p1[c] += lut_leaf_len(ee);
-#endif
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
             // an even step keeps the whole entry; the odd step packs both symbols (leaf bytes 1-2) by one v_perm
-#if HZ_DEC_PERM
             if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x06050201u);
             else pk[c / kChainsPerLane][i] = ee;
-#else
-            if (q & 1) pk[c / kChainsPerLane][i] |= lut_leaf_sym(ee) << 16;
-            else pk[c / kChainsPerLane][i] = lut_leaf_sym(ee);
-#endif
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
         auto issue4 = [&](int c) {
@@ -2623,17 +2562,11 @@ __global__ __launch_bounds__(kSyncThreads) void k_sync_scan2(DecArgs a, SyncArgs
 // ---------------------------------------------------------------------------
 // steps per round: u8 table 8: 25.5 ms, 10: 25.3 ms; 4-bit table 10/12/14: 24.7/24.4/24.6 ms;
 // round 4 (16 GiB Zipf, A/B in one run, k_idx_walk alone): 12 / 14 / 16 steps 17.32 / 17.11 / 17.44 ms
-#ifndef HZ_WALK_STEPS
-#define HZ_WALK_STEPS 14
-#endif
-constexpr int kWalkSteps = HZ_WALK_STEPS;
+constexpr int kWalkSteps = 14;
 // parked chains resume after each part of a round: 2 parts of 6 steps 23.6-23.9 ms, 1 part
 // 23.7-24.3, 2 x 8 23.4-23.9, 3 x 6 23.2-24.3, 3 x 4 24.8, 4 x 4 23.5-24.2 (A/B in one run);
 // round 3 (2.3 % escapes): 2 / 1 / 3 parts 22.1 / 22.1-22.3 / 23.4 ms
-#ifndef HZ_WALK_HALVES
-#define HZ_WALK_HALVES 2
-#endif
-constexpr int kWalkHalves = HZ_WALK_HALVES;
+constexpr int kWalkHalves = 2;
 constexpr uint32_t kWalkLead = 1024;    // lead-in bits before a chain's first segment
 
 struct WalkArgs {
@@ -3003,10 +2936,7 @@ constexpr int kSelectThreads = 256;
 constexpr uint32_t kSelTileSegs = 16;
 constexpr uint32_t kSelTileWords = kSelTileSegs * kBmpWords;  // 2048 = 8 words per thread
 constexpr uint32_t kSelMaxChains = kSelTileWords * 32 / kChainSyms + 2;
-#ifndef HZ_SEL_AHEAD
-#define HZ_SEL_AHEAD 1
-#endif
-constexpr int kSelAhead = HZ_SEL_AHEAD;
+constexpr int kSelAhead = 1;
 __global__ __launch_bounds__(kSelectThreads) void k_sync_select(SyncArgs y, uint64_t nsym, uint64_t nblocks,
                                                                 const unsigned long long* first,
                                                                 unsigned long long* starts, uint16_t* subs) {
