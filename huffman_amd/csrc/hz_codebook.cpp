@@ -637,3 +637,36 @@ void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vect
 }
 
 }  // namespace hz
+
+// The chain walker's length table (hz_kernels.hip k_chain_walk): one BYTE per K-bit window, K =
+// min(max_len, 16) (2^16 bytes, the same 64 KiB of LDS as the 17-bit nibble table): the length of the
+// code the window starts with when that code is at most K bits, or when every code under the
+// window's prefix has one length; 0 (escape: the walker reads esc, build_walk_len's 2^max_len table)
+// for prefixes shared by codes of different lengths. No bias and no nibble select per step, and
+// long lengths need no escape (16 GiB Zipf(1.1): escaped codewords 2.4 % -> 1.4 %). Windows no code
+// starts read min_len, so a walk past the stream's end keeps moving.
+namespace hz {
+void build_walk8(const hz_codebook* cb, std::vector<uint32_t>& img, int& K) {
+    const int M = (int)cb->max_len;
+    K = std::max(1, std::min(M, 16));
+    std::vector<uint8_t> t((size_t)1 << K, (uint8_t)cb->min_len);
+    std::vector<uint8_t> plen((size_t)1 << K, 0);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const int L = cb->len[s];
+        if (!L) continue;
+        const uint64_t c = cb->code[s];
+        if (L <= K) {
+            const uint64_t w0 = c << (K - L), n = (uint64_t)1 << (K - L);
+            memset(t.data() + w0, L, (size_t)n);
+        } else {
+            uint8_t& pl = plen[c >> (L - K)];
+            pl = pl == 0 || pl == (uint8_t)L ? (uint8_t)L : (uint8_t)255;
+        }
+    }
+    for (size_t p = 0; p < plen.size(); ++p)
+        if (plen[p]) t[p] = plen[p] != 255 ? plen[p] : 0;
+    while (t.size() % 16) t.push_back(0);
+    img.assign(t.size() / 4, 0);
+    memcpy(img.data(), t.data(), t.size());
+}
+}  // namespace hz

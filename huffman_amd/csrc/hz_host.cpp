@@ -39,6 +39,7 @@ int build_dec_dense(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
 int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& l2, int& K1, int& lvl);
 void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
                     int& bias);
+void build_walk8(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
 }  // namespace hz
 
 using namespace hz;
@@ -85,7 +86,7 @@ struct hz_ctx {
     uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
-           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0;
+           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_walk8 = 0;
     int last_pack_ranges = 0;       // the last hz_pack_ranges call took the range plan
 };
 
@@ -118,6 +119,7 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_dec_l2);
     (void)hipFree(t.d_walk_lds);
     (void)hipFree(t.d_walk_esc);
+    (void)hipFree(t.d_walk8);
     t = Tables();
 }
 
@@ -411,6 +413,10 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
             if (wesc.empty()) wesc.push_back(0x01010101u);
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;
             t.walk_lds_bytes = (uint32_t)(wimg.size() * 4);
+            std::vector<uint32_t> w8;
+            build_walk8(cb, w8, t.walk8_k);
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk8, &c->cap_walk8, w8))) return rc;
+            t.walk8_bytes = (uint32_t)(w8.size() * 4);
         }
     }
     HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));

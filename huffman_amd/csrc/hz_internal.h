@@ -187,6 +187,9 @@ struct Tables {
     uint32_t walk_lds_bytes = 0;    // 0 = no walker tables (the segment walkers build the index)
     uint32_t* d_walk_esc = nullptr; // index walker: u8 code length per walk_m-bit window (walk_m > walk_k)
     int walk_k = 0, walk_m = 0, walk_bias = 0;
+    uint32_t* d_walk8 = nullptr;    // chain walker: u8 code length per walk8_k-bit window (0 = escape to d_walk_esc)
+    uint32_t walk8_bytes = 0;
+    int walk8_k = 0;
 };
 
 // Count-pass length table layout: the high byte is XORed into the bank bits

@@ -2584,7 +2584,10 @@ struct WalkArgs {
     unsigned long long* cnt;
     unsigned long long* ent;
     uint32_t* dirty;
-    uint32_t lead;            // k_seg_walk: lead-in bits before a chain's first segment
+    uint32_t lead;            // k_chain_walk: lead-in bits before a chain's first bit
+    const uint32_t* w8_img;   // k_chain_walk: u8 code length per k8-bit window (0: escape)
+    uint32_t w8_words;
+    int k8;
 };
 
 // 16 payload bytes at word w (4-aligned): zeros before word 0 / past the end.
@@ -3167,6 +3170,7 @@ static hipError_t scan_walk(const Tables& t, const DecArgs& a, SyncArgs y, int n
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
     w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
     w.bmp = y.bmp; w.cnt = y.cnt; w.ent = y.ent; w.dirty = y.dirty[0]; w.lead = kWalkLead;
+    w.w8_img = nullptr; w.w8_words = 0; w.k8 = 0;
     // chains tid and tid + T of every thread
     const uint64_t threads_needed = (w.nchains + kWalkChains - 1) / kWalkChains;
     uint64_t wgs = (threads_needed + kWalkWaves * 64 - 1) / (kWalkWaves * 64);
@@ -3387,12 +3391,13 @@ constexpr int kSegSteps = 14;
 static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
 
 __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a, ChainArgs y) {
-    // the length table at LDS address 0 (k_idx_walk's layout), the rings and record buffers after it
-    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << kWalkK) / 8];
+    // the byte length table (build_walk8: 2^16 windows at most, 64 KiB) at LDS address 0, the rings and
+    // record buffers after it
+    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << 16) / 4];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    copy_lds_table(wtab, a.lds_img, a.lds_words);
+    copy_lds_table(wtab, a.w8_img, a.w8_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
-    const uint32_t k = (uint32_t)a.k, bias = (uint32_t)a.bias;
+    const uint32_t k8 = (uint32_t)a.k8;
     uint32_t* ring = lds + threadIdx.x * kSegRing;
     uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + blockDim.x * kSegRing) + 8 * threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3446,11 +3451,10 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
             for (int t = 0; t < S; ++t) {
                 const bool ok = !pk & (p < lim);
                 const uint32_t W = seg_window(ring, p);
-                uint32_t e = lds8[W >> (33 - k)];  // two windows per byte (k >= 2)
+                const uint32_t e = lds8[W >> (32 - k8)];  // the code's length, 0: escape
                 HZ_WALK_FENCE();
-                e = __builtin_amdgcn_ubfe(e, (W >> (30 - k)) & 4u, 4);  // the window's nibble
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
-                const uint32_t L = adv ? e + bias : 0u;
+                const uint32_t L = adv ? e : 0u;
                 na += adv ? 1u : 0u;
                 p += L;
                 pk |= park;
@@ -3916,7 +3920,7 @@ uint64_t chain_scratch_words(uint64_t part_begin, uint64_t part_end, uint64_t ns
 }
 
 bool seg_decode_supported(const Tables& t) {
-    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.dec_max_len <= 32 &&
+    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.walk8_bytes > 0 && t.dec_max_len <= 32 &&
            t.dec_max_len <= t.dec_k + t.dec_level_bits;
 }
 
@@ -4011,6 +4015,7 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
     w.start = start_bit; w.nseg = 0;
     w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
     w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
+    w.w8_img = t.d_walk8; w.w8_words = t.walk8_bytes / 4; w.k8 = t.walk8_k;
     w.bmp = nullptr; w.cnt = nullptr; w.ent = nullptr; w.dirty = nullptr;
     // test hook: HZ_SEG_LEAD=<bits> (0: no lead-in, so nearly every chain takes the fix-up path)
     static const uint32_t lead = [] { const char* v = getenv("HZ_SEG_LEAD"); return v ? (uint32_t)atoi(v) : kWalkLead; }();
