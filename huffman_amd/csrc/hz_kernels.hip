@@ -3318,19 +3318,26 @@ struct ChainArgs {
     uint32_t* err;
 };
 
-// The 32-bit window at ring bit position p (p >= 1; bit 0 of the ring = bit 0 of chunk 0): words
-// (p - 1) >> 5 and the next one, one ds_read2_b32.
-HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t p) {
-    const uint32_t* w = ring + (((p - 1) >> 5) & 15u);
-    return __builtin_amdgcn_alignbit(w[0], w[1], ~(p - 1) & 31u);
+// The ring holds its 16 words in DESCENDING order: ring word u (bit 32 u .. 32 u + 31 of the ring) at
+// index 15 - (u & 15), plus index 16 = a copy of index 0, so a window's two words are adjacent
+// (ds_read2_b32) and never wrap. The walk keeps its position as m = kRingM0 - p (decreasing): then the
+// pair's lower index is (m >> 5) & 15 and the funnel shift is m itself (kRingM0 = 0 mod 512; m's low 5
+// bits are 31 - ((p - 1) & 31)): two VALU for the address, none for the shift.
+constexpr uint32_t kRingM0 = 0x7fffffe0u;
+HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t m) {
+    uint32_t i;
+    asm("v_bfe_u32 %0, %1, 5, 4" : "=v"(i) : "v"(m));  // (kept whole: the compiler's shift + and + add is one more)
+    const uint32_t* w = ring + i;
+    return __builtin_amdgcn_alignbit(w[1], w[0], m);
 }
 
-// Chunk slot q of a ring (and word 16 with slot 0's first word), byte-swapped.
+// Chunk slot q of a ring (ring words 4 q .. 4 q + 3), byte-swapped, descending; slot 3's last word
+// (index 0) also at index 16.
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ring[4 * q + i] = v[i];
-    if (q == 0) ring[16] = v[0];
+    for (int i = 0; i < 4; ++i) ring[15 - 4 * q - i] = v[i];
+    if (q == 3) ring[16] = v[3];
 }
 
 // The ring's loader state: the next chunk f and the 64-byte register group it comes from.
@@ -3436,56 +3443,61 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     if (on && p < end) rec_put(p);
     bool pk = false;
     uint32_t pW = 0;
+    uint32_t m = kRingM0 - p;  // the walk's position, descending (seg_window)
+    const uint32_t mend = kRingM0 - end;
     for (;;) {
-        if (!__any(p < end)) break;
+        if (!__any(m > mend)) break;
         const uint32_t fill = 128 * fd.f - 96;  // filled data: both window words lie below p + 64
-        const uint32_t lim = min(on ? end : csr, fill);
+        const uint32_t mlim = kRingM0 - min(on ? end : csr, fill);  // a step needs m > mlim
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
             // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
-            // that parks or reaches lim stays put for the rest of the half), then at p for an escape
+            // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
             constexpr int S = kSegSteps / kWalkHalves;
             uint32_t q[S];
             uint32_t na = 0;
 #pragma unroll
             for (int t = 0; t < S; ++t) {
-                const bool ok = !pk & (p < lim);
-                const uint32_t W = seg_window(ring, p);
+                const bool ok = !pk & (m > mlim);
+                const uint32_t W = seg_window(ring, m);
                 const uint32_t e = lds8[W >> (32 - k8)];  // the code's length, 0: escape
                 HZ_WALK_FENCE();
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
                 const uint32_t L = adv ? e : 0u;
                 na += adv ? 1u : 0u;
-                p += L;
+                m -= L;
                 pk |= park;
                 pW = park ? W : pW;
-                q[t] = p;
+                q[t] = m;
             }
-            const uint32_t m = na + (pk ? 1u : 0u);
+            const uint32_t nm = na + (pk ? 1u : 0u);
             if (pk) {
-                p += a.esc[pW >> (32 - a.m)];
+                m -= a.esc[pW >> (32 - a.m)];
                 pk = false;
             }
+            const uint32_t pc = kRingM0 - m;
             if (on) {
                 // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based)
                 const uint32_t j1 = 8u - (cc & 7u);
-                if (j1 <= m) {
+                if (j1 <= nm) {
                     const uint32_t jj = j1 <= na ? j1 : 0u;
-                    uint32_t rp = p;
+                    uint32_t rm = m;
 #pragma unroll
-                    for (int t = 0; t < S; ++t) rp = jj == (uint32_t)t + 1u ? q[t] : rp;
+                    for (int t = 0; t < S; ++t) rm = jj == (uint32_t)t + 1u ? q[t] : rm;
+                    const uint32_t rp = kRingM0 - rm;
                     if (rp < end) rec_put(rp);  // (a codeword starting at the end is the next chain's)
                 }
-                cc += m;
-            } else if (p >= csr) {  // the lead-in's last step lands on the entry
+                cc += nm;
+            } else if (pc >= csr) {  // the lead-in's last step lands on the entry
                 on = true;
-                ent = p;
+                ent = pc;
                 cc = 0;
-                if (p < end) rec_put(p);
+                if (pc < end) rec_put(pc);
             }
         }
-        seg_feed(a, ring, fd, p);
+        seg_feed(a, ring, fd, kRingM0 - m);
     }
+    p = kRingM0 - m;
     if (!live) return;
     if ((rj & 7u) && (rj & ~7u) < y.cap)  // the last, partial group of records
         *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
