@@ -611,7 +611,10 @@ void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vect
         b = (w & 1) ? (uint8_t)((b & 0x0f) | (v << 4)) : (uint8_t)((b & 0xf0) | v);
     };
     esc.clear();
-    if (M > K) esc.assign(((size_t)1 << M) / 4, 0x01010101u);
+    // esc holds every code longer than KE = min(K, 16) bits: k_idx_walk escapes only codes longer than
+    // K, the chain walker's byte table (build_walk8, 16-bit windows) codes longer than 16
+    const int KE = std::min(K, 16);
+    if (M > KE) esc.assign(((size_t)1 << M) / 4, 0x01010101u);
     uint8_t* t2 = reinterpret_cast<uint8_t*>(esc.data());
     // a K-bit prefix shared only by codes of ONE length L > K still tells the length:
     // such windows read L - bias when it fits the nibble, and only the rest escape
@@ -623,13 +626,13 @@ void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vect
         const int L = cb->len[s];
         if (!L) continue;
         const uint64_t c = cb->code[s];
+        if (L > KE) memset(t2 + (c << (M - L)), L, (size_t)1 << (M - L));
         if (L <= K) {
             const uint64_t w0 = c << (K - L), n = (uint64_t)1 << (K - L);
             for (uint64_t w = w0; w < w0 + n; ++w) put(w, (uint32_t)(L - bias));
         } else {
             uint8_t& pl = plen[c >> (L - K)];
             pl = pl == 0 || pl == (uint8_t)L ? (uint8_t)L : (uint8_t)255;
-            memset(t2 + (c << (M - L)), L, (size_t)1 << (M - L));
         }
     }
     for (size_t p = 0; p < plen.size(); ++p)
