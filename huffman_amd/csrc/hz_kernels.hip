@@ -3703,9 +3703,14 @@ HZ_DEV void chain_store(const DecArgs& a, const ChainMeta& m, int lane, const ui
     const bool full = m.lo == 0 && m.hi == kChainRecs && m.last == 8 && m.out >= 0 &&
                       (uint64_t)m.out + (uint64_t)kBlockSyms <= a.nsym;
     if (full) {
+#ifdef HZ_EXP_ALIGNED_STORE  // timing experiment only (wrong output): the full blocks' stores 16-byte aligned
+        const long long ob = m.out & ~7ll;
+#else
+        const long long ob = m.out;
+#endif
 #pragma unroll
         for (int c = 0; c < kChainsPerLane; ++c) {
-            uint32_t* q = reinterpret_cast<uint32_t*>(out16 + m.out + 8 * (64 * c + lane));
+            uint32_t* q = reinterpret_cast<uint32_t*>(out16 + ob + 8 * (64 * c + lane));
             u32x4a2 v = u32x4a2{pk[4 * c], pk[4 * c + 1], pk[4 * c + 2], pk[4 * c + 3]};
             __builtin_nontemporal_store(v, reinterpret_cast<u32x4a2*>(q));
         }
