@@ -44,7 +44,13 @@ void build_walk8(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
 
 using namespace hz;
 
-#define HZ_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return HZ_EHIP; } while (0)
+// HZ_DEBUG=1: a failing HIP call is named on stderr (file line, call, HIP's message) before HZ_EHIP.
+static int hz_hip_fail(hipError_t e, const char* what, int line) {
+    static const bool dbg = getenv("HZ_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "[huffman_amd] hz_host.cpp:%d %s: %s\n", line, what, hipGetErrorString(e));
+    return HZ_EHIP;
+}
+#define HZ_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return hz_hip_fail(_e, #x, __LINE__); } while (0)
 
 // No C++ exception crosses the C ABI: entry points that allocate host
 // containers run their body through this guard.
