@@ -3443,80 +3443,64 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     if (on && p < end) rec_put(p);
     bool pk = false;
     uint32_t pW = 0;
-    // Register window: the 32 bits at p are alignbit(w0, w1, sh), w0 = ring word u = (p - 1) >> 5, w1 =
-    // word u + 1, nxt = word u + 2, sh = -p & 31. A step of L (< 32) bits that crosses a word shifts the
-    // words and reads ONE ring word (the new nxt): only the crossing lanes touch the ring, so a step's
-    // LDS work is its table read plus about a third of a ring read (two ring words per step before).
-    auto ring_word = [&](uint32_t u) { return ring[(u & 15u) ^ 15u]; };  // descending ring (seg_ring_put)
-    uint32_t wu = (p - 1) >> 5;
-    uint32_t w0 = ring_word(wu), w1 = ring_word(wu + 1), nxt = ring_word(wu + 2);
-    uint32_t sh = (0u - p) & 31u;
-    // one codeword of L bits (L < 32: at most one word crossed)
-    auto advance = [&](uint32_t L) {
-        const int32_t r = (int32_t)sh - (int32_t)L;
-        const bool cr = r < 0;
-        w0 = cr ? w1 : w0;
-        w1 = cr ? nxt : w1;
-        sh = (uint32_t)(cr ? r + 32 : r);
-        if (cr) {  // exec-masked: only the crossing lanes read the ring
-            ++wu;
-            nxt = ring_word(wu + 2);
-        }
-        p += L;
-    };
+    uint32_t m = kRingM0 - p;  // the walk's position, descending (seg_window)
+    const uint32_t mend = kRingM0 - end;
     for (;;) {
-        if (!__any(p < end)) break;
-        const uint32_t fill = 128 * fd.f - 96;  // filled data: ring words up to (p + 95) >> 5
-        const uint32_t lim = min(on ? end : csr, fill);
+        if (!__any(m > mend)) break;
+        const uint32_t fill = 128 * fd.f - 96;  // filled data: both window words lie below p + 64
+        const uint32_t mlim = kRingM0 - min(on ? end : csr, fill);  // a step needs m > mlim
 #pragma unroll
         for (int half = 0; half < kWalkHalves; ++half) {
             // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
-            // that parks or reaches lim stays put for the rest of the half), then at p for an escape
+            // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
             constexpr int S = kSegSteps / kWalkHalves;
             uint32_t q[S];
             uint32_t na = 0;
 #pragma unroll
             for (int t = 0; t < S; ++t) {
-                const bool ok = !pk & (p < lim);
-                const uint32_t W = __builtin_amdgcn_alignbit(w0, w1, sh);
+                const bool ok = !pk & (m > mlim);
+                const uint32_t W = seg_window(ring, m);
                 const uint32_t e = lds8[W >> (32 - k8)];  // the code's length, 0: escape
                 HZ_WALK_FENCE();
                 const bool adv = ok & (e != 0u), park = ok ^ adv;
+                const uint32_t L = adv ? e : 0u;
                 na += adv ? 1u : 0u;
-                advance(adv ? e : 0u);
+                m -= L;
                 pk |= park;
                 pW = park ? W : pW;
-                q[t] = p;
+                q[t] = m;
             }
             const uint32_t nm = na + (pk ? 1u : 0u);
             if (pk) {
-#ifdef HZ_EXP_NOESC  // timing experiment only (wrong output): escapes without their gather
-                advance(20u);
-#else
-                advance(a.esc[pW >> (32 - a.m)]);
-#endif
+                m -= a.esc[pW >> (32 - a.m)];
                 pk = false;
             }
+            // the round's feed right after its last escape wait and before the half's record stores: its
+            // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
+            // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
+            if (half == kWalkHalves - 1) seg_feed(a, ring, fd, kRingM0 - m);
+            const uint32_t pc = kRingM0 - m;
             if (on) {
                 // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based)
                 const uint32_t j1 = 8u - (cc & 7u);
                 if (j1 <= nm) {
                     const uint32_t jj = j1 <= na ? j1 : 0u;
-                    uint32_t rp = p;
+                    uint32_t rm = m;
 #pragma unroll
-                    for (int t = 0; t < S; ++t) rp = jj == (uint32_t)t + 1u ? q[t] : rp;
+                    for (int t = 0; t < S; ++t) rm = jj == (uint32_t)t + 1u ? q[t] : rm;
+                    const uint32_t rp = kRingM0 - rm;
                     if (rp < end) rec_put(rp);  // (a codeword starting at the end is the next chain's)
                 }
                 cc += nm;
-            } else if (p >= csr) {  // the lead-in's last step lands on the entry
+            } else if (pc >= csr) {  // the lead-in's last step lands on the entry
                 on = true;
-                ent = p;
+                ent = pc;
                 cc = 0;
-                if (p < end) rec_put(p);
+                if (pc < end) rec_put(pc);
             }
         }
-        seg_feed(a, ring, fd, p);
     }
+    p = kRingM0 - m;
     if (!live) return;
     if ((rj & 7u) && (rj & ~7u) < y.cap)  // the last, partial group of records
         *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
@@ -3722,11 +3706,7 @@ HZ_DEV void chain_store(const DecArgs& a, const ChainMeta& m, int lane, const ui
     const bool full = m.lo == 0 && m.hi == kChainRecs && m.last == 8 && m.out >= 0 &&
                       (uint64_t)m.out + (uint64_t)kBlockSyms <= a.nsym;
     if (full) {
-#ifdef HZ_EXP_ALIGNED_STORE  // timing experiment only (wrong output): the full blocks' stores 16-byte aligned
-        const long long ob = m.out & ~7ll;
-#else
         const long long ob = m.out;
-#endif
 #pragma unroll
         for (int c = 0; c < kChainsPerLane; ++c) {
             uint32_t* q = reinterpret_cast<uint32_t*>(out16 + ob + 8 * (64 * c + lane));
