@@ -3280,8 +3280,12 @@ hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_
 constexpr int kChainWalkWaves = 16;
 constexpr uint32_t kChainRecs = 256;  // records per decode block (2048 codewords)
 // Per-lane payload ring of k_chain_walk: 4 chunks of 4 words, then a copy of word 0 (so the window's two
-// words q, q + 1 never wrap), odd stride (lanes' rings start in distinct banks).
+// words q, q + 1 never wrap).
 constexpr uint32_t kSegRing = 16 + 1;
+// Ring word j of lane t at LDS word j * kRingRow + t: all of a lane's words lie in bank t mod 32, so the
+// window's two words (one ds_read2st64_b32) and the chunk stores never conflict between lanes (a ring
+// per lane at an odd stride: random banks, 12.43 vs 12.10 ms at 16 GiB Zipf, A/B in one run).
+constexpr uint32_t kRingRow = kChainWalkWaves * 64;
 
 struct ChainBlk {
     unsigned long long b0, b1;  // stream bits of the block's first record and of the one after its last
@@ -3327,8 +3331,8 @@ constexpr uint32_t kRingM0 = 0x7fffffe0u;
 HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t m) {
     uint32_t i;
     asm("v_bfe_u32 %0, %1, 5, 4" : "=v"(i) : "v"(m));  // (kept whole: the compiler's shift + and + add is one more)
-    const uint32_t* w = ring + i;
-    return __builtin_amdgcn_alignbit(w[1], w[0], m);
+    const uint32_t* w = ring + i * kRingRow;
+    return __builtin_amdgcn_alignbit(w[kRingRow], w[0], m);
 }
 
 // Chunk slot q of a ring (ring words 4 q .. 4 q + 3), byte-swapped, descending; slot 3's last word
@@ -3336,8 +3340,8 @@ HZ_DEV uint32_t seg_window(const uint32_t* ring, uint32_t m) {
 HZ_DEV void seg_ring_put(uint32_t* ring, uint32_t q, const uint4& x) {
     const uint32_t v[4] = {bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w)};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ring[15 - 4 * q - i] = v[i];
-    if (q == 3) ring[16] = v[3];
+    for (int i = 0; i < 4; ++i) ring[(15 - 4 * q - i) * kRingRow] = v[i];
+    if (q == 3) ring[16 * kRingRow] = v[3];
 }
 
 // The ring's loader state: the next chunk f and the 64-byte register group it comes from.
@@ -3405,8 +3409,8 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     copy_lds_table(wtab, a.w8_img, a.w8_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
     const uint32_t k8 = (uint32_t)a.k8;
-    uint32_t* ring = lds + threadIdx.x * kSegRing;
-    uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + blockDim.x * kSegRing) + 8 * threadIdx.x;
+    uint32_t* ring = lds + threadIdx.x;
+    uint16_t* rbuf = reinterpret_cast<uint16_t*>(lds + kSegRing * kRingRow) + 8 * threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = ch < y.nchains;
     const uint64_t chc = live ? ch : 0;
@@ -4042,7 +4046,7 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
         uint64_t wpg = (g.nchains + 64ull * ncu - 1) / (64ull * ncu);
         wpg = wpg < 1 ? 1 : (wpg > (uint64_t)kChainWalkWaves ? (uint64_t)kChainWalkWaves : wpg);
         const uint32_t threads = (uint32_t)(64 * wpg);
-        const uint32_t ring_bytes = threads * (kSegRing * 4 + 16);  // rings, record buffers
+        const uint32_t ring_bytes = kSegRing * kRingRow * 4 + threads * 16;  // ring rows (1024 lanes), record buffers
         if ((e = ensure_lds_limit((const void*)k_chain_walk, (int)(kChainWalkWaves * 64 * (kSegRing * 4 + 16)))) !=
             hipSuccess)
             return e;

@@ -63,9 +63,11 @@ def stage_of(name):
 
 
 def read_counter(d, counter):
-    """Per stage: (corrected bytes, raw bytes, corrected kernel names), launches."""
+    """Per stage: (corrected bytes, raw bytes, corrected kernel names), launches, and per stage and
+    kernel (short name) the corrected bytes."""
     path = os.path.join(d, "run_counter_collection.csv")
     per = defaultdict(float)
+    perk = defaultdict(lambda: defaultdict(float))
     raw = defaultdict(float)
     fixed = defaultdict(set)
     calls = defaultdict(set)
@@ -85,12 +87,19 @@ def read_counter(d, counter):
             v = float(row["Counter_Value"]) * 1024.0
             wide = counter == "FETCH_SIZE" and any(_is(row["Kernel_Name"], k) for k in WIDE_READ)
             per[st] += 2.0 * v if wide else v
+            perk[st][short_name(row["Kernel_Name"])] += 2.0 * v if wide else v
             raw[st] += v
             if wide:
                 fixed[st].update(k for k in WIDE_READ if _is(row["Kernel_Name"], k))
             if any(_is(row["Kernel_Name"], k) for k in STAGES[st][1]):
                 calls[st].add(row["Dispatch_Id"])
-    return per, raw, fixed, {k: len(v) for k, v in calls.items()}
+    return per, raw, fixed, {k: len(v) for k, v in calls.items()}, perk
+
+
+def short_name(name):
+    """The kernel's name without namespace, template arguments and parameters."""
+    n = name.split("(")[0].split("<")[0]
+    return n.split("::")[-1].split(" ")[-1]
 
 
 def main():
@@ -101,8 +110,8 @@ def main():
     ap.add_argument("--size", type=int, required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fetch, fraw, ffixed, fcalls = read_counter(a.fetch, "FETCH_SIZE")
-    write, _, _, wcalls = read_counter(a.write, "WRITE_SIZE")
+    fetch, fraw, ffixed, fcalls, fk = read_counter(a.fetch, "FETCH_SIZE")
+    write, _, _, wcalls, wk = read_counter(a.write, "WRITE_SIZE")
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     try:
@@ -126,6 +135,9 @@ def main():
             "correction": "fetch = 2 x FETCH_SIZE for the kernels in fetch_doubled (gfx950 wide-read "
                           "undercount, calibrated shapes), FETCH_SIZE as counted for the rest; write = WRITE_SIZE",
             "fetch_doubled": sorted(ffixed[st]),
+            "kernels": {k: {"fetch_bytes_per_launch": round(fk[st].get(k, 0.0) / nf),
+                            "write_bytes_per_launch": round(wk[st].get(k, 0.0) / nw)}
+                        for k in sorted(set(fk[st]) | set(wk[st]))},
             "build_id": bid,
         }
     res.setdefault(a.dist, {}).update(ent)  # a later pass (e.g. the extract-only run) replaces its stages
