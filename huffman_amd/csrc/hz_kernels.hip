@@ -3431,14 +3431,16 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     // record r: the codeword's stream bit, low 16 bits, into the lane's 16-byte LDS buffer (stored 8 at
     // a time); every 256th also as a u64 checkpoint (a decode block's start). Past the capacity
     // nothing is stored (k_chain_tail decodes those codewords).
+    // (the buffer write needs no capacity test: rows past the capacity are never stored)
     auto rec_put = [&](uint32_t rp) {
         const uint64_t ab = abs0 + rp;
-        if (rj < y.cap) {
-            rbuf[rj & 7] = (uint16_t)ab;
-            if ((rj & (kChainRecs - 1)) == 0) ckp[rj / kChainRecs] = ab;
-            if ((rj & 7) == 7) *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
-        } else if (rj == y.cap) {
-            ckp[y.bpc] = ab;  // the first codeword past the capacity
+        rbuf[rj & 7] = (uint16_t)ab;
+        const bool in = rj < y.cap;
+        const bool row = in & ((rj & 7) == 7);
+        const bool ck = (in & ((rj & (kChainRecs - 1)) == 0)) | (rj == y.cap);  // at the capacity: the first codeword past it
+        if (row | ck) {  // one branch for both rare stores
+            if (row) *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
+            if (ck) ckp[in ? rj / kChainRecs : y.bpc] = ab;
         }
         ++rj;
     };
@@ -3484,24 +3486,26 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
             // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
             if (half == kWalkHalves - 1) seg_feed(a, ring, fd, kRingM0 - m);
             const uint32_t pc = kRingM0 - m;
-            if (on) {
-                // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based)
-                const uint32_t j1 = 8u - (cc & 7u);
-                if (j1 <= nm) {
-                    const uint32_t jj = j1 <= na ? j1 : 0u;
-                    uint32_t rm = m;
+            // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
+            // or m when j1 is the escaped codeword (jj = 0); a three-level select on jj's bits
+            const uint32_t j1 = 8u - (cc & 7u);
+            const uint32_t jj = j1 <= na ? j1 : 0u;
+            static_assert(S <= 7, "q[jj - 1] for jj < 8");
+            uint32_t v[8];
+            v[0] = m;
 #pragma unroll
-                    for (int t = 0; t < S; ++t) rm = jj == (uint32_t)t + 1u ? q[t] : rm;
-                    const uint32_t rp = kRingM0 - rm;
-                    if (rp < end) rec_put(rp);  // (a codeword starting at the end is the next chain's)
-                }
-                cc += nm;
-            } else if (pc >= csr) {  // the lead-in's last step lands on the entry
-                on = true;
-                ent = pc;
-                cc = 0;
-                if (pc < end) rec_put(pc);
-            }
+            for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : m;
+            const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
+            const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
+            const uint32_t rm = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+            // the lead-in's last step lands on the entry: the entry is the record, counting starts there
+            const bool enter = !on & (pc >= csr);
+            const uint32_t rp = on ? kRingM0 - rm : pc;
+            const bool rec = (on ? j1 <= nm : enter) & (rp < end);  // (a codeword starting at the end is the next chain's)
+            ent = enter ? pc : ent;
+            cc = on ? cc + nm : 0u;
+            on |= enter;
+            if (rec) rec_put(rp);
         }
     }
     p = kRingM0 - m;
