@@ -3404,8 +3404,10 @@ static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
 __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a, ChainArgs y) {
     // the byte length table (build_walk8: 2^16 windows at most, 64 KiB) at LDS address 0, the rings and
     // record buffers after it
-    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << 16) / 4];
+    // (+ one zero word: the byte a lane past its limit reads)
+    __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << 16) / 4 + 4];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (threadIdx.x == 0) wtab[(1u << 16) / 4] = 0;
     copy_lds_table(wtab, a.w8_img, a.w8_words);
     const uint8_t* lds8 = reinterpret_cast<const uint8_t*>(wtab);
     const uint32_t k8 = (uint32_t)a.k8;
@@ -3447,8 +3449,6 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     bool on = p >= csr;  // past the lead-in: counting from the entry
     uint32_t ent = p;
     if (on && p < end) rec_put(p);
-    bool pk = false;
-    uint32_t pW = 0;
     uint32_t m = kRingM0 - p;  // the walk's position, descending (seg_window)
     const uint32_t mend = kRingM0 - end;
     for (;;) {
@@ -3459,28 +3459,27 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
         for (int half = 0; half < kWalkHalves; ++half) {
             // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
             // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
+            // A step reads the code's length (0: an escape), or, past the limit, the zero byte after the
+            // table: a chain that reads 0 stays put and reads 0 again, so the advancing steps are a prefix
+            // with no park flags, and an escape's window is the half's last (no lane masks and no SALU
+            // per step: 281 vs 330 clocks per step in tools/microbench/mb_walk_step.hip).
             constexpr int S = kSegSteps / kWalkHalves;
             uint32_t q[S];
-            uint32_t na = 0;
+            uint32_t na = 0, W = 0, e = 0;
+            bool ok = false;
 #pragma unroll
             for (int t = 0; t < S; ++t) {
-                const bool ok = !pk & (m > mlim);
-                const uint32_t W = seg_window(ring, m);
-                const uint32_t e = lds8[W >> (32 - k8)];  // the code's length, 0: escape
+                ok = m > mlim;
+                W = seg_window(ring, m);
+                e = lds8[ok ? W >> (32 - k8) : 1u << 16];
                 HZ_WALK_FENCE();
-                const bool adv = ok & (e != 0u), park = ok ^ adv;
-                const uint32_t L = adv ? e : 0u;
-                na += adv ? 1u : 0u;
-                m -= L;
-                pk |= park;
-                pW = park ? W : pW;
+                m -= e;
+                na += e != 0u ? 1u : 0u;
                 q[t] = m;
             }
+            const bool pk = ok & (e == 0u);  // parked on an escape
             const uint32_t nm = na + (pk ? 1u : 0u);
-            if (pk) {
-                m -= a.esc[pW >> (32 - a.m)];
-                pk = false;
-            }
+            if (pk) m -= a.esc[W >> (32 - a.m)];
             // the round's feed right after its last escape wait and before the half's record stores: its
             // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
             // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
