@@ -3479,24 +3479,28 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
             }
             const bool pk = ok & (e == 0u);  // parked on an escape
             const uint32_t nm = na + (pk ? 1u : 0u);
-            if (pk) m -= a.esc[W >> (32 - a.m)];
+            // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
+            // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
+            const uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
+            // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
+            // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
+            const uint32_t j1 = 8u - (cc & 7u);
+            const uint32_t jj = j1 <= na ? j1 : 0u;
+            static_assert(S <= 7, "q[jj - 1] for jj < 8");
+            uint32_t v[8];
+            v[0] = 0;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : 0u;
+            const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
+            const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
+            const uint32_t sel = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+            m -= pk ? ev : 0u;
             // the round's feed right after its last escape wait and before the half's record stores: its
             // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
             // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
             if (half == kWalkHalves - 1) seg_feed(a, ring, fd, kRingM0 - m);
             const uint32_t pc = kRingM0 - m;
-            // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
-            // or m when j1 is the escaped codeword (jj = 0); a three-level select on jj's bits
-            const uint32_t j1 = 8u - (cc & 7u);
-            const uint32_t jj = j1 <= na ? j1 : 0u;
-            static_assert(S <= 7, "q[jj - 1] for jj < 8");
-            uint32_t v[8];
-            v[0] = m;
-#pragma unroll
-            for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : m;
-            const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
-            const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
-            const uint32_t rm = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+            const uint32_t rm = jj ? sel : m;
             // the lead-in's last step lands on the entry: the entry is the record, counting starts there
             const bool enter = !on & (pc >= csr);
             const uint32_t rp = on ? kRingM0 - rm : pc;
