@@ -239,7 +239,14 @@ def main():
 
     state = {}
 
-    def step(dropin=False):
+    def sidecar(plan, dropin, force_index=False):
+        """Whether pack writes the block index and decode reads it: not on the drop-in path, and not
+        for a FIXED16 codebook (every code 16 bits: its decoder places symbol i at start + 16 i and reads
+        no index; hz_decode_indexless takes it directly) unless the index itself is wanted."""
+        fixed16 = int(plan.cb.min_len) == 16 and int(plan.cb.max_len) == 16
+        return not dropin and (force_index or not fixed16)
+
+    def step(dropin=False, force_index=False):
         codec.histogram(x)
         if world > 1:
             hist_local.copy_(codec.hist)
@@ -257,9 +264,10 @@ def main():
                                last_byte=last, cb=cb)
         if "payload" not in state or state["payload"].numel() < plan.words * 4 + 16:
             state["payload"], state["index"] = codec.alloc_payload(plan, nsym)
-        codec.pack(x, plan, state["payload"], None if dropin else state["index"])
+        side = sidecar(plan, dropin, force_index)
+        codec.pack(x, plan, state["payload"], state["index"] if side else None)
         codec.upload_decode(plan)  # host builds the decode tables while pack runs
-        if dropin:
+        if not side:
             codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit, nsym,
                                        out.data_ptr(), endb.data_ptr())
         else:
@@ -310,11 +318,12 @@ def main():
         for i in range(steps):
             if "payload" not in state or state["payload"].numel() < plan.words * 4 + 16:
                 state["payload"], state["index"] = codec.alloc_payload(plan, nsym)
-            codec.pack(x, plan, state["payload"], None if dropin else state["index"])
+            side = sidecar(plan, dropin)
+            codec.pack(x, plan, state["payload"], state["index"] if side else None)
             if i + 1 < steps:
                 hist_launch()  # the next batch's histogram, between this batch's pack and decode
             codec.upload_decode(plan)  # host builds the decode tables while pack runs
-            if dropin:
+            if not side:
                 codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit,
                                            nsym, out.data_ptr(), endb.data_ptr())
             else:
@@ -359,16 +368,18 @@ def main():
     kms = {"hist": [], "pack": [], "decode": []}
     host_ms = []
     host_dec_ms = []
+    from huffman_amd._lib import STAGE_EXTRACT
     for _ in range(2):
         step()
         torch.cuda.synchronize()
+        side = sidecar(state["plan"], False)
         for k, v in codec.kernel_ms().items():
-            kms[k].append(v)
+            # (a FIXED16 step decodes through hz_decode_indexless: its time is the extract stage's)
+            kms[k].append(v if k != "decode" or side else codec.dev.kernel_ms(STAGE_EXTRACT))
         host_ms.append(codec.timings.get("codebook_ms", 0) + codec.timings.get("upload_ms", 0))
         host_dec_ms.append(codec.timings.get("upload_decode_ms", 0))
     ok = ok and bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
     # the drop-in step's kernels (pack without an index; the index-less decode), serialised, untimed
-    from huffman_amd._lib import STAGE_EXTRACT
     dk = {"hist": [], "pack": [], "extract": []}
     for _ in range(2):
         out.fill_(0)
@@ -379,7 +390,7 @@ def main():
         dk["pack"].append(km["pack"])
         dk["extract"].append(codec.dev.kernel_ms(STAGE_EXTRACT))
     ok = ok and bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
-    step()  # payload and index of the sidecar-index path again, for the checks below
+    step(force_index=True)  # payload and index of the sidecar-index path again, for the checks below
     torch.cuda.synchronize()
     plan = state["plan"]
     log(f"rank {rank}: {elapsed * 1e3 / args.steps:.3f} ms/step; index rebuild from the payload")
@@ -479,7 +490,9 @@ def main():
             },
             "step_schedule": "pipelined, one stream: batch k+1's histogram runs between batch k's pack and "
                              "decode, so its host codebook and encode tables are built while batch k decodes; "
-                             "kernel_ms and host_* come from two further serialised steps",
+                             "kernel_ms and host_* come from two further serialised steps; pack writes the "
+                             "block index and decode reads it, except for a FIXED16 codebook (every code 16 bits), "
+                             "whose decoder needs no index (hz_decode_indexless: symbol i at start + 16 i)",
             "roundtrip_bit_exact": ok,
             "index_build_from_payload": index_build,
             "extract_indexless": extract,

@@ -567,8 +567,26 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
     // nsym codewords end within nsym * max_len bits: the rest of a longer buffer is never walked
     const uint64_t reach = (start_bit + nsym * (uint64_t)std::max(c->t.dec_max_len, 1) + 7) / 8 + 8;
     if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
-    // codebooks the chain decoder does not take (DENSE / FIXED16 tables, codes > 22 bits): block
-    // index, then the block decoder
+    if (c->t.dec_mode == DEC_FIXED16) {
+        // every code 16 bits: symbol i at start_bit + 16 i, so no index and no walk (stream-ordered)
+        const uint64_t endb = nsym <= (UINT64_MAX - start_bit) / 16 ? start_bit + 16 * nsym : ~0ull;
+        const bool fits = endb <= payload_bytes * 8;  // else: the end bit past the payload, nothing decoded
+        HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
+        if (d_end_bit) {
+            const uint64_t eb = fits ? endb : ~0ull;
+            HZ_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_end_bit), (int)(uint32_t)eb, 1, c->stream));
+            HZ_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(reinterpret_cast<uint32_t*>(d_end_bit) + 1),
+                                     (int)(uint32_t)(eb >> 32), 1, c->stream));
+        }
+        if (fits)
+            HZ_TRY(launch_decode(c->t, d_payload, payload_bytes, nsym, nullptr, d_out, c->d_err, c->ncu, c->stream,
+                                 start_bit));
+        HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
+        c->ev_used[HZ_STAGE_EXTRACT] = true;
+        return arm_err_check(c);
+    }
+    // codebooks the chain decoder does not take (DENSE tables, codes > 24 bits): block index, then the
+    // block decoder
     if (!seg_decode_supported(c->t) || payload_bytes < 16)
         return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
     // stream-ordered from here: walk, fix-ups, scans, block decode, tails (no host synchronisation

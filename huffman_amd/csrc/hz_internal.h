@@ -217,7 +217,8 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
 uint64_t pack_scratch_words(uint64_t nsym);  // u64 words of d_scratch hz_pack needs
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                          uint64_t nsym, const unsigned long long* d_index, uint8_t* d_out,
-                         uint32_t* d_err, int ncu, hipStream_t s);
+                         uint32_t* d_err, int ncu, hipStream_t s,
+                         uint64_t start0 = 0);  // d_index null (FIXED16 only): symbol i at start0 + 16 i
 hipError_t launch_index_build(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
                               uint64_t start_bit, uint64_t nsym, unsigned long long* d_index,
                               unsigned long long* d_scratch, uint32_t* d_err, uint32_t* h_scratch, int ncu,

@@ -1432,6 +1432,7 @@ struct DecArgs {
     uint64_t nblocks;
     const unsigned long long* starts;  // block index (hz_internal.h)
     const unsigned long long* subs;    // four u16 chain start bits per lane (low 16 bits)
+    uint64_t start0;         // FIXED16 without an index: the stream's first bit (starts null)
     const uint32_t* lds_img;
     uint32_t lds_words;      // table words; the staging region follows
     uint32_t region_words;   // staging region per workgroup (slots sized in-kernel from max_bits)
@@ -2090,7 +2091,7 @@ __global__ __launch_bounds__(1024) void k_decode_fixed16_blk(DecArgs a, uint64_t
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
     const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
-    const uint64_t p0 = a.starts[0] + a.bit_adj;
+    const uint64_t p0 = (a.starts ? a.starts[0] : a.start0) + a.bit_adj;
     const uint32_t sh = (uint32_t)(p0 & 31);
     const uint32_t* w = a.words + (p0 >> 5);  // any word of the payload view
     const u32x4a4* w4 = reinterpret_cast<const u32x4a4*>(w);
@@ -2136,7 +2137,7 @@ __global__ __launch_bounds__(1024) void k_decode_fixed16(DecArgs a, uint64_t nb)
     const uint64_t j_begin = nb * kWave;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     copy_lds_table(lds, a.lds_img, a.lds_words);
-    const uint64_t p0 = a.starts[0] + a.bit_adj;  // the stream's first bit (the index holds nothing else we need)
+    const uint64_t p0 = (a.starts ? a.starts[0] : a.start0) + a.bit_adj;  // the stream's first bit (all FIXED16 needs)
     const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
     const uint32_t sh = (uint32_t)(p0 & 31);
     const uint64_t W0 = p0 >> 5;
@@ -2250,12 +2251,14 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
 
 hipError_t launch_decode(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t nsym,
                          const unsigned long long* d_index, uint8_t* d_out, uint32_t* d_err, int ncu,
-                         hipStream_t s) {
+                         hipStream_t s, uint64_t start0) {
     if (nsym == 0) return hipSuccess;
+    if (!d_index && t.dec_mode != DEC_FIXED16) return hipErrorInvalidValue;
     DecArgs a;
     fill_dec_args(a, t, d_payload, payload_bytes, nsym);
     a.starts = d_index;
-    a.subs = d_index + index_sub_offset(a.nblocks);
+    a.subs = d_index ? d_index + index_sub_offset(a.nblocks) : nullptr;
+    a.start0 = start0;
     a.out = d_out; a.err = d_err;
     if (t.dec_mode == DEC_FIXED16) {
         hipError_t e = ensure_lds_limit((const void*)k_decode_fixed16, kFixed16LdsBytes);
