@@ -1790,15 +1790,16 @@ HZ_DEV __amdgpu_buffer_rsrc_t lut_l2_rsrc(const uint32_t* l2) {
 // static LDS, so the table and slots are addressed from LDS byte 0. r[c].e: the entry
 // after LDS; r[c].gi: byte offset of its global entry in lut_l2_rsrc.
 template <int NC>
-HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* p1, PipeLane* r) {
+HZ_DEV void dec_pipe_ldsn(const DecArgs& a, const uint32_t* lds, const uint32_t* p1, PipeLane* r, uint32_t adj = 0) {
     const uint32_t k = (uint32_t)a.k;
     uint32_t W[NC], e[NC], x[NC];
     bool h[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         // descending slot (dec_stage_commit<true>): p1 holds m, stream word t + 1 at byte (m >> 3) & ~3,
-        // word t just above it, and m & 31 is the funnel shift (no v_not per step)
-        const uint32_t wb = (p1[c] >> 3) & ~3u;
+        // word t just above it, and m & 31 is the funnel shift (no v_not per step); adj: bytes the
+        // window lies above (p1 short by 128 bits per step taken, a multiple of 32: the shift holds)
+        const uint32_t wb = ((p1[c] >> 3) & ~3u) + adj;
         W[c] = __builtin_amdgcn_alignbit(lds_at(wb + 4), lds_at(wb), p1[c]);
     }
     HZ_WALK_FENCE();
@@ -2005,24 +2006,28 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         PipeLane st[C];
         uint32_t g[C];
         auto finish = [&](int c, int q) {
-            const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
-            p1[c] -= lut_leaf_len(ee);
+            // a leaf in LDS (bit 31) beats its gather's 0 (read past num_records); a link loses to its
+            // gathered leaf: one v_max; and the leaf's byte 3 is 0x80 | L, subtracted whole (128 bits
+            // more per step, which the window address takes back: dec_pipe_ldsn's adj). 12 % fewer VALU
+            // per block pair; k_decode 10.09 -> 9.97 ms, chain decode 11.30 -> 11.13 ms (A/B, 16 GiB Zipf)
+            const uint32_t ee = st[c].e > g[c] ? st[c].e : g[c];
+            p1[c] -= ee >> 24;
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
             // an even step keeps the whole entry; the odd step packs both symbols (leaf bytes 1-2) by one v_perm
             if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x06050201u);
             else pk[c / kChainsPerLane][i] = ee;
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
-        auto issue4 = [&](int c) {
-            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
+        auto issue4 = [&](int c, int q) {
+            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c, 16u * (uint32_t)q);  // q steps taken: 16 q bytes
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
         };
-        issue4(0);
+        issue4(0, 0);
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
-            issue4(4);
+            issue4(4, q);
             if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, mn[j], lane, sn[j]);
@@ -2031,7 +2036,7 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
             }
 #pragma unroll
             for (int c = 0; c < 4; ++c) finish(c, q);
-            if (q + 1 < kChainSyms) issue4(0);
+            if (q + 1 < kChainSyms) issue4(0, q + 1);
 #pragma unroll
             for (int c = 4; c < 8; ++c) finish(c, q);
         }
@@ -3780,22 +3785,26 @@ HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, co
         PipeLane st[C];
         uint32_t g[C];
         auto finish = [&](int c, int q) {
-            const uint32_t ee = lut_leaf(st[c].e) ? st[c].e : g[c];
-            p1[c] -= lut_leaf_len(ee);
+            // a leaf in LDS (bit 31) beats its gather's 0 (read past num_records); a link loses to its
+            // gathered leaf: one v_max; and the leaf's byte 3 is 0x80 | L, subtracted whole (128 bits
+            // more per step, which the window address takes back: dec_pipe_ldsn's adj). 12 % fewer VALU
+            // per block pair; k_decode 10.09 -> 9.97 ms, chain decode 11.30 -> 11.13 ms (A/B, 16 GiB Zipf)
+            const uint32_t ee = st[c].e > g[c] ? st[c].e : g[c];
+            p1[c] -= ee >> 24;
             const int i = ((c % kChainsPerLane) * kChainSyms + q) >> 1;
             if (q & 1) pk[c / kChainsPerLane][i] = __builtin_amdgcn_perm(ee, pk[c / kChainsPerLane][i], 0x06050201u);
             else pk[c / kChainsPerLane][i] = ee;
         };
-        auto issue4 = [&](int c) {
-            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c);
+        auto issue4 = [&](int c, int q) {
+            dec_pipe_ldsn<4>(a, lds, p1 + c, st + c, 16u * (uint32_t)q);  // q steps taken: 16 q bytes
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
         };
-        issue4(0);
+        issue4(0, 0);
 #pragma unroll
         for (int q = 0; q < kChainSyms; ++q) {
-            issue4(4);
+            issue4(4, q);
             if (q == kPfStep) {  // the next two blocks' staging chunks, the metadata after them
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, as_pipe(mn[j]), lane, sn[j]);
@@ -3804,7 +3813,7 @@ HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, co
             }
 #pragma unroll
             for (int c = 0; c < 4; ++c) finish(c, q);
-            if (q + 1 < kChainSyms) issue4(0);
+            if (q + 1 < kChainSyms) issue4(0, q + 1);
 #pragma unroll
             for (int c = 4; c < 8; ++c) finish(c, q);
         }
