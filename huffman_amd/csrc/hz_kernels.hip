@@ -3904,11 +3904,14 @@ __global__ __launch_bounds__(kSyncThreads) void k_chain_tail(DecArgs a, ChainArg
 
 // ---- host side -----------------------------------------------------------------------------
 // Chain geometry of a part of the payload (bits [pbeg, pend) after start): chains of cbits bits, about
-// one per walk lane of the device (16 waves per CU), but at least kChainMinBlocks decode blocks long;
+// one per walk lane of the device (16 waves per CU), but at least kChainMinBlocks decode block long;
 // each chain's record capacity holds its expected records with 25 % headroom (more go to
 // k_chain_tail, serially). avg: expected payload bits per codeword (the lower of the payload's own
 // and the codebook's Kraft estimate: more records, more headroom).
-constexpr uint64_t kChainMinBlocks = 4;
+// (one: a part of ~2 Gbit -- the CLI's 256 MiB payload windows -- gets 90 K chains instead of 23 K, so
+// the walk is not occupancy-starved: 1.85 -> 0.96 ms per window call, 1 GiB 2.50 -> 1.93 ms; 2 blocks:
+// 1.21 / 1.94 ms; long parts are lane-limited and unaffected)
+constexpr uint64_t kChainMinBlocks = 1;
 struct ChainGeom {
     uint64_t nchains = 0, cbits = 0, pbeg = 0, pend = 0;
     uint32_t bpc = 0, cap = 0;

@@ -71,13 +71,59 @@ def test_indexless_table_shapes(codec, name):
     assert ok and end_ok
 
 
-def test_indexless_uniform_fixed16(codec):
+def test_indexless_uniform_near16(codec):
+    """Uniform bytes at 16 MiB: counts vary by more than 2x, so codes of 15-17 bits (the chain path)."""
     import torch
     n = (16 << 20) + 2
     x = torch.empty(n, dtype=torch.uint8, device="cuda")
     codec.dev.generate(x.data_ptr(), n, offset=0, kind=0, alpha=1.1, seed=3)
     ok, end_ok = _check(codec, x)
     assert ok and end_ok
+
+
+# (every count within 2x of every other -- all codes 16 bits -- needs about 48 MiB of uniform bytes)
+@pytest.mark.parametrize("n,shift", [((64 << 20) + 2, 0), ((48 << 20) + 6, 5)])
+def test_indexless_uniform_fixed16(codec, n, shift):
+    """FIXED16 (every code 16 bits): hz_decode_indexless decodes symbol i from start + 16 i directly
+    (no walk, no index); payload moved any number of bytes into its buffer."""
+    import torch
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=0, alpha=1.1, seed=3)
+    plan, _, _ = codec.encode(x)
+    codec.sync()
+    assert int(plan.cb.min_len) == 16 and int(plan.cb.max_len) == 16  # the FIXED16 path is the one tested
+    ok, end_ok = _check(codec, x, shift)
+    assert ok and end_ok
+
+
+def test_indexless_fixed16_truncated_and_captured(codec):
+    """FIXED16 index-less decode: a payload short of nsym codes reports the end bit past it; the call is
+    stream-ordered (captured in a HIP graph and replayed bit-exact)."""
+    import torch
+    n = (48 << 20) + 2
+    nsym = n // 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=0, alpha=1.1, seed=4)
+    plan, payload, _ = codec.encode(x)
+    codec.sync()
+    assert int(plan.cb.min_len) == 16 and int(plan.cb.max_len) == 16
+    out = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    end = torch.zeros(2, dtype=torch.int64, device="cuda")
+    cut = payload.numel() // 2
+    codec.dev.decode_indexless(payload.data_ptr(), cut, plan.start_bit, nsym, out.data_ptr(), end.data_ptr())
+    codec.sync()
+    assert int(end[0].item()) & ((1 << 64) - 1) > 8 * cut
+    end.fill_(0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=codec.stream):
+        codec.dev.decode_indexless(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, out.data_ptr(),
+                                   end.data_ptr())
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out[:n], x)
+    assert int(end[0].item()) == plan.start_bit + 16 * nsym
 
 
 def test_indexless_truncated_end_past_payload(codec):
