@@ -139,6 +139,10 @@ class StreamCodec:
         unchanged since: stream order) in one pass over x, else count + scan + write. A plan is
         used once. index may be None: no block index is written (the drop-in file path)."""
         iptr = index.data_ptr() if index is not None else 0
+        if x.data_ptr() % 16:
+            # hz_pack reads 16-byte vectors (include/huffman_amd.h): an unaligned view is packed from an
+            # aligned copy (its histogram took hz_hist16, so there is no range plan to match)
+            x = x.clone()
         if self._ranges_of is not None and self._ranges_of == self._ident(x):
             self._ranges_of = None
             self.dev.pack_ranges(x.data_ptr(), x.numel(), plan.start_bit, plan.lead, out.data_ptr(), out.numel(),

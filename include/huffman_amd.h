@@ -162,9 +162,9 @@ uint64_t hz_index_stride(void);
 uint64_t hz_index_bytes(uint64_t nsym);
 uint64_t hz_scratch_bytes(uint64_t nsym);
 
-/* Pack the n/2 symbols of d_in with the uploaded codebook into d_out as one
- * MSB-first bit stream beginning at bit `start_bit` of d_out (d_out 4-byte
- * aligned; bits of d_out's first word before start_bit are taken from `lead`,
+/* Pack the n/2 symbols of d_in (16-byte aligned: HZ_EINVAL otherwise) with the
+ * uploaded codebook into d_out as one MSB-first bit stream beginning at bit
+ * `start_bit` of d_out (d_out 4-byte aligned; bits of d_out's first word before start_bit are taken from `lead`,
  * right aligned, i.e. the header's pending bits). Bits after the stream's end
  * up to the next 32-bit word are zero. d_index (optional, hz_index_bytes())
  * receives the block index. Replaces
@@ -278,9 +278,13 @@ int hz_archive_file(const char *path, int verbose);
  * 256 MiB chunks. Replaces the whole-file buffers of Compressor.cu:343-367,585-601. */
 int hz_archive_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* Streaming extract of in_path into out_path through a device window of
- * chunk_bytes of payload (index-less: hz_index_build per window), bounded
- * host and device memory. hz_extract_file uses it with 256 MiB windows.
- * Replaces the whole-file buffers of Decompressor.cu:65-114,259-291. */
+ * chunk_bytes of payload, bounded host and device memory: each round decodes
+ * the codewords the window surely holds with hz_decode_indexless (no block
+ * index) and carries the unconsumed tail into the next window; the host waits
+ * once per round (for the round's end bit), and the next window's file read
+ * and this round's fwrite overlap the device. hz_extract_file uses it with
+ * 256 MiB windows. Replaces the whole-file buffers of
+ * Decompressor.cu:65-114,259-291. */
 int hz_extract_stream(const char *in_path, const char *out_path, uint64_t chunk_bytes, int verbose);
 /* Stage split of the calling thread's last hz_archive_stream /
  * hz_extract_stream call (hz_archive_file / hz_extract_file included). Stage

@@ -143,3 +143,31 @@ def test_range_plan_pipeline_matches_oracle_slices(built_lib):
     assert c.file_image(plan, payload) == oracle_lib.encode(host)
     del x
     torch.cuda.empty_cache()
+
+
+def test_unaligned_view_of_256mib_encodes_like_an_aligned_copy(built_lib):
+    """An input view that is not 16-byte aligned (no range plan: hz_hist16 + count + scan + write)
+    encodes to the same payload and index as an aligned copy of the same bytes (the range plan), and
+    decodes back (the range plan must not be taken for unaligned inputs)."""
+    import torch
+    from huffman_amd.pipeline import StreamCodec
+    codec = StreamCodec(0)
+    n = (256 << 20) + 2
+    big = torch.empty(n + 32, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(big.data_ptr(), n + 32, offset=0, kind=1, alpha=1.1, seed=17)
+    view = big[3:3 + n]
+    assert view.data_ptr() % 16 != 0
+    plan_u, pay_u, idx_u = codec.encode(view)
+    codec.sync()
+    copy = view.clone()
+    assert copy.data_ptr() % 16 == 0
+    plan_a, pay_a, idx_a = codec.encode(copy)
+    codec.sync()
+    assert plan_u.payload_bits == plan_a.payload_bits
+    nbytes = (plan_a.payload_bits + plan_a.start_bit + 7) // 8
+    assert torch.equal(pay_u[:nbytes], pay_a[:nbytes])
+    assert torch.equal(idx_u, idx_a)
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(pay_u, n // 2, idx_u, out)
+    codec.sync()
+    assert torch.equal(out[:n], copy)
