@@ -104,9 +104,9 @@ enum DecMode : int {
     DEC_LUT = 1,    // 2^K1 u32 level-1 entries in LDS, deeper levels in global
     DEC_FIXED16 = 2 // every code 16 bits: u16 symbol per code in LDS, positions are arithmetic
 };
-constexpr int kDecLutMaxK1 = 13;  // + 9-bit global levels: pipelined up to 22-bit codes
-constexpr int kDecLevelBits = 11; // widest global subtable (each link's is as wide as its codes need; fewer
-                                  // bits when the table would exceed kLutMaxL2): codes up to 24 bits in two levels
+constexpr int kDecLutMaxK1 = 13;  // + global levels of up to kDecLevelBits: pipelined up to 25-bit codes
+constexpr int kDecLevelBits = 12; // widest global subtable (each link's is as wide as its codes need; fewer
+                                  // bits when the table would exceed kLutMaxL2): codes up to 25 bits in two levels
 // LUT entries (DEC_LUT; hz_codebook.cpp build_dec_lut):
 //   leaf  1 << 31 | L << 24 | sym << 8   (bits 7..0 zero)
 //   link  raw << 10 | nb << 5 | pos   (bit 31 clear). raw < kLutGlobal: the subtable starts at word raw of
@@ -138,7 +138,7 @@ constexpr int kDecMaxWaves = 16;
 // round 25.3 vs 8 steps 25.5 ms. With the earlier u32 LUT walker: 2 chains per
 // lane x 4 waves 53.7 vs 1 x 8 waves 38.4 ms.
 constexpr int kWalkK = 17;            // walker length table: 2^17 4-bit lengths (64 KB) in LDS
-constexpr int kWalkMaxLen = 24;       // escape table: 2^max_len u8 in global memory (<= 16 MiB)
+constexpr int kWalkMaxLen = 25;       // escape table: 2^max_len u8 in global memory (<= 32 MiB)
 constexpr int kWalkChains = 1;
 constexpr int kWalkWaves = 12;
 constexpr uint32_t kWalkMarkChunks = 2;

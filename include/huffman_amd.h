@@ -226,7 +226,7 @@ int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes
  * unless the context's scratch grows. A FIXED16 codebook (every code 16 bits)
  * needs no walk: symbol i sits at start_bit + 16 i, decoded directly (also
  * stream-ordered). Codebooks the chain decoder does not take (codes longer than
- * 24 bits, DENSE tables) go through hz_index_build + hz_decode, with the same
+ * 25 bits, DENSE tables) go through hz_index_build + hz_decode, with the same
  * result (that path synchronises). */
 int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                         uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);

@@ -226,7 +226,7 @@ def _split_worker(rank, world, port, n_total, lead, result_dir):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world,n_total,lead", [(2, (8 << 20) + 2, None), (3, (24 << 20) + 6, None),
-                                                (8, (24 << 20) + 6, None), (4, (16 << 20) + 2, 0)])
+                                                (8, (64 << 20) + 2, None), (4, (16 << 20) + 2, 0)])
 def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead):
     mp.start_processes(_split_worker, args=(world, _free_port(), n_total, lead, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")

@@ -232,3 +232,36 @@ def test_indexless_graph_capture(codec):
         torch.cuda.synchronize()
         assert torch.equal(out[:n], x)
         assert int(end[0].item()) == end_pack
+
+
+def test_indexless_25_bit_codes_stream_ordered(codec):
+    """A codebook with 25-bit codes (this 48 MiB Zipf stream) takes the chain path too (global subtables
+    of up to 12 bits, a 2^25-byte escape table): captured in a HIP graph and replayed bit-exact."""
+    import torch
+    from huffman_amd import index_starts
+    n = (48 << 20) + 2
+    nsym = n // 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=1, alpha=1.1, seed=21)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    assert int(plan.cb.max_len) == 25
+    end_pack = int(index_starts(index.cpu().numpy(), nsym)[-1])
+    out = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    end = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+
+    def call():
+        codec.dev.decode_indexless(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, out.data_ptr(),
+                                   end.data_ptr())
+
+    call()
+    codec.sync()
+    assert torch.equal(out[:n], x) and int(end[0].item()) == end_pack
+    out.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=codec.stream):
+        call()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out[:n], x)
