@@ -410,6 +410,9 @@ struct PackArgs {
     uint32_t slot_words;         // k_pack_write: per-wave LDS output slot (0: store from the lanes)
     const unsigned long long* rstart;  // range plan: start bit of every range (k_range_scan)
     uint64_t bpr, nranges;       // range plan: blocks per range, ranges
+    // blocks k_pack_write leaves to k_pack_cold (all but WIDE): [0] = count, then (block, start bit)
+    // pairs -- the stream's last block and blocks larger than the wave's LDS slot
+    unsigned long long* cold;
 };
 
 template <int MODE> struct PackEnt { using T = uint32_t; static constexpr int kShift = 26; };
@@ -714,10 +717,18 @@ struct PackBlk {
     int nvalid;
 };
 
-template <int MODE, typename Mid = NoMid>
+// FULL_ONLY: every lane's 32 symbols are in the stream (k_pack_write's split loop: the stream's last
+// block, the only partial one, is packed again by k_pack_cold; this pass only needs its lookups to be
+// in bounds, which pack_prefetch's clamp gives)
+template <int MODE, bool FULL_ONLY = false, typename Mid = NoMid>
 HZ_DEV void pack_block_lookup(const PackArgs& a, const uint32_t* lds, uint64_t blk, int lane, PackIn& in,
                               PackBlk<MODE>& b, Mid mid = Mid()) {
     const uint64_t sym0 = blk * kBlockSyms + (uint64_t)lane * kSPT;
+    if constexpr (FULL_ONLY) {
+        b.nvalid = kSPT;
+        pack_lookup<MODE, true>(a, lds, sym0, b.nvalid, in.raw, b.e, in.psym, b.pe, mid);
+        return;
+    }
     b.nvalid = sym0 >= a.nsym ? 0 : (a.nsym - sym0 >= (uint64_t)kSPT ? kSPT : (int)(a.nsym - sym0));
     // a wave-uniform choice: mid() may run wave-wide code (DPP scans of the pipelined emit), so it
     // must not run once per branch of a divergent split (the stream's last block mixes full and
@@ -789,8 +800,10 @@ HZ_DEV void pack_block_count(int lane, PackBlk<MODE>& b) {
     b.bits = readlane(sn, 63);
 }
 
-// Writes block `blk` starting at absolute bit `bstart`, plus its index entries.
-template <int MODE>
+// Writes block `blk` starting at absolute bit `bstart`, plus its index entries. SLOT_ONLY: the caller
+// has checked that the block goes through the wave's LDS slot (not the last block, fits the slot), so
+// the direct path is not compiled in.
+template <int MODE, bool SLOT_ONLY = false>
 HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int lane, const PackBlk<MODE>& b,
                             uint64_t bstart, uint64_t& max_bits, PackOut* defer = nullptr) {
     using T = typename PackEnt<MODE>::T;
@@ -826,7 +839,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
     const uint64_t wfirst = bstart >> 5;
     const uint32_t nwords = (uint32_t)((bend >> 5) - wfirst);  // words completed inside the block
     const uint32_t sh4 = (uint32_t)(wfirst & 3);  // slot word i holds output word (wfirst & ~3) + i
-    if (slot && !last && nwords + sh4 <= a.slot_words) {
+    if (SLOT_ONLY || (slot && !last && nwords + sh4 <= a.slot_words)) {
         // Every lane holds 32 codes of >= 1 bit, so its last 32 bits are its
         // own: emit with the leading bits zero, then OR in the previous
         // lane's tail once all lanes are done. The slot is laid out like the
@@ -892,7 +905,7 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
             }
         }
         __builtin_amdgcn_wave_barrier();
-    } else {
+    } else if constexpr (!SLOT_ONLY) {
         // direct path: each lane needs the 32 bits before its run from the
         // (bits, tail) scan, since a lane of the last block may hold < 32 bits
         uint64_t t64 = 0;
@@ -947,8 +960,12 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
     // Output slot of this wave: the block's words are assembled in LDS and
-    // leave as contiguous 256-byte stores (a block that does not fit, and the
-    // stream's last block, store straight from the lanes).
+    // leave as contiguous 256-byte stores. A block that does not fit, and the
+    // stream's last block, go to k_pack_cold (kSplit: all but WIDE, whose
+    // loop keeps the in-line direct path): without that path in the loop the
+    // kernel needs 70 SGPRs and 152 VGPRs instead of 106 (51 spilled to VGPR
+    // lanes, reloaded every block) and 175 (pack 8.6 -> 8.1-8.3 ms, 16 GiB Zipf).
+    constexpr bool kSplit = MODE != ENC_WIDE;
     // (the wave index stays a VGPR value here: as a scalar, 12.4-12.7 vs 11.8-12.2 ms pack stage)
     uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -981,16 +998,55 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
         PackIn cur = nx;
         PackBlk<MODE> b;
         // the previous block's stores go out behind this block's escape loads
-        pack_block_lookup<MODE>(a, lds, blk, lane, cur, b, [&]() { pack_copyout(a, slot, lane, po); });
+        pack_block_lookup<MODE, kSplit>(a, lds, blk, lane, cur, b, [&]() { pack_copyout(a, slot, lane, po); });
         po.pending = false;
         // next block's loads: after this block's escapes, so no wait covers them early
         pack_prefetch(a, nb < a.nblocks ? nb : blk, lane, nx);
         pack_block_count<MODE>(lane, b);
-        pack_block_emit<MODE>(a, slot, blk, lane, b, RNG ? run : cur.bstart, max_bits, &po);
+        const uint64_t bst = RNG ? run : cur.bstart;
+        if constexpr (kSplit) {
+            const uint64_t wfirst = bst >> 5;
+            const uint32_t nwords = (uint32_t)(((bst + b.bits) >> 5) - wfirst), sh4 = (uint32_t)(wfirst & 3);
+            if (blk + 1 == a.nblocks || nwords + sh4 > a.slot_words) {  // slot_words 0: no slots, all cold
+                if (lane == 0) {
+                    const unsigned long long i = atomicAdd(a.cold, 1ull);
+                    a.cold[1 + 2 * i] = blk;
+                    a.cold[2 + 2 * i] = bst;
+                }
+            } else {
+                pack_block_emit<MODE, true>(a, slot, blk, lane, b, bst, max_bits, &po);
+            }
+        } else {
+            pack_block_emit<MODE>(a, slot, blk, lane, b, bst, max_bits, &po);
+        }
         if (RNG) run = newr ? nrun : run + b.bits;
         blk = nb;
     }
     pack_copyout(a, slot, lane, po);
+    if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
+}
+
+// The blocks k_pack_write listed in a.cold (the stream's last block, which may be partial, and blocks
+// larger than a wave's LDS slot): per-symbol masked lookups, each lane's codes stored straight to the
+// output, the index entries. Usually one block; workgroups past the list leave before loading the table.
+template <int MODE>
+__global__ __launch_bounds__(kPackWriteThreads) void k_pack_cold(PackArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint64_t n = a.cold[0];
+    const uint64_t waves = blockDim.x >> 6, W = (uint64_t)gridDim.x * waves;
+    if ((uint64_t)blockIdx.x * waves >= n) return;  // uniform over the workgroup
+    load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
+    const int lane = threadIdx.x & 63;
+    uint64_t max_bits = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * waves + (threadIdx.x >> 6); i < n; i += W) {
+        const uint64_t blk = a.cold[1 + 2 * i], bst = a.cold[2 + 2 * i];
+        PackIn in;
+        pack_prefetch(a, blk, lane, in);
+        PackBlk<MODE> b;
+        pack_block_lookup<MODE>(a, lds, blk, lane, in, b);
+        pack_block_count<MODE>(lane, b);
+        pack_block_emit<MODE>(a, nullptr, blk, lane, b, bst, max_bits, nullptr);
+    }
     if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
 }
 
@@ -1297,7 +1353,22 @@ __global__ __launch_bounds__(kScanThreads) void k_range_scan(RangeArgs r, uint64
 uint64_t pack_scratch_words(uint64_t nsym) {
     const uint64_t nblocks = (nsym + kBlockSyms - 1) / kBlockSyms;
     const uint64_t ntiles = (nblocks + kScanTile - 1) / kScanTile;
-    return 2 * nblocks + ntiles;
+    return 2 * nblocks + ntiles + 1 + 2 * nblocks;  // counts, starts, scan tiles, k_pack_cold's list
+}
+
+// k_pack_write's list of blocks for k_pack_cold: zero the count first, run the cold pass after.
+static hipError_t pack_cold_reset(const PackArgs& a, hipStream_t s) {
+    return hipMemsetAsync(a.cold, 0, sizeof(unsigned long long), s);
+}
+static void pack_cold_launch(const Tables& t, const PackArgs& a, uint32_t lds, int ncu, hipStream_t s) {
+    const uint64_t waves = kPackWriteThreads / 64;
+    uint64_t g = (a.nblocks + waves - 1) / waves;
+    if (g > (uint64_t)ncu) g = ncu;  // table-sized LDS: one workgroup per CU
+    switch (t.enc_mode) {
+        case ENC_DENSE: hipLaunchKernelGGL(k_pack_cold<ENC_DENSE>, dim3(g), dim3(kPackWriteThreads), lds, s, a); break;
+        case ENC_HOT: hipLaunchKernelGGL(k_pack_cold<ENC_HOT>, dim3(g), dim3(kPackWriteThreads), lds, s, a); break;
+        default: break;  // WIDE keeps the direct path inside k_pack_write
+    }
 }
 
 hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint64_t start_bit, uint32_t lead,
@@ -1320,6 +1391,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     a.blk_start = blk_start; a.index = d_index; a.err = d_err;
     a.index_sub = d_index ? d_index + index_sub_offset(nblocks) : nullptr;
     a.rstart = nullptr; a.bpr = 0; a.nranges = 0;
+    a.cold = tiles + ntiles;
     if (d_index && t.enc_mode != ENC_FIXED16) {
         hipError_t e = hipMemsetAsync(d_index + nblocks + 1, 0, 8, s);  // max_bits, raised per block
         if (e != hipSuccess) return e;
@@ -1366,6 +1438,13 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     if (wgs > cap) wgs = cap;
     // Range plan (the histogram's snapshots, hz_hist16_ranges): every pack wave takes whole ranges,
     // so the plan is used when the waves cover the ranges evenly; else count + scan + write.
+    const bool split = t.enc_mode != ENC_WIDE;  // k_pack_write leaves its cold blocks to k_pack_cold
+    if (split) {
+        const void* fc = t.enc_mode == ENC_DENSE ? (const void*)k_pack_cold<ENC_DENSE> : (const void*)k_pack_cold<ENC_HOT>;
+        hipError_t e = ensure_lds_limit(fc, kLdsBytes);
+        if (e != hipSuccess) return e;
+        if ((e = pack_cold_reset(a, s)) != hipSuccess) return e;
+    }
     const RangeGeom g = d_ranges ? range_geom(nsym) : RangeGeom{};
     if (g.bytes && t.d_lenpair) {
         uint64_t rw = (g.nranges + waves - 1) / waves;
@@ -1386,6 +1465,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
                 case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, true>), dim3(rw), dim3(threads), lds, s, a); break;
                 default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, true>), dim3(rw), dim3(threads), lds, s, a); break;
             }
+            if (split) pack_cold_launch(t, a, 4 * table_words, ncu, s);
             if (used_ranges) *used_ranges = 1;
             return hipGetLastError();
         }
@@ -1413,6 +1493,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
         case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, false>), dim3(wgs), dim3(threads), lds, s, a); break;
         default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
     }
+    if (split) pack_cold_launch(t, a, 4 * table_words, ncu, s);
     return hipGetLastError();
 }
 

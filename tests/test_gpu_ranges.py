@@ -171,3 +171,38 @@ def test_unaligned_view_of_256mib_encodes_like_an_aligned_copy(built_lib):
     codec.decode(pay_u, n // 2, idx_u, out)
     codec.sync()
     assert torch.equal(out[:n], copy)
+
+
+def test_range_plan_blocks_over_the_slot_match_oracle(dev):
+    """Blocks larger than a pack wave's LDS slot (runs of rare symbols, ~20-bit codes, in a Zipf
+    stream) and the stream's partial last block leave k_pack_write for k_pack_cold's list: spans at
+    block-aligned and unaligned offsets in several ranges, one covering the last block. The range
+    plan and the three-pass encode agree byte for byte (payload and block index), the plan's file
+    equals the oracle's, and the stream decodes back."""
+    import torch
+    from huffman_amd.pipeline import StreamCodec
+    n = 256 * MIB + 2 * 777 + 1
+    x = _zipf(n, 5)
+    host = x.cpu().numpy()
+    sym = host[: n - 1].view("<u2")
+    rng = np.random.default_rng(3)
+    nsym = sym.size
+    for s0, ln in [(2048 * 7, 2048 * 3), (2048 * 4001 + 100, 5000), (nsym // 2 + 33, 2048 * 9 + 17),
+                   (nsym - 2048 * 2 - 5, 2048 * 2 + 5)]:
+        sym[s0:s0 + ln] = rng.integers(20000, 65536, ln)
+    x.copy_(torch.from_numpy(host))
+    torch.cuda.synchronize()
+    ((h3, p3, i3, _, _), (hr, pr, ir, took, _)), nb, _ = _both(dev, x, 0, 0)
+    assert took == 1, "the range plan did not run"
+    assert np.array_equal(p3, pr)
+    assert np.array_equal(i3.view(np.uint8)[:nb], ir.view(np.uint8)[:nb])
+    c = StreamCodec(0)
+    plan, payload, index = c.encode(x)
+    assert c.dev.last_pack_ranges() == 1
+    assert c.file_image(plan, payload) == oracle_lib.encode(host)
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    c.decode(payload, nsym, index, out)
+    c.sync()
+    assert torch.equal(out[: n - 1], x[: n - 1])
+    del x, out
+    torch.cuda.empty_cache()
