@@ -459,6 +459,74 @@ HZ_DEV void pack_prefetch(const PackArgs& a, uint64_t blk, int lane, PackIn& x) 
     x.bstart = a.blk_start ? a.blk_start[blk] : 0;  // range pack: a running sum instead
 }
 
+// HOT lookups of one block in two halves, for k_pack_write's pipelined loop: issue (slot
+// addresses, LDS reads, hit tests, the 33 escape loads) and, a block later, finish (the blends),
+// so the escape loads' latency is covered by the previous block's count and emit.
+struct HotLook {
+    uint32_t x[kSPT], mk[kSPT], v[kSPT];
+    uint32_t xx, xmk, xv;
+};
+// Slot arithmetic on both symbols of a word at once (packed 16-bit shifts): slot = s ^ (mask if
+// bit 15), LDS word hot_word(slot); byte addresses (the table sits at LDS byte 0 of the pack
+// kernels). A slot's entry carries its owner's bit 15 as the tag in bit 31: hit <=> bit 31 of
+// entry ^ (s << 16) is 0. A miss is the slot's other symbol, whose entry the escape table holds at
+// the same byte offset, so the escape address is one AND. !FULL: symbols k >= nvalid read 0.
+template <bool FULL>
+HZ_DEV void hot_issue(const PackArgs& a, const uint32_t (&raw)[kSPT / 2], uint32_t xs, HotLook& h, int nvalid = kSPT) {
+    const uint32_t m2 = a.hot_mask | (a.hot_mask << 16);
+    uint32_t ad[kSPT];
+#pragma unroll
+    for (int j = 0; j < kSPT / 2; ++j) {
+        const uint32_t r = raw[j];
+        // (inline asm with an inline-constant shift would shift the high half by 0: VOP3P takes
+        // a constant for the low half only; vector types let the compiler place the operands)
+        const uint32_t sgn = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_i16x2, r) >> (hz_i16x2){15, 15});
+        const uint32_t sl = r ^ (sgn & m2);
+        const uint32_t hi8 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_u16x2, sl) >> (hz_u16x2){8, 8});
+        // hw = sl ^ (hi8 & 0x003f003f) as one v_bitop3 (the mask in an SGPR: the compiler emits an
+        // AND and an XOR for the literal), and each half's slot byte address as one SDWA shift
+        // (pack 8.62 -> 8.50 ms, A/B)
+        uint32_t hw, a0, a1;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(hw) : "s"(a.hw_mask), "v"(sl), "v"(hi8));
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+            : "=v"(a0) : "v"(2u), "v"(hw));
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+            : "=v"(a1) : "v"(2u), "v"(hw));
+        ad[2 * j] = a0;
+        ad[2 * j + 1] = a1;
+    }
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        h.x[k] = lds_at(ad[k]);
+        if (!FULL) h.x[k] = k < nvalid ? h.x[k] : 0u;
+    }
+    uint32_t xslot = xs ^ ((uint32_t)((int32_t)(xs << 16) >> 31) & a.hot_mask);
+    xslot = hot_word(xslot & 0x7fffu) << 2;
+    h.xx = lds_at(xslot);
+    const char* esc = reinterpret_cast<const char*>(a.esc);
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        const uint32_t tag = (k & 1) ? raw[k >> 1] : raw[k >> 1] << 16;
+        h.mk[k] = (uint32_t)((int32_t)(h.x[k] ^ tag) >> 31);
+        h.v[k] = *reinterpret_cast<const uint32_t*>(esc + (ad[k] & h.mk[k]));
+    }
+    h.xmk = (uint32_t)((int32_t)(h.xx ^ (xs << 16)) >> 31);
+    h.xv = *reinterpret_cast<const uint32_t*>(esc + (xslot & h.xmk));
+}
+// the blend is a v_bfi the compiler cannot turn back into a select: written as `miss ? esc[s] : e`
+// the loads become 33 exec-masked branches (12.73-12.87 vs 12.61-12.67 ms at 16 GiB Zipf, round 3 A/B)
+HZ_DEV void hot_finish(const HotLook& h, uint32_t (&e)[kSPT], uint32_t& xe) {
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {
+        uint32_t r;
+        asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(h.mk[k]), "v"(h.v[k]), "v"(h.x[k]));
+        e[k] = r;
+    }
+    uint32_t r;
+    asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(h.xmk), "v"(h.xv), "v"(h.xx));
+    xe = r;
+}
+
 // (len, code) of the lane's 32 symbols in register format (len << SH | code),
 // plus the entry of one more symbol `xs` (the previous block's tail). HOT
 // slots hold tag << 31 | len << 26 | code, and every occurring symbol's code
@@ -501,66 +569,10 @@ HZ_DEV void pack_lookup(const PackArgs& a, const uint32_t* lds, uint64_t sym0, i
         xe = pack_dense_one<T, SH>(lds, xs);
         mid();
     } else if constexpr (MODE == ENC_HOT) {
-        // Slot arithmetic on both symbols of a word at once (packed 16-bit shifts): slot =
-        // s ^ (mask if bit 15), LDS word hot_word(slot); byte addresses (the table sits at LDS
-        // byte 0 of k_pack_write). A slot's entry carries its owner's bit 15 as the tag in bit 31:
-        // hit <=> bit 31 of entry ^ (s << 16) is 0. A miss is the slot's other symbol, whose
-        // entry the escape table holds at the same byte offset, so the escape address is one AND.
-        const uint32_t m2 = a.hot_mask | (a.hot_mask << 16);
-        uint32_t ad[kSPT];
-#pragma unroll
-        for (int j = 0; j < kSPT / 2; ++j) {
-            const uint32_t r = raw[j];
-            // (inline asm with an inline-constant shift would shift the high half by 0: VOP3P takes
-            // a constant for the low half only; vector types let the compiler place the operands)
-            const uint32_t sgn = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_i16x2, r) >> (hz_i16x2){15, 15});
-            const uint32_t sl = r ^ (sgn & m2);
-            const uint32_t hi8 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(hz_u16x2, sl) >> (hz_u16x2){8, 8});
-            // hw = sl ^ (hi8 & 0x003f003f) as one v_bitop3 (the mask in an SGPR: the compiler emits an
-            // AND and an XOR for the literal), and each half's slot byte address as one SDWA shift (pack 8.62 -> 8.50 ms, A/B)
-            uint32_t hw, a0, a1;
-            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(hw) : "s"(a.hw_mask), "v"(sl), "v"(hi8));
-            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
-                : "=v"(a0) : "v"(2u), "v"(hw));
-            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-                : "=v"(a1) : "v"(2u), "v"(hw));
-            ad[2 * j] = a0;
-            ad[2 * j + 1] = a1;
-        }
-        uint32_t x[kSPT];
-#pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            x[k] = lds_at(ad[k]);
-            if (!FULL) x[k] = k < nvalid ? x[k] : 0u;
-        }
-        uint32_t xslot = xs ^ ((uint32_t)((int32_t)(xs << 16) >> 31) & a.hot_mask);
-        xslot = hot_word(xslot & 0x7fffu) << 2;
-        const uint32_t xx = lds_at(xslot);
-        const char* esc = reinterpret_cast<const char*>(a.esc);
-        uint32_t v[kSPT], mk[kSPT];
-#pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            const uint32_t tag = (k & 1) ? raw[k >> 1] : raw[k >> 1] << 16;  // the symbol's bit 15 in bit 31
-            mk[k] = (uint32_t)((int32_t)(x[k] ^ tag) >> 31);
-            v[k] = *reinterpret_cast<const uint32_t*>(esc + (ad[k] & mk[k]));
-        }
-        const uint32_t xmk = (uint32_t)((int32_t)(xx ^ (xs << 16)) >> 31);
-        const uint32_t xv = *reinterpret_cast<const uint32_t*>(esc + (xslot & xmk));
+        HotLook h;
+        hot_issue<FULL>(a, raw, xs, h, nvalid);
         mid();
-        // the blend is a v_bfi the compiler cannot turn back into a select: written as
-        // `miss ? esc[s] : e` the loads become 33 exec-masked branches (12.73-12.87 vs
-        // 12.61-12.67 ms at 16 GiB Zipf, round 3 A/B)
-#pragma unroll
-        for (int k = 0; k < kSPT; ++k) {
-            uint32_t r;
-            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk[k]), "v"(v[k]), "v"(x[k]));
-            e[k] = (T)r;
-        }
-        {
-            uint32_t r;
-            asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(xmk), "v"(xv), "v"(xx));
-            xe = (T)r;
-        }
+        hot_finish(h, e, xe);
     } else {
 #pragma unroll
         for (int k = 0; k < kSPT; ++k) {
@@ -977,10 +989,79 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
         rend = blk + a.bpr < a.nblocks ? blk + a.bpr : a.nblocks;
         run = r < a.nranges ? a.rstart[r] : 0;
     }
-    PackIn nx;  // the next block's inputs, in flight while this block is packed
-    if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
     PackOut po;
     po.pending = false;
+    if constexpr (MODE == ENC_HOT) {
+        // Pipelined: block k is finished (blends) and emitted while block k+1's escape loads and
+        // block k+2's input are in flight; the wave's block sequence runs two ahead of the emit.
+        // 239 VGPRs (LDS already holds the kernel at 2 waves per SIMD); pack 8.42 -> 8.33 ms mean
+        // of 5 paired runs. The escapes cost issue/TA throughput more than latency: without them
+        // pack takes 7.8-7.9 ms, and skipping a load no lane needs (a uniform branch) is slower
+        // (8.95-9.06 ms: +2 VALU per symbol).
+        auto next = [&](uint64_t b, bool& newr, uint64_t& nrun) -> uint64_t {
+            newr = false;
+            nrun = 0;
+            if (!RNG) return b + W;
+            if (b + 1 < rend) return b + 1;
+            r += W;  // the wave's next range
+            newr = true;
+            const uint64_t n = r < a.nranges ? r * a.bpr : a.nblocks;
+            rend = n + a.bpr < a.nblocks ? n + a.bpr : a.nblocks;
+            nrun = r < a.nranges ? a.rstart[r] : 0;
+            return n;
+        };
+        bool nb_newr;
+        uint64_t nb_run;
+        uint64_t nb = next(blk, nb_newr, nb_run);
+        PackIn nx;
+        HotLook hl;
+        uint64_t bst_cur = run;
+        if (blk < a.nblocks) {
+            PackIn cur;
+            pack_prefetch(a, blk, lane, cur);
+            hot_issue<true>(a, cur.raw, cur.psym, hl);
+            if (!RNG) bst_cur = cur.bstart;
+            pack_prefetch(a, nb < a.nblocks ? nb : blk, lane, nx);
+        }
+        while (blk < a.nblocks) {
+            bool nn_newr;
+            uint64_t nn_run;
+            const uint64_t nnb = next(nb, nn_newr, nn_run);
+            PackBlk<MODE> b;
+            hot_finish(hl, b.e, b.pe);
+            b.nvalid = kSPT;
+            hot_issue<true>(a, nx.raw, nx.psym, hl);  // block k+1 (past the wave's end: a repeat, unused)
+            const uint64_t nbst = nx.bstart;
+            pack_copyout(a, slot, lane, po);  // block k-1's stores, behind the escape loads
+            po.pending = false;
+            const uint64_t pb = nnb < a.nblocks ? nnb : (nb < a.nblocks ? nb : blk);
+            pack_prefetch(a, pb, lane, nx);
+            pack_block_count<MODE>(lane, b);
+            const uint64_t bst = bst_cur;
+            const uint64_t wfirst = bst >> 5;
+            const uint32_t nwords = (uint32_t)(((bst + b.bits) >> 5) - wfirst), sh4 = (uint32_t)(wfirst & 3);
+            if (blk + 1 == a.nblocks || nwords + sh4 > a.slot_words) {
+                if (lane == 0) {
+                    const unsigned long long i = atomicAdd(a.cold, 1ull);
+                    a.cold[1 + 2 * i] = blk;
+                    a.cold[2 + 2 * i] = bst;
+                }
+            } else {
+                pack_block_emit<MODE, true>(a, slot, blk, lane, b, bst, max_bits, &po);
+            }
+            if (RNG) run = nb_newr ? nb_run : run + b.bits;
+            bst_cur = RNG ? run : nbst;
+            blk = nb;
+            nb = nnb;
+            nb_newr = nn_newr;
+            nb_run = nn_run;
+        }
+        pack_copyout(a, slot, lane, po);
+        if (a.index && lane == 0 && max_bits) atomicMax(a.index + a.nblocks + 1, (unsigned long long)max_bits);
+        return;
+    }
+    PackIn nx;  // the next block's inputs, in flight while this block is packed
+    if (blk < a.nblocks) pack_prefetch(a, blk, lane, nx);
     while (blk < a.nblocks) {
         uint64_t nb = blk + W, nrun = 0;
         bool newr = false;
