@@ -966,18 +966,19 @@ HZ_DEV void pack_block_emit(const PackArgs& a, uint32_t* slot, uint64_t blk, int
 // range plan (after k_range_dot + k_range_scan; wave w packs the blocks of
 // ranges w, w + W, ... in order, each block starting where the one before it
 // ended: a running sum, no count pass).
-template <int MODE, bool RNG>
+template <int MODE, bool RNG, bool SPLIT>
 __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     load_lds_table<MODE>(lds, a.lds_img, a.lds_words);
     const int lane = threadIdx.x & 63;
     // Output slot of this wave: the block's words are assembled in LDS and
     // leave as contiguous 256-byte stores. A block that does not fit, and the
-    // stream's last block, go to k_pack_cold (kSplit: all but WIDE, whose
-    // loop keeps the in-line direct path): without that path in the loop the
+    // stream's last block, go to k_pack_cold (SPLIT: the host's choice when the
+    // workgroup has slots; WIDE, and a DENSE table too large for slots beside
+    // it, keep the in-line direct path): without that path in the loop the
     // kernel needs 70 SGPRs and 152 VGPRs instead of 106 (51 spilled to VGPR
     // lanes, reloaded every block) and 175 (pack 8.6 -> 8.1-8.3 ms, 16 GiB Zipf).
-    constexpr bool kSplit = MODE != ENC_WIDE;
+    constexpr bool kSplit = SPLIT && MODE != ENC_WIDE;
     // (the wave index stays a VGPR value here: as a scalar, 12.4-12.7 vs 11.8-12.2 ms pack stage)
     uint32_t* slot = a.slot_words ? lds + a.lds_words + (threadIdx.x >> 6) * a.slot_words : nullptr;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -991,7 +992,7 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
     }
     PackOut po;
     po.pending = false;
-    if constexpr (MODE == ENC_HOT) {
+    if constexpr (MODE == ENC_HOT && kSplit) {
         // Pipelined: block k is finished (blends) and emitted while block k+1's escape loads and
         // block k+2's input are in flight; the wave's block sequence runs two ahead of the emit.
         // 239 VGPRs (LDS already holds the kernel at 2 waves per SIMD); pack 8.42 -> 8.33 ms mean
@@ -1437,6 +1438,22 @@ uint64_t pack_scratch_words(uint64_t nsym) {
     return 2 * nblocks + ntiles + 1 + 2 * nblocks;  // counts, starts, scan tiles, k_pack_cold's list
 }
 
+// The k_pack_write instance: SPLIT (cold blocks to k_pack_cold) for HOT, and for DENSE when the
+// workgroup has output slots; WIDE and a slot-less DENSE keep the direct path in the loop (split,
+// every block of a slot-less pack would be looked up twice).
+static const void* pack_write_fn(int mode, bool rng, bool split) {
+    if (mode == ENC_HOT) return rng ? (const void*)k_pack_write<ENC_HOT, true, true> : (const void*)k_pack_write<ENC_HOT, false, true>;
+    if (mode == ENC_DENSE) {
+        if (split) return rng ? (const void*)k_pack_write<ENC_DENSE, true, true> : (const void*)k_pack_write<ENC_DENSE, false, true>;
+        return rng ? (const void*)k_pack_write<ENC_DENSE, true, false> : (const void*)k_pack_write<ENC_DENSE, false, false>;
+    }
+    return rng ? (const void*)k_pack_write<ENC_WIDE, true, false> : (const void*)k_pack_write<ENC_WIDE, false, false>;
+}
+static hipError_t pack_write_launch(const void* fn, uint64_t grid, int threads, uint32_t lds, hipStream_t s, PackArgs a) {
+    void* args[] = {&a};
+    return hipLaunchKernel(fn, dim3((uint32_t)grid), dim3(threads), args, lds, s);
+}
+
 // k_pack_write's list of blocks for k_pack_cold: zero the count first, run the cold pass after.
 static hipError_t pack_cold_reset(const PackArgs& a, hipStream_t s) {
     return hipMemsetAsync(a.cold, 0, sizeof(unsigned long long), s);
@@ -1519,7 +1536,8 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     if (wgs > cap) wgs = cap;
     // Range plan (the histogram's snapshots, hz_hist16_ranges): every pack wave takes whole ranges,
     // so the plan is used when the waves cover the ranges evenly; else count + scan + write.
-    const bool split = t.enc_mode != ENC_WIDE;  // k_pack_write leaves its cold blocks to k_pack_cold
+    // k_pack_write leaves its cold blocks to k_pack_cold (HOT always has slots: mean code <= 17 bits)
+    const bool split = t.enc_mode == ENC_HOT || (t.enc_mode == ENC_DENSE && a.slot_words > 0);
     if (split) {
         const void* fc = t.enc_mode == ENC_DENSE ? (const void*)k_pack_cold<ENC_DENSE> : (const void*)k_pack_cold<ENC_HOT>;
         hipError_t e = ensure_lds_limit(fc, kLdsBytes);
@@ -1532,20 +1550,15 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
         if (rw > cap) rw = cap;
         const uint64_t W = rw * waves;
         if (W >= g.nranges || g.nranges % W == 0) {
-            const void* fr[3] = {(const void*)k_pack_write<ENC_DENSE, true>, (const void*)k_pack_write<ENC_HOT, true>,
-                                 (const void*)k_pack_write<ENC_WIDE, true>};
-            hipError_t e = ensure_lds_limit(fr[t.enc_mode], kLdsBytes);
+            const void* fr = pack_write_fn(t.enc_mode, true, split);
+            hipError_t e = ensure_lds_limit(fr, kLdsBytes);
             if (e != hipSuccess) return e;
             const RangeArgs r = range_args(d_ranges, g, d_err);
             uint64_t dg = g.nranges < (uint64_t)ncu * 4 ? g.nranges : (uint64_t)ncu * 4;
             hipLaunchKernelGGL(k_range_dot, dim3(dg), dim3(kDotThreads), 0, s, r, (const uint32_t*)t.d_lenpair);
             hipLaunchKernelGGL(k_range_scan, dim3(1), dim3(kScanThreads), 0, s, r, start_bit);
             a.rstart = r.start; a.bpr = g.bpr; a.nranges = g.nranges; a.blk_start = nullptr;
-            switch (t.enc_mode) {
-                case ENC_DENSE: hipLaunchKernelGGL((k_pack_write<ENC_DENSE, true>), dim3(rw), dim3(threads), lds, s, a); break;
-                case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, true>), dim3(rw), dim3(threads), lds, s, a); break;
-                default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, true>), dim3(rw), dim3(threads), lds, s, a); break;
-            }
+            if ((e = pack_write_launch(fr, rw, threads, lds, s, a)) != hipSuccess) return e;
             if (split) pack_cold_launch(t, a, 4 * table_words, ncu, s);
             if (used_ranges) *used_ranges = 1;
             return hipGetLastError();
@@ -1554,9 +1567,7 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     {
         hipError_t e = ensure_lds_limit((const void*)k_pack_count, kLen8LdsBytes);
         if (e != hipSuccess) return e;
-        const void* fw[3] = {(const void*)k_pack_write<ENC_DENSE, false>, (const void*)k_pack_write<ENC_HOT, false>,
-                             (const void*)k_pack_write<ENC_WIDE, false>};
-        if ((e = ensure_lds_limit(fw[t.enc_mode], kLdsBytes)) != hipSuccess) return e;
+        if ((e = ensure_lds_limit(pack_write_fn(t.enc_mode, false, split), kLdsBytes)) != hipSuccess) return e;
     }
     {
         const uint64_t cw = kCountThreads / 64;
@@ -1569,10 +1580,9 @@ hipError_t launch_pack(const Tables& t, const uint8_t* d_in, uint64_t nsym, uint
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, ntiles, start_bit);
     hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanThreads), 0, s, (const unsigned long long*)a.blk,
                        nblocks, (const unsigned long long*)tiles, blk_start, 0xffffffffull);
-    switch (t.enc_mode) {
-        case ENC_DENSE: hipLaunchKernelGGL((k_pack_write<ENC_DENSE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
-        case ENC_HOT: hipLaunchKernelGGL((k_pack_write<ENC_HOT, false>), dim3(wgs), dim3(threads), lds, s, a); break;
-        default: hipLaunchKernelGGL((k_pack_write<ENC_WIDE, false>), dim3(wgs), dim3(threads), lds, s, a); break;
+    {
+        hipError_t e = pack_write_launch(pack_write_fn(t.enc_mode, false, split), wgs, threads, lds, s, a);
+        if (e != hipSuccess) return e;
     }
     if (split) pack_cold_launch(t, a, 4 * table_words, ncu, s);
     return hipGetLastError();

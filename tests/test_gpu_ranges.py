@@ -206,3 +206,30 @@ def test_range_plan_blocks_over_the_slot_match_oracle(dev):
     assert torch.equal(out[: n - 1], x[: n - 1])
     del x, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [256 * MIB + 6, 8 * MIB + 3])
+def test_dense_without_slots_matches_oracle(built_lib, n):
+    """Symbols uniform over 40 000 values: codes of 15 and 16 bits, a DENSE table (max_len 16) whose
+    mean code (~15.3 bits) leaves no room for output slots beside it, so k_pack_write keeps the
+    direct path in its loop (no cold list); the range plan (256 MiB) and the three-pass encode
+    (8 MiB) both equal the oracle's file and decode back."""
+    import torch
+    from huffman_amd.pipeline import StreamCodec
+    rng = np.random.default_rng(n)
+    sym = rng.integers(0, 40000, n // 2).astype("<u2")
+    host = sym.view(np.uint8)
+    if n % 2:
+        host = np.concatenate([host, np.array([0x5a], np.uint8)])
+    x = torch.from_numpy(host).cuda()
+    c = StreamCodec(0)
+    plan, payload, index = c.encode(x)
+    assert int(plan.cb.max_len) == 16 and int(plan.cb.min_len) < 16  # DENSE, not FIXED16
+    assert c.dev.last_pack_ranges() == (1 if n >= 256 * MIB else 0)
+    assert c.file_image(plan, payload) == oracle_lib.encode(host)
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    c.decode(payload, n // 2, index, out)
+    c.sync()
+    assert torch.equal(out[: n - (n & 1)], x[: n - (n & 1)])
+    del x, out
+    torch.cuda.empty_cache()

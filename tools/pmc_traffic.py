@@ -34,7 +34,8 @@ from collections import defaultdict
 SHARED = ("k_scan_reduce", "k_scan_tiles", "k_scan_apply")
 STAGES = {
     "hist": (("k_hist16", "k_hist16_rng"), ("k_hist16", "k_hist16_rng")),
-    "pack": (("k_pack_count", "k_range_dot", "k_range_scan", "k_pack_write", "k_pack_fixed16", "k_pack_fixed16_blk"),
+    "pack": (("k_pack_count", "k_range_dot", "k_range_scan", "k_pack_write", "k_pack_cold", "k_pack_fixed16",
+              "k_pack_fixed16_blk"),
              ("k_pack_write", "k_pack_fixed16")),
     "decode": (("k_decode", "k_decode_fixed16", "k_decode_fixed16_blk"), ("k_decode", "k_decode_fixed16")),
     "index": (("k_idx_walk", "k_idx_fixed16", "k_sync_scan", "k_sync_scan2", "k_sync_iter", "k_sync_select",
@@ -46,7 +47,8 @@ STAGES = {
 
 
 # kernels whose HBM reads are the calibrated wide shapes (FETCH_SIZE doubled)
-WIDE_READ = ("k_hist16", "k_hist16_rng", "k_range_dot", "k_pack_count", "k_pack_write", "k_pack_one", "k_pack_fixed16",
+WIDE_READ = ("k_hist16", "k_hist16_rng", "k_range_dot", "k_pack_count", "k_pack_write", "k_pack_cold", "k_pack_one",
+             "k_pack_fixed16",
              "k_pack_fixed16_blk", "k_decode", "k_decode_fixed16", "k_decode_fixed16_blk", "k_idx_walk", "k_chain_walk",
              "k_chain_decode")
 
