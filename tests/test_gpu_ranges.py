@@ -233,3 +233,33 @@ def test_dense_without_slots_matches_oracle(built_lib, n):
     assert torch.equal(out[: n - (n & 1)], x[: n - (n & 1)])
     del x, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,rare", [(256 * MIB + 4, 16000), (8 * MIB + 1, 8000)])
+def test_dense_blocks_over_the_slot_match_oracle(built_lib, n, rare):
+    """A DENSE table with output slots (90 % zeros, the rest over 8 000 / 16 000 symbols: codes of 1
+    and 13-15 bits, 768-word slots sized for ~2.3 bits per symbol) and spans of rare symbols only,
+    whose blocks (~900-960 words) exceed a slot: k_pack_cold packs them and the stream's last block.
+    The range plan (256 MiB) and the three-pass encode (8 MiB) equal the oracle's file and decode back."""
+    import torch
+    from huffman_amd.pipeline import StreamCodec
+    rng = np.random.default_rng(n)
+    nsym = n // 2
+    sym = np.where(rng.random(nsym) < 0.9, 0, rng.integers(1, rare + 1, nsym)).astype("<u2")
+    for s0 in (2048 * 3 + 5, nsym // 3, nsym - 2048 * 3 - 7):
+        sym[s0:s0 + 2048 * 2 + 100] = rng.integers(1, rare + 1, 2048 * 2 + 100)
+    host = sym.view(np.uint8)
+    if n % 2:
+        host = np.concatenate([host, np.array([0x21], np.uint8)])
+    x = torch.from_numpy(host).cuda()
+    c = StreamCodec(0)
+    plan, payload, index = c.encode(x)
+    assert int(plan.cb.max_len) <= 16 and int(plan.cb.min_len) < 16  # DENSE
+    assert c.dev.last_pack_ranges() == (1 if n >= 256 * MIB else 0)
+    assert c.file_image(plan, payload) == oracle_lib.encode(host)
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    c.decode(payload, nsym, index, out)
+    c.sync()
+    assert torch.equal(out[: n - (n & 1)], x[: n - (n & 1)])
+    del x, out
+    torch.cuda.empty_cache()
