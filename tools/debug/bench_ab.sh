@@ -9,6 +9,6 @@ for r in $(seq 1 $R); do
       || { [ -s gpurun_out/bab_$v.json ] || { echo "variant $v failed"; tail -5 gpurun_out/bab_$v.err; exit 3; }; }
     python3 -c "
 import json,sys; j=json.loads(open('gpurun_out/bab_$v.json').read().strip().splitlines()[-1])
-print('%-10s %8.3f ms/step %8.2f GB/s  kernels %s  dropin %.3f ms  ok %s' % ('$v', j['ms_per_step'], j['value'], j['kernel_ms'], j['dropin']['ms_per_step'], j['roundtrip_bit_exact']))"
+print('%-10s %8.3f ms/step %8.2f GB/s  kernels %s  dropin %.3f ms (extract %.3f)  ok %s' % ('$v', j['ms_per_step'], j['value'], j['kernel_ms'], j['dropin']['ms_per_step'], j['dropin']['kernel_ms'].get('extract', 0), j['roundtrip_bit_exact']))"
   done
 done
