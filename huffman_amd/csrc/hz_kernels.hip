@@ -1031,7 +1031,11 @@ __global__ __launch_bounds__(kPackWriteThreads) void k_pack_write(PackArgs a) {
             PackBlk<MODE> b;
             hot_finish(hl, b.e, b.pe);
             b.nvalid = kSPT;
+            // issue priority while the lookups and escape loads go out (the SIMD's other wave computes):
+            // pack 8.31-8.33 -> 8.23-8.26 ms, A/B
+            __builtin_amdgcn_s_setprio(2);
             hot_issue<true>(a, nx.raw, nx.psym, hl);  // block k+1 (past the wave's end: a repeat, unused)
+            __builtin_amdgcn_s_setprio(0);
             const uint64_t nbst = nx.bstart;
             pack_copyout(a, slot, lane, po);  // block k-1's stores, behind the escape loads
             po.pending = false;
@@ -2207,10 +2211,13 @@ HZ_DEV void dec_wave_pipe2(const DecArgs& a, const uint32_t* lds, uint32_t* stg,
         };
         // two quads (one per block): a quad's gathers land behind the other quad's walk
         auto issue4 = [&](int c, int q) {
+            // issue priority over the quad's LDS walk and gathers (decode 9.96-9.99 -> 9.88-9.91 ms, A/B)
+            __builtin_amdgcn_s_setprio(2);
             dec_pipe_ldsn<4>(a, lds, p1 + c, st + c, 16u * (uint32_t)q);  // q steps taken: 16 q bytes
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
         };
         issue4(0, 0);
 #pragma unroll
@@ -3984,10 +3991,13 @@ HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, co
             else pk[c / kChainsPerLane][i] = ee;
         };
         auto issue4 = [&](int c, int q) {
+            // issue priority over the quad's LDS walk and gathers (decode 9.96-9.99 -> 9.88-9.91 ms, A/B)
+            __builtin_amdgcn_s_setprio(2);
             dec_pipe_ldsn<4>(a, lds, p1 + c, st + c, 16u * (uint32_t)q);  // q steps taken: 16 q bytes
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 g[c + t] = __builtin_amdgcn_raw_buffer_load_b32(l2r, st[c + t].gi, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
         };
         issue4(0, 0);
 #pragma unroll
