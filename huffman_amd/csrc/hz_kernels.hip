@@ -3670,6 +3670,9 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
             uint32_t q[S];
             uint32_t na = 0, W = 0, e = 0;
             bool ok = false;
+            // issue priority over the dependent steps and the escape gather's issue, normal for the
+            // record select, feed and stores (extract 21.14-21.45 -> 20.48-20.62 ms, A/B)
+            __builtin_amdgcn_s_setprio(2);
 #pragma unroll
             for (int t = 0; t < S; ++t) {
                 ok = m > mlim;
@@ -3685,6 +3688,7 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
             // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
             // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
             const uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
+            __builtin_amdgcn_s_setprio(0);
             // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
             // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
             const uint32_t j1 = 8u - (cc & 7u);
