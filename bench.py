@@ -302,11 +302,85 @@ def main():
         h = hs.sum(axis=0) if world > 1 else hs[0]
         cb = build_codebook(h)
         offset = 0
+        bits = None
         if world > 1:
-            bits = [payload_bits(cb, hs[r]) for r in range(rank)]
-            offset = int(sum(bits))
-        return codec.make_plan(h, n_total, hist_local=hs[rank], first_shard=(rank == 0), shard_bit_offset=offset,
+            bits = [int(payload_bits(cb, hs[r])) for r in range(world)]  # every shard's (the split decode)
+            offset = int(sum(bits[:rank]))
+        plan = codec.make_plan(h, n_total, hist_local=hs[rank], first_shard=(rank == 0), shard_bit_offset=offset,
                                last_byte=0, cb=cb)  # N is even for every shard here
+        plan.all_bits = bits
+        return plan
+
+    # N > 1 drop-in: the `extract` of ONE reference-format stream by every rank (SURVEY.md 8e decode):
+    # the global payload (every shard at its global bit offset) is split into equal bit parts
+    # (dist.part_range), not at the shards' encode start bits -- a .compressed file carries none. Each
+    # rank's part window (the part, its 1024-bit lead-in, max_len bits after) lies in its own shard's
+    # buffer plus a halo: the neighbours' words inside it travel point-to-point (dist.fill_window), and
+    # the part is decoded through hz_indexless_scan / _refix / _decode with the ranks' exchange
+    # (dist.decode_indexless_split).
+    from huffman_amd import dist as hd
+    HALO = 1 << 22  # words on each side of the shard (16 MiB): equal bit parts lie this close to the shards
+    split = {}
+
+    def split_geometry(plan):
+        S0 = plan.header_bits % 8
+        offs = [int(sum(plan.all_bits[:g])) for g in range(world)]
+        shards = []
+        for g in range(world):
+            w0, _, words = hd.local_geometry(plan.header_bits, offs[g], plan.all_bits[g], g == 0)
+            shards.append((w0, words))
+        P = int(sum(plan.all_bits))
+        parts = [hd.part_range(P, world, r) for r in range(world)]
+        windows = [hd.part_window(S0, pb, pe, int(plan.cb.max_len)) for pb, pe in parts]
+        return S0, shards, parts, windows
+
+    def split_alloc(plan):
+        need = 4 * (2 * HALO + plan.words + 4)
+        if "ext" not in split or split["ext"].numel() < need:
+            split.pop("ext", None)
+            split["ext"] = torch.zeros(need, dtype=torch.uint8, device=dev)
+        ext = split["ext"]
+        return ext, ext[4 * HALO:4 * (HALO + plan.words) + 16]
+
+    def split_decode(plan, ext):
+        """The part of this rank, decoded into split['out']; returns (first symbol, symbols taken)."""
+        S0, shards, parts, windows = split_geometry(plan)
+        w0, words = shards[rank]
+        ext_word0 = w0 - HALO
+        lo, hi = windows[rank]
+        if not (ext_word0 <= lo and hi <= ext_word0 + ext.numel() // 4):
+            raise RuntimeError(f"rank {rank}: part window {lo}..{hi} beyond the shard's halo")
+        ext[:4 * HALO].zero_()
+        ext[4 * (HALO + words):].zero_()
+        hd.fill_window(ext, ext_word0, w0, words, windows, shards, via_host=args.rehearse)
+        sl = ext[4 * (lo - ext_word0):4 * (hi - ext_word0)]
+        pb, pe = parts[rank]
+        summ = split["summ"]
+        nsym_all = n_total // 2
+
+        def read():
+            codec.sync()
+            v = [int(t) & ((1 << 64) - 1) for t in summ[:3].cpu().tolist()]
+            return v[0], v[1], v[2]
+
+        def scan():
+            codec.dev.indexless_scan(sl.data_ptr(), sl.numel(), S0, pb, pe,
+                                     S0 if rank == 0 else hd.UNKNOWN_ENTRY, summ.data_ptr(), nsym=nsym_all,
+                                     payload_bit_base=32 * lo)
+            return read()
+
+        def refix(entry):
+            codec.dev.indexless_refix(entry, summ.data_ptr())
+            return read()
+
+        def decode(first, take):
+            if take > split["cap"]:
+                raise RuntimeError(f"rank {rank}: part of {take} symbols over the output buffer")
+            codec.dev.indexless_decode(take, split["out"].data_ptr(), endb.data_ptr())
+
+        grp_dev = torch.device("cpu") if args.rehearse else dev
+        first, count, _ = hd.decode_indexless_split(scan, refix, decode, nsym_all, grp_dev, empty=pb == pe)
+        return first, max(0, min(count, nsym_all - first))
 
     def run(steps, dropin=False):
         """dropin=False: pack writes its block index beside the payload and decode reads it (the
@@ -319,11 +393,18 @@ def main():
             if "payload" not in state or state["payload"].numel() < plan.words * 4 + 16:
                 state["payload"], state["index"] = codec.alloc_payload(plan, nsym)
             side = sidecar(plan, dropin)
-            codec.pack(x, plan, state["payload"], state["index"] if side else None)
+            splitting = dropin and world > 1
+            if splitting:  # the shard packed into its place in the part-window buffer
+                ext, pay = split_alloc(plan)
+                codec.pack(x, plan, pay, None)
+            else:
+                codec.pack(x, plan, state["payload"], state["index"] if side else None)
             if i + 1 < steps:
                 hist_launch()  # the next batch's histogram, between this batch's pack and decode
             codec.upload_decode(plan)  # host builds the decode tables while pack runs
-            if not side:
+            if splitting:
+                split["last"] = split_decode(plan, ext)
+            elif not side:
                 codec.dev.decode_indexless(state["payload"].data_ptr(), state["payload"].numel(), plan.start_bit,
                                            nsym, out.data_ptr(), endb.data_ptr())
             else:
@@ -345,6 +426,10 @@ def main():
         return time.perf_counter() - t0
 
     endb = torch.zeros(2, dtype=torch.int64, device=dev)
+    if world > 1:
+        split["summ"] = torch.zeros(4, dtype=torch.int64, device=dev)
+        split["cap"] = nsym + 32 * HALO  # a part's symbols: its shard's give or take the halo's bits
+        split["out"] = torch.empty(2 * split["cap"] + 16, dtype=torch.uint8, device=dev)
 
     log(f"rank {rank}: {N} bytes generated; {args.warmup} warmup steps")
     if args.warmup:
@@ -362,7 +447,18 @@ def main():
     codec.sync()
     elapsed_dropin = timed(args.steps, dropin=True)
     codec.sync()
-    ok_dropin = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    if world > 1:
+        # this rank's part of the one stream: its symbols from the generator at their global offset
+        first, take = split["last"]
+        ref = torch.empty(2 * take + 16, dtype=torch.uint8, device=dev)
+        if take:
+            codec.dev.generate(ref.data_ptr(), 2 * take, offset=2 * first, kind=kind, alpha=1.1, seed=42)
+        codec.sync()
+        ok_dropin = bool(torch.equal(split["out"][:2 * take], ref[:2 * take]))
+        split["checked"] = {"first_symbol": first, "symbols": take, "bit_exact": ok_dropin}
+        del ref
+    else:
+        ok_dropin = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
     ok = ok and ok_dropin
     # Kernel times (HIP events) and host stage costs: two more steps, serialised, untimed.
     kms = {"hist": [], "pack": [], "decode": []}
@@ -509,6 +605,15 @@ def main():
                 "value": round(n_total / (ms_dropin / 1e3) / 1e9, 2),
                 "unit": "GB/s",
                 "roundtrip_bit_exact": ok_dropin,
+                # N > 1: the timed decode is ONE stream's extract split over the ranks at equal bit parts
+                # (not at the shards' encode start bits, which a .compressed file does not carry)
+                "decode": ("index-less extract of the one global stream, split over the ranks at equal payload "
+                           "bit parts: halo words point-to-point (dist.fill_window), hz_indexless_scan/refix/decode "
+                           "with the ranks' exchange (dist.decode_indexless_split)") if world > 1
+                          else "hz_decode_indexless of the whole payload",
+                "split_check_rank0": split.get("checked") if world > 1 else None,
+                "transport": ("gloo via host (one-GPU rehearsal)" if args.rehearse else "RCCL") if world > 1 else None,
+                # kernel_ms: serialised per-rank steps; N > 1 they decode each rank's own shard
                 "kernel_ms": {k: round(float(np.mean(v)), 4) for k, v in dk.items()},
                 "roofline": {
                     "kernel": "extract",

@@ -98,7 +98,7 @@ PROTOTYPES = [
     ("hz_decode", _I, [_P, _P, _U64, _U64, _P, _P]),
     ("hz_index_build", _I, [_P, _P, _U64, _U64, _U64, _P]),
     ("hz_decode_indexless", _I, [_P, _P, _U64, _U64, _U64, _P, _P]),
-    ("hz_indexless_scan", _I, [_P, _P, _U64, _U64, _U64, _U64, _U64, _P]),
+    ("hz_indexless_scan", _I, [_P, _P, _U64, _U64, _U64, _U64, _U64, _U64, _U64, _P]),
     ("hz_indexless_refix", _I, [_P, _U64, _P]),
     ("hz_indexless_decode", _I, [_P, _U64, _P, _P]),
     ("hz_last_kernel_ms", _I, [_P, _I, ctypes.POINTER(ctypes.c_float)]),

@@ -228,11 +228,14 @@ class Device:
               "hz_decode_indexless")
 
     # -- one index-less stream in parts (one per rank; huffman_amd/dist.py decode_indexless_split) -----
-    def indexless_scan(self, d_payload, payload_bytes, start_bit, part_begin, part_end, entry_bit, d_summary):
+    def indexless_scan(self, d_payload, payload_bytes, start_bit, part_begin, part_end, entry_bit, d_summary,
+                       nsym=0, payload_bit_base=0):
         """Walk + fix-ups of payload bits [part_begin, part_end) after start_bit; entry_bit: the part's true
-        entry or 2**64 - 1 (its walked entry). d_summary (device, 3 x u64): codewords, true exit, walked entry."""
-        check(self.lib.hz_indexless_scan(self.h, d_payload, payload_bytes, start_bit, part_begin, part_end,
-                                         entry_bit, d_summary), "hz_indexless_scan")
+        entry or 2**64 - 1 (its walked entry). d_summary (device, 3 x u64): codewords, true exit, entry in
+        use. Stream bits throughout; d_payload holds stream bits from payload_bit_base (a rank's slice:
+        the part plus HZ_INDEXLESS_LEAD_BITS before it). nsym: the stream's symbols (0: unknown)."""
+        check(self.lib.hz_indexless_scan(self.h, d_payload, payload_bytes, payload_bit_base, start_bit, nsym,
+                                         part_begin, part_end, entry_bit, d_summary), "hz_indexless_scan")
 
     def indexless_refix(self, entry_bit, d_summary):
         check(self.lib.hz_indexless_refix(self.h, entry_bit, d_summary), "hz_indexless_refix")

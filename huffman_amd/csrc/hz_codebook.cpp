@@ -673,3 +673,32 @@ void build_walk8(const hz_codebook* cb, std::vector<uint32_t>& img, int& K) {
     memcpy(img.data(), t.data(), t.size());
 }
 }  // namespace hz
+
+// The chain walker's escape table for codebooks whose codes exceed kWalkMaxLen bits (build_walk_len's
+// 2^max_len table would not fit): one byte per M = kChainEscMaxBits window, the length of every code
+// longer than 16 bits (the byte table's escapes) that is at most M bits, or shared by every code under
+// the window when they are longer; 0 (a DEEP escape, resolved through the decode LUT) for M-bit
+// prefixes of codes of different lengths. Windows no code starts read 1.
+namespace hz {
+void build_chain_esc(const hz_codebook* cb, std::vector<uint32_t>& img, int& M) {
+    M = std::min((int)cb->max_len, kChainEscMaxBits);
+    std::vector<uint8_t> t((size_t)1 << M, (uint8_t)1);
+    std::vector<uint8_t> plen((size_t)1 << M, 0);
+    for (uint32_t s = 0; s < HZ_NSYM; ++s) {
+        const int L = cb->len[s];
+        if (L <= 16) continue;
+        const uint64_t c = cb->code[s];
+        if (L <= M) {
+            memset(t.data() + (c << (M - L)), L, (size_t)1 << (M - L));
+        } else {
+            uint8_t& pl = plen[c >> (L - M)];
+            pl = pl == 0 || pl == (uint8_t)L ? (uint8_t)L : (uint8_t)255;
+        }
+    }
+    for (size_t p = 0; p < plen.size(); ++p)
+        if (plen[p]) t[p] = plen[p] != 255 ? plen[p] : 0;
+    while (t.size() % 16) t.push_back(1);
+    img.assign(t.size() / 4, 0);
+    memcpy(img.data(), t.data(), t.size());
+}
+}  // namespace hz

@@ -40,6 +40,7 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
 void build_walk_len(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector<uint32_t>& esc, int& K, int& M,
                     int& bias);
 void build_walk8(const hz_codebook* cb, std::vector<uint32_t>& img, int& K);
+void build_chain_esc(const hz_codebook* cb, std::vector<uint32_t>& img, int& M);
 }  // namespace hz
 
 using namespace hz;
@@ -92,8 +93,15 @@ struct hz_ctx {
     uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
-           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_walk8 = 0;
+           cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_walk8 = 0, cap_chain_lds = 0, cap_chain_l2 = 0,
+           cap_chain_esc = 0;
     int last_pack_ranges = 0;       // the last hz_pack_ranges call took the range plan
+    // a FIXED16 part of hz_indexless_scan (every code 16 bits: positions are arithmetic, no chains)
+    struct {
+        bool on = false;
+        const uint8_t* payload = nullptr;
+        uint64_t bytes = 0, base = 0, start = 0, entry = 0, xit = 0;
+    } fx;
 };
 
 extern "C" const char* hz_strerror(int st) {
@@ -126,6 +134,9 @@ static void free_tables(Tables& t) {
     (void)hipFree(t.d_walk_lds);
     (void)hipFree(t.d_walk_esc);
     (void)hipFree(t.d_walk8);
+    (void)hipFree(t.d_chain_lds);
+    (void)hipFree(t.d_chain_l2);
+    (void)hipFree(t.d_chain_esc);
     t = Tables();
 }
 
@@ -388,6 +399,8 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     HZ_TRY(hipSetDevice(c->device));
     Tables& t = c->t;
     t.dec_mode = -1;
+    chain_invalidate(c->chain);  // its arguments point at the tables replaced here
+    c->fx.on = false;
     if (cb->nsym == 0) return HZ_OK;
     int rc;
     if ((rc = staging_begin(c->stage_dec))) return rc;
@@ -412,6 +425,8 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
     // the index walker's length tables (FIXED16 streams have an arithmetic index)
     t.walk_lds_bytes = 0;
+    t.walk8_bytes = 0;
+    t.chain_lds_bytes = 0;
     if (mode != DEC_FIXED16 && cb->max_len >= 1 && cb->max_len <= kWalkMaxLen) {
         build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m, t.walk_bias);
         if (wimg.size() * 4 <= (1u << kWalkK) / 2) {  // k_idx_walk's static table
@@ -419,10 +434,40 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
             if (wesc.empty()) wesc.push_back(0x01010101u);
             if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;
             t.walk_lds_bytes = (uint32_t)(wimg.size() * 4);
-            std::vector<uint32_t> w8;
-            build_walk8(cb, w8, t.walk8_k);
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk8, &c->cap_walk8, w8))) return rc;
-            t.walk8_bytes = (uint32_t)(w8.size() * 4);
+        }
+    }
+    // the index-less chain decoder's tables (every codebook but FIXED16): the byte length table, the
+    // escape table (the index walker's when it has one: codes <= kWalkMaxLen bits), LUT decode images
+    if (mode != DEC_FIXED16 && cb->max_len >= 1) {
+        std::vector<uint32_t> w8;
+        build_walk8(cb, w8, t.walk8_k);
+        if ((rc = stage_copy(c, c->stage_dec, &t.d_walk8, &c->cap_walk8, w8))) return rc;
+        t.walk8_bytes = (uint32_t)(w8.size() * 4);
+        if (t.walk_lds_bytes > 0) {
+            t.chain_esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc);
+            t.chain_esc_m = t.walk_m;
+        } else {
+            std::vector<uint32_t> cesc;
+            build_chain_esc(cb, cesc, t.chain_esc_m);
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_esc, &c->cap_chain_esc, cesc))) return rc;
+            t.chain_esc = reinterpret_cast<const uint8_t*>(t.d_chain_esc);
+        }
+        if (mode == DEC_LUT) {
+            t.chain_lds = t.d_dec_lds;
+            t.chain_l2 = t.d_dec_l2;
+            t.chain_lds_bytes = t.dec_lds_bytes;
+            t.chain_k = t.dec_k;
+            t.chain_level_bits = t.dec_level_bits;
+        } else {  // DENSE: a LUT image beside the DENSE decoder's
+            std::vector<uint32_t> cimg, cl2;
+            if ((rc = build_dec_lut(cb, cimg, cl2, t.chain_k, t.chain_level_bits))) return rc;
+            while (cimg.size() % 4) cimg.push_back(0);
+            if (cl2.empty()) cl2.push_back(lut_leaf_entry(1, 0));
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_lds, &c->cap_chain_lds, cimg))) return rc;
+            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_l2, &c->cap_chain_l2, cl2))) return rc;
+            t.chain_lds = t.d_chain_lds;
+            t.chain_l2 = t.d_chain_l2;
+            t.chain_lds_bytes = (uint32_t)(cimg.size() * 4);
         }
     }
     HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
@@ -444,7 +489,11 @@ extern "C" uint64_t hz_index_stride(void) { return kBlockSyms; }
 extern "C" uint64_t hz_index_bytes(uint64_t nsym) { return index_bytes(nsym); }
 extern "C" uint64_t hz_scratch_bytes(uint64_t nsym) { return pack_scratch_words(nsym) * sizeof(uint64_t); }
 
+// Every call that writes the context's scratch (or reallocates it, or replaces the decode tables) ends
+// a pending index-less part (hz_indexless_scan ... hz_indexless_decode): its chain state points there.
 static int ensure_scratch(hz_ctx* c, uint64_t words) {
+    chain_invalidate(c->chain);
+    c->fx.on = false;
     if (c->desc_cap >= words) return HZ_OK;
     HZ_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(c->d_desc);
@@ -595,10 +644,11 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
     int rc = ensure_scratch(c, chain_scratch_words(0, pbits, nsym, c->t, c->ncu));
     if (rc) return rc;
     HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
-    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, start_bit, nsym, 0, pbits, ~0ull, c->d_desc, c->d_err,
-                      c->ncu, c->stream));
+    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, 0, start_bit, nsym, 0, pbits, ~0ull, c->d_desc,
+                      c->d_err, c->ncu, c->stream));
     HZ_TRY(chain_decode(c->chain, c->t, nsym, d_out, reinterpret_cast<unsigned long long*>(d_end_bit), c->ncu,
                         c->stream));
+    chain_invalidate(c->chain);  // not a part: hz_indexless_refix / _decode may not continue it
     HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
     c->ev_used[HZ_STAGE_EXTRACT] = true;
     return arm_err_check(c);
@@ -607,27 +657,64 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
 // ---- one stream over several devices: the index-less decode in parts -----------------
 static int part_summary(hz_ctx* c, uint64_t* d_summary) {
     if (!d_summary) return HZ_OK;
-    const unsigned long long* info = chain_info(c->chain);
-    if (!info) return HZ_EINVAL;
-    HZ_TRY(hipMemcpyAsync(d_summary, info + 3, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
+    if (!chain_info(c->chain)) return HZ_EINVAL;
+    HZ_TRY(chain_summary(c->chain, reinterpret_cast<unsigned long long*>(d_summary), c->stream));
     return HZ_OK;
 }
 
-extern "C" int hz_indexless_scan(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
-                                 uint64_t part_begin, uint64_t part_end, uint64_t entry_bit, uint64_t* d_summary) {
-    if (!c || !d_payload || part_end <= part_begin) return HZ_EINVAL;
-    if (c->t.dec_mode < 0 || !seg_decode_supported(c->t)) return HZ_EINVAL;
-    if (start_bit + part_end > payload_bytes * 8) return HZ_EINVAL;
+// FIXED16 parts: codeword i starts at start + 16 i, so a part's entry, exit and count are arithmetic.
+static int fixed_part_summary(hz_ctx* c, uint64_t* d_summary) {
+    if (!d_summary) return HZ_OK;
+    HZ_TRY(put3(reinterpret_cast<unsigned long long*>(d_summary), (c->fx.xit - c->fx.entry) / 16, c->fx.xit,
+                c->fx.entry, c->stream));
+    return HZ_OK;
+}
+
+extern "C" int hz_indexless_scan(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t payload_bit_base,
+                                 uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end,
+                                 uint64_t entry_bit, uint64_t* d_summary) {
+    if (!c || !d_payload || part_end <= part_begin || payload_bytes < 16) return HZ_EINVAL;
+    if (c->t.dec_mode < 0) return HZ_EINVAL;
+    if (start_bit > UINT64_MAX - part_end || payload_bytes > (UINT64_MAX - payload_bit_base) / 8) return HZ_EINVAL;
+    // the view must hold the part, and the lead-in before it (the stream's bits from its start, when the
+    // part begins less than HZ_INDEXLESS_LEAD_BITS into it)
+    const uint64_t lead = part_begin < HZ_INDEXLESS_LEAD_BITS ? part_begin : HZ_INDEXLESS_LEAD_BITS;
+    if (start_bit + part_begin - lead < payload_bit_base) return HZ_EINVAL;
+    if (start_bit + part_end > payload_bit_base + payload_bytes * 8) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
-    int rc = ensure_scratch(c, chain_scratch_words(part_begin, part_end, 0, c->t, c->ncu));
+    chain_invalidate(c->chain);
+    c->fx.on = false;
+    if (c->t.dec_mode == DEC_FIXED16) {
+        c->fx.payload = d_payload;
+        c->fx.bytes = payload_bytes;
+        c->fx.base = payload_bit_base;
+        c->fx.start = start_bit;
+        c->fx.entry = entry_bit != UINT64_MAX ? entry_bit : start_bit + 16 * ((part_begin + 15) / 16);
+        c->fx.xit = start_bit + 16 * ((part_end + 15) / 16);
+        if (c->fx.entry < start_bit || (c->fx.entry - start_bit) % 16 || c->fx.entry > c->fx.xit) return HZ_EINVAL;
+        c->fx.on = true;
+        return fixed_part_summary(c, d_summary);
+    }
+    if (!seg_decode_supported(c->t)) return HZ_EINVAL;
+    // record capacity from the stream's own bits per codeword when the caller knows its symbols
+    const uint64_t pbits = payload_bit_base + payload_bytes * 8 > start_bit ? payload_bit_base + payload_bytes * 8 - start_bit : 0;
+    const uint64_t hint = nsym ? std::max<uint64_t>(1, (uint64_t)((double)nsym * (double)(part_end - part_begin) /
+                                                                  (double)std::max<uint64_t>(pbits, 1))) : 0;
+    int rc = ensure_scratch(c, chain_scratch_words(part_begin, part_end, hint, c->t, c->ncu));
     if (rc) return rc;
-    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, start_bit, 0, part_begin, part_end, entry_bit,
-                      c->d_desc, c->d_err, c->ncu, c->stream));
+    HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, payload_bit_base, start_bit, hint, part_begin, part_end,
+                      entry_bit, c->d_desc, c->d_err, c->ncu, c->stream));
     if ((rc = part_summary(c, d_summary))) return rc;
     return arm_err_check(c);
 }
 
 extern "C" int hz_indexless_refix(hz_ctx* c, uint64_t entry_bit, uint64_t* d_summary) {
+    if (c && c->fx.on) {
+        if (entry_bit < c->fx.start || (entry_bit - c->fx.start) % 16 || entry_bit > c->fx.xit) return HZ_EINVAL;
+        HZ_TRY(hipSetDevice(c->device));
+        c->fx.entry = entry_bit;
+        return fixed_part_summary(c, d_summary);
+    }
     if (!c || !chain_info(c->chain)) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));
     HZ_TRY(chain_refix(c->chain, c->t, entry_bit, c->ncu, c->stream));
@@ -637,6 +724,22 @@ extern "C" int hz_indexless_refix(hz_ctx* c, uint64_t entry_bit, uint64_t* d_sum
 }
 
 extern "C" int hz_indexless_decode(hz_ctx* c, uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
+    if (c && c->fx.on) {
+        if (nsym && (!d_out || (((uintptr_t)d_out) & 15))) return HZ_EINVAL;
+        HZ_TRY(hipSetDevice(c->device));
+        const uint64_t count = (c->fx.xit - c->fx.entry) / 16;
+        const uint64_t take = nsym < count ? nsym : count;
+        if (take)
+            HZ_TRY(launch_decode(c->t, c->fx.payload, c->fx.bytes, take, nullptr, d_out, c->d_err, c->ncu, c->stream,
+                                 c->fx.entry - c->fx.base));
+        if (d_end_bit) {
+            const uint64_t eb = nsym && nsym <= count ? c->fx.entry + 16 * nsym : UINT64_MAX;
+            HZ_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_end_bit), (int)(uint32_t)eb, 1, c->stream));
+            HZ_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(reinterpret_cast<uint32_t*>(d_end_bit) + 1),
+                                     (int)(uint32_t)(eb >> 32), 1, c->stream));
+        }
+        return arm_err_check(c);
+    }
     if (!c || !chain_info(c->chain)) return HZ_EINVAL;
     if (nsym && (!d_out || (((uintptr_t)d_out) & 15))) return HZ_EINVAL;
     HZ_TRY(hipSetDevice(c->device));

@@ -191,7 +191,22 @@ struct Tables {
     uint32_t* d_walk8 = nullptr;    // chain walker: u8 code length per walk8_k-bit window (0 = escape to d_walk_esc)
     uint32_t walk8_bytes = 0;
     int walk8_k = 0;
+    // The index-less chain decoder's tables (hz_decode_indexless, hz_indexless_*): LUT-format decode
+    // images (DEC_LUT codebooks: the decode tables themselves; DEC_DENSE: a LUT built beside them) and
+    // the walker's escape table of u8 lengths per chain_esc_m-bit window (chain_esc_m = min(max_len,
+    // kWalkMaxLen); 0 = a DEEP escape for codes longer than that, resolved through the LUT).
+    const uint32_t* chain_lds = nullptr;  // level 1 (+ hot heads) LDS image
+    const uint32_t* chain_l2 = nullptr;   // global levels
+    uint32_t chain_lds_bytes = 0;         // 0: no chain tables (FIXED16: positions are arithmetic)
+    int chain_k = 0, chain_level_bits = 0;
+    const uint8_t* chain_esc = nullptr;
+    int chain_esc_m = 0;
+    uint32_t* d_chain_lds = nullptr;      // owned images behind chain_* when they are not the decode tables'
+    uint32_t* d_chain_l2 = nullptr;
+    uint32_t* d_chain_esc = nullptr;
 };
+// Walker escape table resolution (kWalkMaxLen bits at most: a 32 MiB table).
+constexpr int kChainEscMaxBits = kWalkMaxLen;
 
 // Count-pass length table layout: the high byte is XORed into the bank bits
 // so skewed symbol sets (small high and low bytes) spread over LDS banks.
@@ -238,13 +253,18 @@ ChainState* chain_state_create();
 void chain_state_destroy(ChainState* st);
 bool seg_decode_supported(const Tables& t);
 uint64_t chain_scratch_words(uint64_t part_begin, uint64_t part_end, uint64_t nsym, const Tables& t, int ncu);
+// base: stream bit of byte 0 of d_payload (0: the buffer starts with the stream); every bit argument
+// and result is a stream bit
 hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                      uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end, uint64_t entry0,
-                      unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
+                      uint64_t base, uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end,
+                      uint64_t entry0, unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s);
 hipError_t chain_refix(ChainState* st, const Tables& t, uint64_t entry0, int ncu, hipStream_t s);
 hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
                         int ncu, hipStream_t s);
 const unsigned long long* chain_info(const ChainState* st);
+void chain_invalidate(ChainState* st);  // the scratch or tables it points into changed
+hipError_t chain_summary(const ChainState* st, unsigned long long* d_dst, hipStream_t s);  // 3 x u64, stream bits
+hipError_t put3(unsigned long long* d_dst, uint64_t a, uint64_t b, uint64_t c, hipStream_t s);  // stream-ordered
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -2791,6 +2791,9 @@ struct WalkArgs {
     const uint32_t* w8_img;   // k_chain_walk: u8 code length per k8-bit window (0: escape)
     uint32_t w8_words;
     int k8;
+    const uint32_t* lut1;     // k_chain_walk<DEEP>: the decode LUT (level-1 image, global levels) that
+    const uint32_t* lut2;     // resolves escapes the m-bit escape table leaves at 0 (codes > m bits)
+    int lutk;
 };
 
 // 16 payload bytes at word w (4-aligned): zeros before word 0 / past the end.
@@ -3604,6 +3607,102 @@ HZ_DEV void seg_feed(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint32_t p)
 constexpr int kSegSteps = 14;
 static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
 
+// The chain walk's ring in two SLOTS of 256 bits (ring words 8 s .. 8 s + 7, rows 15 - 8 s - j, row 16
+// the copy of word 15): a round takes up to 14 codewords (~162 bits of Zipf), more than one 128-bit
+// chunk, so a ring fed one chunk per round starves (~21 % of the steps of a 16 GiB Zipf walk idle at the
+// fill limit); one 256-bit slot per round keeps ahead, from the same 64-byte register group (two slots:
+// a 2-way pick, 8 selects per 256 bits instead of 12 per 128).
+constexpr uint32_t kSlotBits = 256;
+struct SlotFeed {
+    uint4 pre[4];   // payload slots 2 g and 2 g + 1 (one 64-byte group)
+    bool gin;       // the group lies inside the payload (no zero fill)
+    uint64_t bsl;   // payload slot of ring slot 0 of the first lap
+    uint32_t f;     // next slot to put (slots below f are in the ring)
+};
+
+HZ_DEV void slot_put(uint32_t* ring, uint32_t s, const uint4& x0, const uint4& x1) {
+    const uint32_t v[8] = {bswap32(x0.x), bswap32(x0.y), bswap32(x0.z), bswap32(x0.w),
+                           bswap32(x1.x), bswap32(x1.y), bswap32(x1.z), bswap32(x1.w)};
+    uint32_t* base = ring + (8u - 8u * s) * kRingRow;  // row 8 (1 - s): word 7 of the slot
+#pragma unroll
+    for (int j = 0; j < 8; ++j) base[(7 - j) * kRingRow] = v[j];
+    if (s) ring[16 * kRingRow] = v[7];
+}
+
+// Slots 0 and 1 of a ring whose bit 0 is payload word 8 * bsl, and the group holding slot 2.
+HZ_DEV void slot_feed_init(const WalkArgs& a, uint32_t* ring, SlotFeed& fd, uint64_t bsl) {
+    fd.bsl = bsl;
+    uint4 v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = walk_load(a, 8 * bsl + 4 * g);
+    const uint64_t gq = (bsl + 2) & ~1ull;
+    fd.gin = 8 * gq + 16 <= a.nwords;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) fd.pre[g] = walk_load(a, 8 * gq + 4 * g);
+    if ((bsl + 2) & 1) {
+        fd.pre[0] = fd.pre[2];
+        fd.pre[1] = fd.pre[3];
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = walk_fix(a, 8 * bsl + 4 * g, v[g]);
+    slot_put(ring, 0, v[0], v[1]);
+    slot_put(ring, 1, v[2], v[3]);
+    fd.f = 2;
+}
+
+// Once per round: slot f goes into the ring when the walk at p no longer reads slot f - 2 (the window
+// reads words floor(p / 32) and up); the next group is loaded once the current one is in the ring.
+HZ_DEV void slot_feed(const WalkArgs& a, uint32_t* ring, SlotFeed& fd, uint32_t p) {
+    // pre[0..1] always holds slot f (the group's second slot moves down after the first is put: no
+    // select between slots, whose loads the compiler would fold into a dynamically indexed array)
+    if (fd.f <= (p >> 8) + 1) {
+        const uint64_t q = fd.bsl + fd.f;
+        uint4 x0 = fd.pre[0], x1 = fd.pre[1];
+        if (!fd.gin) {
+            x0 = walk_fix(a, 8 * q, x0);
+            x1 = walk_fix(a, 8 * q + 4, x1);
+        }
+        slot_put(ring, fd.f & 1, x0, x1);
+        ++fd.f;
+        if (q & 1) {  // the group is in the ring: the next one
+            const uint64_t w = 8 * (q + 1);
+            fd.gin = w + 16 <= a.nwords;
+            if (fd.gin) {
+                const uint4* src = reinterpret_cast<const uint4*>(a.words + w);
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) fd.pre[i] = src[i];
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) fd.pre[i] = walk_load(a, w + 4 * i);
+            }
+        } else {
+            fd.pre[0] = fd.pre[2];
+            fd.pre[1] = fd.pre[3];
+        }
+    }
+}
+
+// Length of the code at view bit P through the decode LUT in global memory (k_chain_walk<DEEP>: codes
+// longer than the escape table's m bits; rare, never on the path of codebooks within m bits).
+HZ_DEV uint32_t deep_len(const WalkArgs& a, uint64_t P) {
+    const uint64_t w = P >> 5;
+    const uint32_t sh = (uint32_t)(P & 31);
+    const uint32_t w0 = w < a.nwords ? bswap32(a.words[w]) : 0u;
+    const uint32_t w1 = w + 1 < a.nwords ? bswap32(a.words[w + 1]) : 0u;
+    const uint32_t w2 = w + 2 < a.nwords ? bswap32(a.words[w + 2]) : 0u;
+    const uint64_t win = ((((uint64_t)w0 << 32) | w1) << sh) | (sh ? ((uint64_t)w2 << sh) >> 32 : 0ull);
+    uint32_t e = a.lut1[(uint32_t)(win >> (64 - a.lutk))];
+    uint32_t D = (uint32_t)a.lutk;
+    while (!(e >> 31)) {
+        const uint32_t nb = (e >> 5) & 15u;
+        const uint32_t idx = (e >> 10) + (uint32_t)((win << D) >> (64 - nb));
+        e = idx < kLutGlobal ? a.lut1[idx] : a.lut2[idx - kLutGlobal];
+        D += nb;
+    }
+    return lut_leaf_len(e);
+}
+
+template <bool DEEP>
 __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a, ChainArgs y) {
     // the byte length table (build_walk8: 2^16 windows at most, 64 KiB) at LDS address 0, the rings and
     // record buffers after it
@@ -3623,9 +3722,9 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     const uint64_t ce = cs + y.cbits < y.pend ? cs + y.cbits : y.pend;
     const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
     const uint64_t P0 = y.start + a.bit_adj + x0;
-    SegFeed fd;
-    seg_feed_init(a, ring, fd, (P0 >> 7) - 1);  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
-    uint32_t p = (uint32_t)(P0 - 128 * fd.bch);    // ring bit position of the walk (>= 128)
+    SlotFeed fd;
+    slot_feed_init(a, ring, fd, P0 / kSlotBits);
+    uint32_t p = (uint32_t)(P0 - kSlotBits * fd.bsl);  // ring bit position of the walk (< 256)
     const uint64_t abs0 = y.start + x0 - p;        // absolute stream bit of ring position q: abs0 + q
     const uint32_t end = live ? p + (uint32_t)(ce - x0) : p;
     const uint32_t csr = p + (uint32_t)(cs - x0);  // the chain's first bit
@@ -3638,14 +3737,13 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     // nothing is stored (k_chain_tail decodes those codewords).
     // (the buffer write needs no capacity test: rows past the capacity are never stored)
     auto rec_put = [&](uint32_t rp) {
-        const uint64_t ab = abs0 + rp;
-        rbuf[rj & 7] = (uint16_t)ab;
+        rbuf[rj & 7] = (uint16_t)((uint32_t)abs0 + rp);
         const bool in = rj < y.cap;
         const bool row = in & ((rj & 7) == 7);
         const bool ck = (in & ((rj & (kChainRecs - 1)) == 0)) | (rj == y.cap);  // at the capacity: the first codeword past it
         if (row | ck) {  // one branch for both rare stores
             if (row) *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
-            if (ck) ckp[in ? rj / kChainRecs : y.bpc] = ab;
+            if (ck) ckp[in ? rj / kChainRecs : y.bpc] = abs0 + rp;
         }
         ++rj;
     };
@@ -3654,68 +3752,97 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     if (on && p < end) rec_put(p);
     uint32_t m = kRingM0 - p;  // the walk's position, descending (seg_window)
     const uint32_t mend = kRingM0 - end;
-    for (;;) {
-        if (!__any(m > mend)) break;
-        const uint32_t fill = 128 * fd.f - 96;  // filled data: both window words lie below p + 64
+    const uint32_t ml = (uint32_t)a.m;  // longest code: the most one step moves
+    // One half-round. FAST: every lane of the wave is at least 7 codes away from its limit (the chain's
+    // end, or its first bit during the lead-in) and the ring holds 6 codes past it, so no step needs a
+    // limit test (two VALU per step fewer) and nothing enters or leaves a chain; otherwise each step
+    // tests the limit and a lane past it reads the zero byte after the table.
+    auto half_round = [&](auto fastc, bool feed) {
+        constexpr bool FAST = decltype(fastc)::value;
+        const uint32_t fill = kSlotBits * fd.f - 31;  // a window at p < fill reads filled ring words
         const uint32_t mlim = kRingM0 - min(on ? end : csr, fill);  // a step needs m > mlim
+        // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
+        // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
+        // A step reads the code's length (0: an escape), or, past the limit, the zero byte after the
+        // table: a chain that reads 0 stays put and reads 0 again, so the advancing steps are a prefix
+        // with no park flags, and an escape's window is the half's last (no lane masks and no SALU
+        // per step: 281 vs 330 clocks per step in tools/microbench/mb_walk_step.hip).
+        constexpr int S = kSegSteps / kWalkHalves;
+        uint32_t q[S];
+        uint32_t na = 0, W = 0, e = 0;
+        bool ok = true;
+        // issue priority over the dependent steps and the escape gather's issue, normal for the
+        // record select, feed and stores (extract 21.14-21.45 -> 20.48-20.62 ms, A/B)
+        __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-        for (int half = 0; half < kWalkHalves; ++half) {
-            // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
-            // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
-            // A step reads the code's length (0: an escape), or, past the limit, the zero byte after the
-            // table: a chain that reads 0 stays put and reads 0 again, so the advancing steps are a prefix
-            // with no park flags, and an escape's window is the half's last (no lane masks and no SALU
-            // per step: 281 vs 330 clocks per step in tools/microbench/mb_walk_step.hip).
-            constexpr int S = kSegSteps / kWalkHalves;
-            uint32_t q[S];
-            uint32_t na = 0, W = 0, e = 0;
-            bool ok = false;
-            // issue priority over the dependent steps and the escape gather's issue, normal for the
-            // record select, feed and stores (extract 21.14-21.45 -> 20.48-20.62 ms, A/B)
-            __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-            for (int t = 0; t < S; ++t) {
+        for (int t = 0; t < S; ++t) {
+            W = seg_window(ring, m);
+            if constexpr (FAST) {
+                e = lds8[W >> (32 - k8)];
+            } else {
                 ok = m > mlim;
-                W = seg_window(ring, m);
                 e = lds8[ok ? W >> (32 - k8) : 1u << 16];
-                HZ_WALK_FENCE();
-                m -= e;
-                na += e != 0u ? 1u : 0u;
-                q[t] = m;
             }
-            const bool pk = ok & (e == 0u);  // parked on an escape
-            const uint32_t nm = na + (pk ? 1u : 0u);
-            // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
-            // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
-            const uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
-            __builtin_amdgcn_s_setprio(0);
-            // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
-            // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
-            const uint32_t j1 = 8u - (cc & 7u);
-            const uint32_t jj = j1 <= na ? j1 : 0u;
-            static_assert(S <= 7, "q[jj - 1] for jj < 8");
-            uint32_t v[8];
-            v[0] = 0;
+            HZ_WALK_FENCE();
+            m -= e;
+            na += e != 0u ? 1u : 0u;
+            q[t] = m;
+        }
+        const bool pk = ok & (e == 0u);  // parked on an escape
+        const uint32_t nm = na + (pk ? 1u : 0u);
+        // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
+        // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
+        const uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
+        __builtin_amdgcn_s_setprio(0);
+        // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
+        // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
+        const uint32_t j1 = 8u - (cc & 7u);
+        const uint32_t jj = j1 <= na ? j1 : 0u;
+        static_assert(S <= 7, "q[jj - 1] for jj < 8");
+        uint32_t v[8];
+        v[0] = 0;
 #pragma unroll
-            for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : 0u;
-            const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
-            const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
-            const uint32_t sel = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
-            m -= pk ? ev : 0u;
-            // the round's feed right after its last escape wait and before the half's record stores: its
-            // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
-            // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
-            if (half == kWalkHalves - 1) seg_feed(a, ring, fd, kRingM0 - m);
-            const uint32_t pc = kRingM0 - m;
-            const uint32_t rm = jj ? sel : m;
+        for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : 0u;
+        const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
+        const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
+        const uint32_t sel = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+        m -= pk ? ev : 0u;
+        if constexpr (DEEP) {  // an escape the table leaves at 0: the code is longer than its m bits
+            const bool deep = pk & (ev == 0u);
+            if (__any(deep)) {
+                if (deep) m -= deep_len(a, abs0 + (kRingM0 - m) + a.bit_adj);
+            }
+        }
+        // the round's feed right after its last escape wait and before the half's record stores: its
+        // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
+        // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
+        if (feed) slot_feed(a, ring, fd, kRingM0 - m);
+        const uint32_t pc = kRingM0 - m;
+        const uint32_t rm = jj ? sel : m;
+        const uint32_t rp = on ? kRingM0 - rm : pc;
+        if constexpr (FAST) {
+            const bool rec = on & (j1 <= nm);  // (FAST: every codeword of the half starts before the end)
+            cc = on ? cc + nm : 0u;
+            if (rec) rec_put(rp);
+        } else {
             // the lead-in's last step lands on the entry: the entry is the record, counting starts there
             const bool enter = !on & (pc >= csr);
-            const uint32_t rp = on ? kRingM0 - rm : pc;
             const bool rec = (on ? j1 <= nm : enter) & (rp < end);  // (a codeword starting at the end is the next chain's)
             ent = enter ? pc : ent;
             cc = on ? cc + nm : 0u;
             on |= enter;
             if (rec) rec_put(rp);
+        }
+    };
+    for (;;) {
+        if (!__any(m > mend)) break;
+#pragma unroll
+        for (int half = 0; half < kWalkHalves; ++half) {
+            // FAST when every lane has 7 codes to its limit and 6 codes of filled ring (wave-uniform)
+            const uint32_t pp = kRingM0 - m;
+            const bool fast = pp + 7 * ml < (on ? end : csr) && pp + 6 * ml < kSlotBits * fd.f - 31;
+            if (__all(fast)) half_round(std::true_type(), half == kWalkHalves - 1);
+            else half_round(std::false_type(), half == kWalkHalves - 1);
         }
     }
     p = kRingM0 - m;
@@ -4056,6 +4183,32 @@ __global__ __launch_bounds__(kDecPipe2Threads) void k_chain_decode(DecArgs a, Ch
     dec_wave_chain(a, y, nb, lds, lds + a.lds_words + wid * 2 * slot, slot, b, stride, lane);
 }
 
+// Codebooks past the pipelined decoder's two table levels (codes longer than chain_k +
+// chain_level_bits bits): every record of every block serially, one thread per record of 8 codewords,
+// through br_next's multi-level lookup; the block count from the device (k_chain_meta).
+__global__ __launch_bounds__(kSyncThreads) void k_chain_decode_serial(DecArgs a, ChainArgs y) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(a.out);
+    const uint64_t nrec = y.info[0] * kChainRecs;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += stride) {
+        const ChainBlk& d = y.blk[i / kChainRecs];
+        const uint32_t t = (uint32_t)(i % kChainRecs);
+        if (t < d.lo || t >= d.hi) continue;
+        const long long o = d.out + 8ll * t;
+        const uint32_t cn = t + 1 == d.hi ? d.last : 8u;
+        BitReader r;
+        br_init(r, a, d.b0 + (uint16_t)(y.rec[d.rec + t] - (uint16_t)d.b0) + a.bit_adj);
+        for (uint32_t q = 0; q < cn; ++q) {
+            uint32_t sym;
+            const uint32_t L = br_next<DEC_LUT>(r, a, lds, sym);
+            if (L == 0) { atomicOr(a.err, 2u); break; }
+            if (o + q >= 0 && (uint64_t)(o + q) < a.nsym) out16[o + q] = (uint16_t)sym;
+        }
+    }
+}
+
 // One thread per chain: its head (true codewords before its first valid record), the codewords past
 // its record capacity, and the end bit of codeword nsym - 1, decoded serially (rare, short).
 template <int MODE>
@@ -4164,8 +4317,24 @@ uint64_t chain_scratch_words(uint64_t part_begin, uint64_t part_end, uint64_t ns
 }
 
 bool seg_decode_supported(const Tables& t) {
-    return t.dec_mode == DEC_LUT && t.walk_lds_bytes > 0 && t.walk8_bytes > 0 && t.dec_max_len <= 32 &&
-           t.dec_max_len <= t.dec_k + t.dec_level_bits;
+    return t.dec_mode >= 0 && t.dec_mode != DEC_FIXED16 && t.chain_lds_bytes > 0 && t.walk8_bytes > 0 &&
+           t.chain_esc != nullptr;
+}
+
+// Codes the pipelined chain decoder resolves (an LDS level, then one global level); longer codebooks
+// decode their records serially (k_chain_decode_serial).
+static bool chain_pipelined(const Tables& t) { return t.dec_max_len <= t.chain_k + t.chain_level_bits; }
+
+// The decoder arguments of the chain phases: the chain's LUT images (the decode tables' for a LUT
+// codebook, the LUT built beside a DENSE one).
+static void fill_chain_dec_args(DecArgs& d, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
+                                uint64_t nsym) {
+    fill_dec_args(d, t, d_payload, payload_bytes, nsym);
+    d.lds_img = t.chain_lds;
+    d.lds_words = t.chain_lds_bytes / 4;
+    d.k = t.chain_k;
+    d.level_bits = t.chain_level_bits;
+    d.l2 = t.chain_l2;
 }
 
 // HZ_CAPTURE_DEBUG=1 (debug): the stream's capture status after each step of the launchers.
@@ -4196,11 +4365,42 @@ struct ChainState {
     DecArgs d;
     WalkArgs w;
     unsigned long long* tiles = nullptr;  // scan scratch
+    uint64_t base = 0;                     // stream bit of byte 0 of the payload view (hz_indexless_scan)
     bool valid = false;
 };
 ChainState* chain_state_create() { return new ChainState(); }
 void chain_state_destroy(ChainState* st) { delete st; }
 const unsigned long long* chain_info(const ChainState* st) { return st->valid ? st->y.info : nullptr; }
+void chain_invalidate(ChainState* st) { st->valid = false; }
+
+// The part's summary in stream bits: codewords, true exit, entry in use (view bits + base).
+__global__ void k_chain_summary(const unsigned long long* info, unsigned long long* dst, uint64_t base) {
+    if (threadIdx.x == 0) {
+        dst[0] = info[3];
+        dst[1] = info[4] + base;
+        dst[2] = info[5] + base;
+    }
+}
+// The end bit in stream bits (all ones: not in this part).
+__global__ void k_chain_end(const unsigned long long* info, unsigned long long* dst, uint64_t base) {
+    if (threadIdx.x == 0) dst[0] = info[2] == ~0ull ? ~0ull : info[2] + base;
+}
+__global__ void k_put3(unsigned long long* dst, uint64_t a, uint64_t b, uint64_t c) {
+    if (threadIdx.x == 0) {
+        dst[0] = a;
+        dst[1] = b;
+        dst[2] = c;
+    }
+}
+hipError_t put3(unsigned long long* d_dst, uint64_t a, uint64_t b, uint64_t c, hipStream_t s) {
+    hipLaunchKernelGGL(k_put3, dim3(1), dim3(64), 0, s, d_dst, a, b, c);
+    return hipGetLastError();
+}
+hipError_t chain_summary(const ChainState* st, unsigned long long* d_dst, hipStream_t s) {
+    if (!st->valid) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_chain_summary, dim3(1), dim3(64), 0, s, (const unsigned long long*)st->y.info, d_dst, st->base);
+    return hipGetLastError();
+}
 
 // fix-ups (every chain once, then the listed ones on one workgroup), the scans and the descriptors
 static hipError_t chain_fix_and_meta(ChainState* st, const Tables& t, int ncu, hipStream_t s) {
@@ -4212,8 +4412,8 @@ static hipError_t chain_fix_and_meta(ChainState* st, const Tables& t, int ncu, h
     if ((e = ensure_lds_limit((const void*)k_chain_fix_loop<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
     uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
     wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
-    hipLaunchKernelGGL(k_chain_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, st->d, y);
-    hipLaunchKernelGGL(k_chain_fix_loop<DEC_LUT>, dim3(1), dim3(kSyncThreads), t.dec_lds_bytes, s, st->d, y);
+    hipLaunchKernelGGL(k_chain_fix<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.chain_lds_bytes, s, st->d, y);
+    hipLaunchKernelGGL(k_chain_fix_loop<DEC_LUT>, dim3(1), dim3(kSyncThreads), t.chain_lds_bytes, s, st->d, y);
     cap_check(s, "fix");
     if ((e = scan_u64(y.tcnt, y.nchains, st->tiles, y.first, s)) != hipSuccess) return e;
     if ((e = scan_u64(y.nblk, y.nchains, st->tiles, y.bbase, s)) != hipSuccess) return e;
@@ -4223,12 +4423,17 @@ static hipError_t chain_fix_and_meta(ChainState* st, const Tables& t, int ncu, h
 }
 
 hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes,
-                      uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end, uint64_t entry0,
-                      unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s) {
+                      uint64_t base, uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end,
+                      uint64_t entry0, unsigned long long* d_scratch, uint32_t* d_err, int ncu, hipStream_t s) {
     st->valid = false;
+    // bits of the view from here on: stream bit b is view bit b - base (mod 2^64: start_bit may lie
+    // before the view when it begins inside the stream)
+    st->base = base;
+    start_bit -= base;
+    if (entry0 != ~0ull) entry0 -= base;
     if (!seg_decode_supported(t)) return hipErrorInvalidValue;
     DecArgs& d = st->d;
-    fill_dec_args(d, t, d_payload, payload_bytes, nsym);
+    fill_chain_dec_args(d, t, d_payload, payload_bytes, nsym);
     d.starts = nullptr; d.subs = nullptr; d.out = nullptr; d.err = d_err;
     if (d.nwords < 4) return hipErrorInvalidValue;
     const ChainGeom& g = st->g = chain_geom(part_begin, part_end,
@@ -4257,9 +4462,10 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
     WalkArgs& w = st->w;
     w.words = d.words; w.nwords = d.nwords; w.bit_adj = d.bit_adj;
     w.start = start_bit; w.nseg = 0;
-    w.lds_img = t.d_walk_lds; w.lds_words = t.walk_lds_bytes / 4;
-    w.k = t.walk_k; w.bias = t.walk_bias; w.esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc); w.m = t.walk_m;
+    w.lds_img = nullptr; w.lds_words = 0; w.k = 0; w.bias = 0;
+    w.esc = t.chain_esc; w.m = t.chain_esc_m;
     w.w8_img = t.d_walk8; w.w8_words = t.walk8_bytes / 4; w.k8 = t.walk8_k;
+    w.lut1 = t.chain_lds; w.lut2 = t.chain_l2; w.lutk = t.chain_k;
     w.bmp = nullptr; w.cnt = nullptr; w.ent = nullptr; w.dirty = nullptr;
     // test hook: HZ_SEG_LEAD=<bits> (0: no lead-in, so nearly every chain takes the fix-up path)
     static const uint32_t lead = [] { const char* v = getenv("HZ_SEG_LEAD"); return v ? (uint32_t)atoi(v) : kWalkLead; }();
@@ -4271,11 +4477,13 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
         wpg = wpg < 1 ? 1 : (wpg > (uint64_t)kChainWalkWaves ? (uint64_t)kChainWalkWaves : wpg);
         const uint32_t threads = (uint32_t)(64 * wpg);
         const uint32_t ring_bytes = kSegRing * kRingRow * 4 + threads * 16;  // ring rows (1024 lanes), record buffers
-        if ((e = ensure_lds_limit((const void*)k_chain_walk, (int)(kChainWalkWaves * 64 * (kSegRing * 4 + 16)))) !=
-            hipSuccess)
-            return e;
+        // DEEP: escapes past the escape table's bits (codes longer than kChainEscMaxBits)
+        const bool deep = t.dec_max_len > t.chain_esc_m;
+        const void* fn = deep ? (const void*)k_chain_walk<true> : (const void*)k_chain_walk<false>;
+        if ((e = ensure_lds_limit(fn, (int)(kChainWalkWaves * 64 * (kSegRing * 4 + 16)))) != hipSuccess) return e;
         const uint64_t wgs = (g.nchains + threads - 1) / threads;
-        hipLaunchKernelGGL(k_chain_walk, dim3(wgs), dim3(threads), ring_bytes, s, w, y);
+        if (deep) hipLaunchKernelGGL(k_chain_walk<true>, dim3(wgs), dim3(threads), ring_bytes, s, w, y);
+        else hipLaunchKernelGGL(k_chain_walk<false>, dim3(wgs), dim3(threads), ring_bytes, s, w, y);
         cap_check(s, "walk");
     }
     // 2.-4. fix-ups, scans, block descriptors and the part's summary
@@ -4286,7 +4494,7 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
 
 hipError_t chain_refix(ChainState* st, const Tables& t, uint64_t entry0, int ncu, hipStream_t s) {
     if (!st->valid) return hipErrorInvalidValue;
-    st->y.entry0 = entry0;
+    st->y.entry0 = entry0 != ~0ull ? entry0 - st->base : entry0;
     return chain_fix_and_meta(st, t, ncu, s);
 }
 
@@ -4299,7 +4507,12 @@ hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t*
     d.nsym = nsym;
     hipError_t e;
     if ((e = hipMemsetAsync(y.info + 2, 0xff, 8, s)) != hipSuccess) return e;  // end bit: not found
-    if (nsym) {
+    if (nsym && !chain_pipelined(t)) {
+        // 5'. codes past two table levels: the records one thread each
+        if ((e = ensure_lds_limit((const void*)k_chain_decode_serial, kLdsBytes)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_chain_decode_serial, dim3(4 * ncu), dim3(kSyncThreads), t.chain_lds_bytes, s, d, y);
+    }
+    if (nsym && chain_pipelined(t)) {
         // 5. the block decoder: k_decode's slot sizing, two slots per wave, persistent over every CU
         if ((e = ensure_lds_limit((const void*)k_chain_decode, kLdsBytes)) != hipSuccess) return e;
         const uint64_t bits = st->g.pend - st->g.pbeg;
@@ -4320,13 +4533,21 @@ hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t*
         const uint32_t lds = 4 * (table + b.region_words);
         hipLaunchKernelGGL(k_chain_decode, dim3(ncu), dim3(threads), lds, s, b, y);
         cap_check(s, "decode");
+    }
+    if (nsym) {
         // 6. heads, records past the capacity, the end bit
         if ((e = ensure_lds_limit((const void*)k_chain_tail<DEC_LUT>, kLdsBytes)) != hipSuccess) return e;
         uint64_t wgs = (y.nchains + kSyncThreads - 1) / kSyncThreads;
         wgs = wgs < (uint64_t)ncu ? (wgs ? wgs : 1) : (uint64_t)ncu;
-        hipLaunchKernelGGL(k_chain_tail<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.dec_lds_bytes, s, d, y);
+        hipLaunchKernelGGL(k_chain_tail<DEC_LUT>, dim3(wgs), dim3(kSyncThreads), t.chain_lds_bytes, s, d, y);
     }
-    if (d_end && (e = hipMemcpyAsync(d_end, y.info + 2, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if (d_end) {
+        if (st->base == 0) {
+            if ((e = hipMemcpyAsync(d_end, y.info + 2, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        } else {
+            hipLaunchKernelGGL(k_chain_end, dim3(1), dim3(64), 0, s, (const unsigned long long*)y.info, d_end, st->base);
+        }
+    }
     cap_check(s, "tail+end");
     return hipGetLastError();
 }

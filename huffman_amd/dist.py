@@ -218,14 +218,18 @@ UNKNOWN_ENTRY = (1 << 64) - 1
 
 def part_range(payload_bits, world, rank, align=128):
     """Payload bits [begin, end) (after the stream's first bit) of rank `rank`'s part: equal parts,
-    boundaries on `align` bits, the last part takes the rest."""
-    per = (payload_bits // world) // align * align
+    boundaries on `align` bits, the last non-empty part takes the rest. A payload shorter than `world`
+    aligned parts has fewer parts: the ranks past them get the empty part [payload_bits, payload_bits)."""
+    parts = max(1, min(world, payload_bits // align))
+    if rank >= parts:
+        return payload_bits, payload_bits
+    per = (payload_bits // parts) // align * align
     beg = per * rank
-    end = payload_bits if rank == world - 1 else beg + per
+    end = payload_bits if rank == parts - 1 else beg + per
     return beg, end
 
 
-def decode_indexless_split(scan, refix, decode, nsym, device, group=None):
+def decode_indexless_split(scan, refix, decode, nsym, device, group=None, empty=False):
     """The exchange of a split index-less decode. Per-rank engines (every bit a stream bit, the same
     coordinates on every rank):
       scan() -> (codewords, exit, walked entry) of this rank's part (rank 0: from the stream's start)
@@ -233,21 +237,27 @@ def decode_indexless_split(scan, refix, decode, nsym, device, group=None):
       decode(first, nsym_from_first) -> decodes the part's codewords (at most nsym_from_first)
     On the GPU these are hz_indexless_scan / hz_indexless_refix / hz_indexless_decode (bench.py,
     tests/test_gpu_dist.py); tests/test_dist.py drives the same exchange with the CPU oracle's walk.
+    empty: this rank's part is empty (part_range past the parts of a short payload): no engine is
+    called, the rank passes the previous part's exit on and still joins every all-gather.
     Returns (first symbol of this rank, its codewords, rounds of refixes)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    count, exit_, entry = scan()
+    count, exit_, entry = (0, UNKNOWN_ENTRY, UNKNOWN_ENTRY) if empty else scan()
     rounds = 0
     while True:
-        mine = torch.tensor([count, exit_ & ((1 << 63) - 1), exit_ >> 63, entry & ((1 << 63) - 1), entry >> 63],
-                            dtype=torch.int64, device=device)
-        allv = torch.zeros(world * 5, dtype=torch.int64, device=device)
+        mine = torch.tensor([count, exit_ & ((1 << 63) - 1), exit_ >> 63, entry & ((1 << 63) - 1), entry >> 63,
+                             1 if empty else 0], dtype=torch.int64, device=device)
+        allv = torch.zeros(world * 6, dtype=torch.int64, device=device)
         dist.all_gather_into_tensor(allv, mine, group=group)
-        v = allv.view(world, 5).cpu().tolist()
+        v = allv.view(world, 6).cpu().tolist()
         counts = [int(x[0]) for x in v]
         exits = [int(x[1]) | (int(x[2]) << 63) for x in v]
         entries = [int(x[3]) | (int(x[4]) << 63) for x in v]
-        stale = [r for r in range(1, world) if entries[r] != exits[r - 1]]
+        void = [bool(x[5]) for x in v]
+        for r in range(1, world):  # an empty part's entry and exit are the previous part's exit
+            if void[r]:
+                entries[r] = exits[r] = exits[r - 1]
+        stale = [r for r in range(1, world) if not void[r] and entries[r] != exits[r - 1]]
         if not stale:
             break
         if rounds >= world:  # a change moves one part per round: cannot happen
@@ -257,5 +267,69 @@ def decode_indexless_split(scan, refix, decode, nsym, device, group=None):
             count, exit_, entry = refix(exits[rank - 1])
     first = sum(counts[:rank])
     take = max(0, min(count, nsym - first))
-    decode(first, take)
+    if not empty:
+        decode(first, take)
     return first, count, rounds
+
+
+def part_window(start_bit, part_begin, part_end, max_len, lead=1024):
+    """Global payload words [lo, hi) a rank's part reads: the part (payload bits after start_bit), the
+    lead-in before it (HZ_INDEXLESS_LEAD_BITS, or the stream from its start) and max_len bits after it."""
+    b0 = start_bit + part_begin - min(lead, part_begin)
+    b1 = start_bit + part_end + max_len
+    return b0 // 32, (b1 + 31) // 32
+
+
+def fill_window(ext, ext_word0, own_word0, own_words, windows, shards, group=None, via_host=False):
+    """Bring the words of this rank's part window that other ranks' shards hold into `ext`.
+
+    ext: this rank's uint8 device buffer holding global payload words [ext_word0, ext_word0 + len/4), its
+    own shard packed in place at words [own_word0, own_word0 + own_words) (zeros around it);
+    windows[r] = (lo, hi): the global words rank r's part reads; shards[r] = (word0, words): rank r's
+    shard. For every pair of ranks, the words of one's shard inside the other's window travel
+    point-to-point (RCCL over xGMI; gloo through host copies when via_host) and are ORed in (adjacent
+    shards share a boundary word). Every rank knows every window and shard, so the sends and receives
+    match without a handshake. The window must lie inside ext (the caller sizes ext's halo)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = windows[rank]
+    assert ext_word0 <= lo and hi <= ext_word0 + ext.numel() // 4, "part window outside the buffer"
+
+    def inter(win, shard):
+        a = max(win[0], shard[0])
+        b = min(win[1], shard[0] + shard[1])
+        return (a, b) if a < b else None
+
+    sends, recvs = [], []
+    for g in range(world):
+        if g == rank:
+            continue
+        s = inter(windows[g], (own_word0, own_words))
+        if s:
+            sends.append((g, ext[4 * (s[0] - ext_word0):4 * (s[1] - ext_word0)]))
+        r = inter((lo, hi), shards[g])
+        if r:
+            recvs.append((g, r, torch.empty(4 * (r[1] - r[0]), dtype=torch.uint8,
+                                            device="cpu" if via_host else ext.device)))
+    if via_host:
+        # blocking, in a global order every rank follows: (src, dst) pairs by (min, max) rank
+        pairs = sorted({(min(rank, g), max(rank, g)) for g, _ in sends} | {(min(rank, g), max(rank, g)) for g, _, _ in recvs})
+        sd = {g: t for g, t in sends}
+        rv = {g: t for g, _, t in recvs}
+        for a, b in pairs:
+            g = b if a == rank else a
+            first = a == rank  # the lower rank sends first
+            for phase in (0, 1):
+                if (phase == 0) == first:
+                    if g in sd:
+                        dist.send(sd[g].cpu().contiguous(), _global(group, g), group=group)
+                elif g in rv:
+                    dist.recv(rv[g], _global(group, g), group=group)
+    else:
+        ops = [dist.P2POp(dist.isend, t, _global(group, g), group=group) for g, t in sends]
+        ops += [dist.P2POp(dist.irecv, t, _global(group, g), group=group) for g, _, t in recvs]
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+    for g, (a, b), t in recvs:
+        ext[4 * (a - ext_word0):4 * (b - ext_word0)].bitwise_or_(t.to(ext.device))

@@ -225,9 +225,11 @@ int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes
  * does). Stream-ordered: no host synchronisation (a HIP graph can capture it)
  * unless the context's scratch grows. A FIXED16 codebook (every code 16 bits)
  * needs no walk: symbol i sits at start_bit + 16 i, decoded directly (also
- * stream-ordered). Codebooks the chain decoder does not take (codes longer than
- * 25 bits, DENSE tables) go through hz_index_build + hz_decode, with the same
- * result (that path synchronises). */
+ * stream-ordered). Every other codebook takes the chain path: DENSE codebooks
+ * through a LUT built beside their tables, codes longer than 25 bits through
+ * DEEP escapes (the walk resolves them in the decode LUT) and a serial record
+ * decoder. Only payloads under 16 bytes go through hz_index_build + hz_decode
+ * (that path synchronises). */
 int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                         uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
 
@@ -241,18 +243,35 @@ int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_
  *       entry: right for the stream's first part, and for every part whose
  *       lead-in resynchronised). d_summary (device, 3 x u64): codewords of the
  *       part, its true exit bit (the next part's true entry), the entry bit in
- *       use (entry_bit, or the walked entry for UINT64_MAX). Bits are stream bits from byte 0 of d_payload, which must hold the
- *       part plus 1024 bits before it and max_len bits after it.
+ *       use (entry_bit, or the walked entry for UINT64_MAX).
+ *       Bits are STREAM bits: bit 0 is bit 0 of the stream's payload buffer
+ *       (the one hz_decode_indexless takes), and d_payload holds stream bits
+ *       [payload_bit_base, payload_bit_base + 8 * payload_bytes) -- a rank may
+ *       pass only its slice (payload_bit_base a multiple of 8). The slice must
+ *       hold the part and the HZ_INDEXLESS_LEAD_BITS before it (or the stream
+ *       from its start), else HZ_EINVAL; the part's last codeword may run up to
+ *       max_len bits past part_end (missing bits read as zeros: keep them in
+ *       the slice). nsym: the stream's symbols (sizes the part's record capacity
+ *       from its mean bits per codeword; 0 = unknown: the codebook's estimate).
  *   hz_indexless_refix : the part again from its true entry (the previous
  *       part's exit, when it differs from the walked entry); d_summary updated.
  *   hz_indexless_decode : the part's codewords into d_out (2 bytes each, from
  *       the part's first codeword), at most nsym of them (the stream's symbols
  *       from the part's first on); *d_end_bit as hz_decode_indexless when the
- *       stream's last codeword falls in this part.
- * The three calls use the context's scratch: one part per context at a time.
- * Codebooks as hz_decode_indexless's chain path only (HZ_EINVAL otherwise). */
-int hz_indexless_scan(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
-                      uint64_t part_begin, uint64_t part_end, uint64_t entry_bit, uint64_t *d_summary);
+ *       stream's last codeword falls in this part (a stream bit).
+ * The three calls keep their state in the context's scratch and point at its
+ * decode tables: one part per context at a time, and any other call that uses
+ * the scratch or the tables (hz_pack*, hz_index_build, hz_decode_indexless,
+ * hz_codebook_upload_decode) ends the pending part -- hz_indexless_refix /
+ * _decode then return HZ_EINVAL. The same holds for a HIP graph that captured
+ * hz_decode_indexless: replay it only while no call on the context has grown
+ * the scratch or replaced the decode tables since the capture.
+ * Every codebook takes this path; a FIXED16 part (every code 16 bits) is
+ * arithmetic: codeword i at start_bit + 16 i, no walk. */
+#define HZ_INDEXLESS_LEAD_BITS 1024
+int hz_indexless_scan(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t payload_bit_base,
+                      uint64_t start_bit, uint64_t nsym, uint64_t part_begin, uint64_t part_end, uint64_t entry_bit,
+                      uint64_t *d_summary);
 int hz_indexless_refix(hz_ctx *ctx, uint64_t entry_bit, uint64_t *d_summary);
 int hz_indexless_decode(hz_ctx *ctx, uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
 

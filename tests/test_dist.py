@@ -181,7 +181,11 @@ def _split_worker(rank, world, port, n_total, kind, lead, result_path):
             _, _, syms = oracle_lib.walk(pay, ln, code, st["entry"], start + end, max_count=max(take, 0), decode=True)
             st["out"] = (first, syms[:2 * take].tobytes())
 
-        first, count, rounds = hd.decode_indexless_split(scan, refix, decode, nsym, torch.device("cpu"))
+        empty = beg == end  # a payload shorter than `world` parts: the trailing ranks have none
+        first, count, rounds = hd.decode_indexless_split(scan, refix, decode, nsym, torch.device("cpu"),
+                                                         empty=empty)
+        if empty:
+            st["out"] = (first, b"")
         parts = [None] * world
         dist.all_gather_object(parts, (st["out"][0], st["out"][1], rounds))
         if rank == 0:
@@ -197,9 +201,65 @@ def _split_worker(rank, world, port, n_total, kind, lead, result_path):
 
 @pytest.mark.parametrize("world,n_total,kind,lead", [(2, 300001, 1, 1024), (3, 1 << 20, 1, 1024), (3, 200000, 1, 0),
                                                      (8, (1 << 20) + 7, 1, 1024), (8, 1 << 19, 0, 0),
-                                                     (8, 400002, 1, 0)])
+                                                     (8, 400002, 1, 0), (8, 301, 1, 1024), (3, 41, 1, 1024)])
 def test_indexless_split_over_ranks(tmp_path, world, n_total, kind, lead):
+    """(The last two: payloads of fewer than `world` 128-bit parts -- trailing ranks get empty parts,
+    join every all-gather and pass the exit on, instead of failing before it and hanging the group.)"""
     result = str(tmp_path / "result.txt")
     mp.start_processes(_split_worker, args=(world, _free_port(), n_total, kind, lead, result), nprocs=world, join=True,
+                       start_method="spawn")
+    assert open(result).read() == "ok"
+
+
+def _window_worker(rank, world, port, result_path):
+    """dist.fill_window on CPU tensors (gloo): shards of one global bit stream packed at their bit offsets
+    into word-aligned buffers with a halo (adjacent shards share a boundary word); after the fill, every
+    rank's part window holds the global stream's words exactly."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from huffman_amd import dist as hd
+        rng = np.random.default_rng(3)
+        bits = [int(b) for b in rng.integers(3000, 9000, world)]  # shard payload bits (uneven)
+        S0 = 5
+        total = sum(bits)
+        nw = (S0 + total + 31) // 32 + 64
+        stream = np.zeros(nw * 32, dtype=np.uint8)
+        stream[S0:S0 + total] = rng.integers(0, 2, total)
+        gwords = np.packbits(stream).view(">u4").astype(np.uint32)  # big-endian words of the global stream
+        offs = [sum(bits[:g]) for g in range(world)]
+        shards = []
+        for g in range(world):
+            w0, start, words = hd.local_geometry(S0, offs[g], bits[g], g == 0)
+            shards.append((w0, words))
+        w0, words = shards[rank]
+        halo = 256
+        ext = torch.zeros(4 * (2 * halo + words + 4), dtype=torch.uint8)
+        # this rank's shard: only its own bits (zeros elsewhere in its boundary words)
+        own = np.zeros(words * 32, dtype=np.uint8)
+        a = S0 + offs[rank] - 32 * w0
+        own[a:a + bits[rank]] = stream[S0 + offs[rank]:S0 + offs[rank] + bits[rank]]
+        ext[4 * halo:4 * (halo + words)] = torch.from_numpy(np.packbits(own).copy())
+        parts = [hd.part_range(total, world, r) for r in range(world)]
+        windows = [hd.part_window(S0, pb, pe, 22, lead=1024) for pb, pe in parts]
+        hd.fill_window(ext, w0 - halo, w0, words, windows, shards, via_host=True)
+        lo, hi = windows[rank]
+        got = ext[4 * (lo - (w0 - halo)):4 * (hi - (w0 - halo))].numpy().view(">u4")
+        want = gwords[lo:hi]
+        ok = np.array_equal(got, want)
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write("ok" if all(flags) else f"mismatch {flags}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_fill_window_brings_neighbour_words(tmp_path, world):
+    result = str(tmp_path / "result.txt")
+    mp.start_processes(_window_worker, args=(world, _free_port(), result), nprocs=world, join=True,
                        start_method="spawn")
     assert open(result).read() == "ok"

@@ -127,8 +127,12 @@ def test_bench_rehearsal_three_ranks(tmp_path):
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert line["n_gpus"] == 3 and line["roundtrip_bit_exact"]
+    assert line["n_gpus"] == 3 and line["roundtrip_bit_exact"]  # every rank's, the split drop-in's included
     assert line["reassembly_outside_step"]["whole_stream_decoded_bit_exact"]
+    # the drop-in figure is ONE stream's extract split over the ranks at equal bit parts
+    chk = line["dropin"]["split_check_rank0"]
+    assert chk["bit_exact"] and chk["first_symbol"] == 0 and chk["symbols"] > 0
+    assert line["dropin"]["decode"].startswith("index-less extract of the one global stream")
 
 
 @pytest.mark.timeout(900)
@@ -152,14 +156,15 @@ def test_bench_rehearsal_eight_ranks_1gib_shards(tmp_path, dist_kind):
     r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=840)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert line["n_gpus"] == 8 and line["roundtrip_bit_exact"]
+    assert line["n_gpus"] == 8 and line["roundtrip_bit_exact"]  # every rank's, the split drop-in's included
+    assert line["dropin"]["split_check_rank0"]["bit_exact"]
     re = line["reassembly_outside_step"]
     assert re["whole_stream_decoded_bit_exact"]
     if dist_kind == "uniform":
         assert line["config"]["payload_bytes_rank0"] > (1 << 30) + 4  # a shard body spans two messages
 
 
-def _split_worker(rank, world, port, n_total, lead, result_dir):
+def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
     """One index-less stream decoded by `world` ranks on one GPU, one part each, through
     hz_indexless_scan / hz_indexless_refix / hz_indexless_decode and the exchange of
     huffman_amd/dist.py decode_indexless_split (gloo here; RCCL on a multi-GPU node)."""
@@ -177,8 +182,18 @@ def _split_worker(rank, world, port, n_total, lead, result_dir):
         from huffman_amd.pipeline import StreamCodec
         codec = StreamCodec(0)
         dev = codec.device
-        x = torch.empty(n_total, dtype=torch.uint8, device=dev)
-        codec.dev.generate(x.data_ptr(), n_total, offset=0, kind=1, alpha=1.1, seed=7)
+        if kind == "zipf":
+            x = torch.empty(n_total, dtype=torch.uint8, device=dev)
+            codec.dev.generate(x.data_ptr(), n_total, offset=0, kind=1, alpha=1.1, seed=7)
+        elif kind == "dense":  # every code 11-12 bits: a DEC_DENSE codebook (the LUT built beside it)
+            g = torch.Generator(device=dev)
+            g.manual_seed(5)
+            s = torch.randint(0, 3000, (n_total // 2,), dtype=torch.int32, device=dev, generator=g)
+            x = (s * 19 + 7).to(torch.int16).view(torch.uint8)
+        else:  # "deep": Fibonacci counts, codes of up to 31 bits (DEEP escapes, serial records)
+            from test_gpu_extract import _fib_stream
+            x = torch.from_numpy(_fib_stream(2)).to(dev)
+        n_total = x.numel()
         plan, payload, _ = codec.encode(x)  # every rank holds the whole stream (as read from one file)
         codec.sync()
         nsym = n_total // 2
@@ -216,8 +231,8 @@ def _split_worker(rank, world, port, n_total, lead, result_dir):
         dist.all_gather(allf, flags)
         total = sum(int(f[2]) for f in allf)
         status = "ok" if all(int(f[0]) == 0 for f in allf) and total == nsym else f"bad {[f.tolist() for f in allf]}"
-        if lead == 0 and rank == 0:
-            status += f" rounds={rounds}"
+        if lead == 0 and world > 1 and rounds < 1:  # no lead-in: the refix exchange must have run
+            status = f"bad rounds={rounds}"
     finally:
         with open(os.path.join(result_dir, f"r{rank}.txt"), "w") as f:
             f.write(status)
@@ -225,10 +240,13 @@ def _split_worker(rank, world, port, n_total, lead, result_dir):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,n_total,lead", [(2, (8 << 20) + 2, None), (3, (24 << 20) + 6, None),
-                                                (8, (64 << 20) + 2, None), (4, (16 << 20) + 2, 0)])
-def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead):
-    mp.start_processes(_split_worker, args=(world, _free_port(), n_total, lead, str(tmp_path)), nprocs=world,
+@pytest.mark.parametrize("world,n_total,lead,kind", [(2, (8 << 20) + 2, None, "zipf"), (3, (24 << 20) + 6, None, "zipf"),
+                                                     (8, (64 << 20) + 2, None, "zipf"), (4, (16 << 20) + 2, 0, "zipf"),
+                                                     (3, (64 << 20) + 2, None, "dense"), (2, 0, None, "deep")])
+def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead, kind):
+    """One index-less stream split over `world` ranks on one GPU: Zipf (LUT tables), a DEC_DENSE codebook
+    (hz_indexless_scan used to refuse it) and 31-bit codes (DEEP escapes, serial records)."""
+    mp.start_processes(_split_worker, args=(world, _free_port(), n_total, lead, str(tmp_path), kind), nprocs=world,
                        join=True, start_method="spawn")
     for r in range(world):
         assert open(tmp_path / f"r{r}.txt").read().startswith("ok"), open(tmp_path / f"r{r}.txt").read()

@@ -265,3 +265,86 @@ def test_indexless_25_bit_codes_stream_ordered(codec):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out[:n], x)
+
+
+def _dense_stream(nsym, seed):
+    """u16 symbols uniform over 3000 values: every code 11 or 12 bits (a DEC_DENSE codebook)."""
+    import torch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    s = torch.randint(0, 3000, (nsym,), dtype=torch.int32, device="cuda", generator=g)
+    return (s * 19 + 7).to(torch.int16).view(torch.uint8)
+
+
+def _fib_stream(seed):
+    """32 symbols with Fibonacci counts (1, 1, 2, 3, 5, ..., F(32)): the Huffman tree is a path, so the
+    longest codes are 31 bits -- past the chain walker's 25-bit escape table (DEEP escapes through the
+    decode LUT) and the pipelined decoder's two table levels (records decoded serially)."""
+    c = [1, 1]
+    while len(c) < 32:
+        c.append(c[-1] + c[-2])
+    sym = np.repeat((np.arange(32, dtype=np.uint32) * 2053 % 65536).astype(np.uint16), c)
+    np.random.default_rng(seed).shuffle(sym)
+    return sym.view(np.uint8)
+
+
+def _captured_indexless(codec, x, plan, payload, nsym):
+    """hz_decode_indexless eager, then captured in a HIP graph and replayed: (eager ok, replay ok, end bit)."""
+    import torch
+    out = torch.zeros(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+    end = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+
+    def call():
+        codec.dev.decode_indexless(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, out.data_ptr(),
+                                   end.data_ptr())
+
+    call()
+    codec.sync()
+    eager = bool(torch.equal(out[:2 * nsym], x[:2 * nsym]))
+    end_bit = int(end[0].item())
+    out.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=codec.stream):  # a host synchronisation inside would break the capture
+        call()
+    g.replay()
+    torch.cuda.synchronize()
+    return eager, bool(torch.equal(out[:2 * nsym], x[:2 * nsym])), end_bit
+
+
+def test_indexless_dense_codebook_256mib_chain_path(codec):
+    """A DEC_DENSE codebook (every code 11-12 bits) at 256 MiB: the chain walk + chain-block decode take
+    it through the LUT built beside the DENSE tables -- stream-ordered (captured in a HIP graph and
+    replayed bit-exact), end bit equal to pack's."""
+    from huffman_amd import codebook_arrays, index_starts
+    nsym = 128 << 20
+    x = _dense_stream(nsym, 3)
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    _, ln, _ = codebook_arrays(plan.cb)
+    used = ln[ln > 0]
+    assert int(used.max()) <= 16 and int(used.max()) - int(used.min()) <= 3  # DEC_DENSE
+    end_pack = int(index_starts(index.cpu().numpy(), nsym)[-1])
+    eager, replay, end_bit = _captured_indexless(codec, x, plan, payload, nsym)
+    assert eager and replay and end_bit == end_pack
+
+
+@pytest.mark.parametrize("shift", [0, 7])
+def test_indexless_31_bit_codes_chain_path(codec, shift):
+    """Codes of up to 31 bits (Fibonacci counts): DEEP escapes in the walk and the serial record decoder,
+    stream-ordered (graph capture), bit-exact; also moved `shift` bytes into a buffer."""
+    import torch
+    from huffman_amd import codebook_arrays
+    x = torch.from_numpy(_fib_stream(1)).cuda()
+    plan, _, _ = codec.encode(x)
+    codec.sync()
+    _, ln, _ = codebook_arrays(plan.cb)
+    assert int(ln.max()) == 31
+    ok, end_ok = _check(codec, x, shift)
+    assert ok and end_ok
+    if shift == 0:
+        nsym = x.numel() // 2
+        plan, payload, _ = codec.encode(x)
+        codec.sync()
+        eager, replay, _ = _captured_indexless(codec, x, plan, payload, nsym)
+        assert eager and replay
