@@ -89,8 +89,6 @@ struct hz_ctx {
     double thr_alpha = -1.0;
     hipEvent_t ev[5][2] = {};
     bool ev_used[5] = {false, false, false, false, false};
-    unsigned long long* d_xidx = nullptr;  // hz_decode_indexless fallback: a block index
-    uint64_t xidx_cap = 0;                 // bytes
     Staging stage_enc, stage_dec;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
            cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_walk8 = 0, cap_chain_lds = 0, cap_chain_l2 = 0,
@@ -185,7 +183,6 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
     (void)hipHostFree(c->h_err);
     for (int i = 0; i < 5; ++i)
         for (int j = 0; j < 2; ++j) (void)hipEventDestroy(c->ev[i][j]);
-    (void)hipFree(c->d_xidx);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return HZ_OK;
@@ -577,35 +574,6 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     return arm_err_check(c);
 }
 
-// hz_decode_indexless through a rebuilt block index (hz_index_build, then the block decoder): for
-// codebooks the piece decoder does not take and segments with more pieces than it planned.
-static int hz_decode_indexless_via_index(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes,
-                                         uint64_t start_bit, uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
-    const uint64_t ib = hz_index_bytes(nsym);
-    if (c->xidx_cap < ib) {
-        HZ_TRY(hipStreamSynchronize(c->stream));
-        (void)hipFree(c->d_xidx);
-        c->d_xidx = nullptr;
-        c->xidx_cap = 0;
-        HZ_TRY(hipMalloc(&c->d_xidx, ib));
-        c->xidx_cap = ib;
-    }
-    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
-    int rc = hz_index_build(c, d_payload, payload_bytes, start_bit, nsym, (uint64_t*)c->d_xidx);
-    if (rc) return rc;
-    const uint64_t* end = (const uint64_t*)c->d_xidx + index_blocks(nsym);
-    if (d_end_bit) HZ_TRY(hipMemcpyAsync(d_end_bit, end, 8, hipMemcpyDeviceToDevice, c->stream));
-    // a payload with fewer than nsym codewords (end bit all ones) must not reach the decoder
-    uint64_t eb = 0;
-    HZ_TRY(hipMemcpyAsync(&eb, end, 8, hipMemcpyDeviceToHost, c->stream));
-    if ((rc = hz_ctx_sync(c))) return rc;
-    if (eb > payload_bytes * 8) return HZ_OK;  // the caller sees the end bit past the payload
-    if ((rc = hz_decode(c, d_payload, payload_bytes, nsym, (const uint64_t*)c->d_xidx, d_out))) return rc;
-    HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
-    c->ev_used[HZ_STAGE_EXTRACT] = true;
-    return arm_err_check(c);
-}
-
 extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
                                    uint64_t nsym, uint8_t* d_out, uint64_t* d_end_bit) {
     if (!c) return HZ_EINVAL;
@@ -634,10 +602,15 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
         c->ev_used[HZ_STAGE_EXTRACT] = true;
         return arm_err_check(c);
     }
-    // codebooks the chain decoder does not take (DENSE tables, codes > 24 bits): block index, then the
-    // block decoder
-    if (!seg_decode_supported(c->t) || payload_bytes < 16)
-        return hz_decode_indexless_via_index(c, d_payload, payload_bytes, start_bit, nsym, d_out, d_end_bit);
+    if (!seg_decode_supported(c->t)) return HZ_EINVAL;  // (every codebook but FIXED16 has chain tables)
+    if (payload_bytes < 16) {  // too short for the walk: one thread, serially (stream-ordered too)
+        HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
+        HZ_TRY(chain_decode_tiny(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
+                                 reinterpret_cast<unsigned long long*>(d_end_bit), c->d_err, c->stream));
+        HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 1));
+        c->ev_used[HZ_STAGE_EXTRACT] = true;
+        return arm_err_check(c);
+    }
     // stream-ordered from here: walk, fix-ups, scans, block decode, tails (no host synchronisation
     // unless the context's scratch has to grow)
     const uint64_t pbits = payload_bytes * 8 > start_bit ? payload_bytes * 8 - start_bit : 0;

@@ -261,6 +261,9 @@ hipError_t chain_scan(ChainState* st, const Tables& t, const uint8_t* d_payload,
 hipError_t chain_refix(ChainState* st, const Tables& t, uint64_t entry0, int ncu, hipStream_t s);
 hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t* d_out, unsigned long long* d_end,
                         int ncu, hipStream_t s);
+// payloads under 16 bytes: one thread, serially, stream-ordered (d_end: the end bit or UINT64_MAX)
+hipError_t chain_decode_tiny(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                             uint64_t nsym, uint8_t* d_out, unsigned long long* d_end, uint32_t* d_err, hipStream_t s);
 const unsigned long long* chain_info(const ChainState* st);
 void chain_invalidate(ChainState* st);  // the scratch or tables it points into changed
 hipError_t chain_summary(const ChainState* st, unsigned long long* d_dst, hipStream_t s);  // 3 x u64, stream bits

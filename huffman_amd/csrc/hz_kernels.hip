@@ -3607,81 +3607,6 @@ HZ_DEV void seg_feed(const WalkArgs& a, uint32_t* ring, SegFeed& fd, uint32_t p)
 constexpr int kSegSteps = 14;
 static_assert(kSegSteps / kWalkHalves + 1 <= 8, "one record per half-round");
 
-// The chain walk's ring in two SLOTS of 256 bits (ring words 8 s .. 8 s + 7, rows 15 - 8 s - j, row 16
-// the copy of word 15): a round takes up to 14 codewords (~162 bits of Zipf), more than one 128-bit
-// chunk, so a ring fed one chunk per round starves (~21 % of the steps of a 16 GiB Zipf walk idle at the
-// fill limit); one 256-bit slot per round keeps ahead, from the same 64-byte register group (two slots:
-// a 2-way pick, 8 selects per 256 bits instead of 12 per 128).
-constexpr uint32_t kSlotBits = 256;
-struct SlotFeed {
-    uint4 pre[4];   // payload slots 2 g and 2 g + 1 (one 64-byte group)
-    bool gin;       // the group lies inside the payload (no zero fill)
-    uint64_t bsl;   // payload slot of ring slot 0 of the first lap
-    uint32_t f;     // next slot to put (slots below f are in the ring)
-};
-
-HZ_DEV void slot_put(uint32_t* ring, uint32_t s, const uint4& x0, const uint4& x1) {
-    const uint32_t v[8] = {bswap32(x0.x), bswap32(x0.y), bswap32(x0.z), bswap32(x0.w),
-                           bswap32(x1.x), bswap32(x1.y), bswap32(x1.z), bswap32(x1.w)};
-    uint32_t* base = ring + (8u - 8u * s) * kRingRow;  // row 8 (1 - s): word 7 of the slot
-#pragma unroll
-    for (int j = 0; j < 8; ++j) base[(7 - j) * kRingRow] = v[j];
-    if (s) ring[16 * kRingRow] = v[7];
-}
-
-// Slots 0 and 1 of a ring whose bit 0 is payload word 8 * bsl, and the group holding slot 2.
-HZ_DEV void slot_feed_init(const WalkArgs& a, uint32_t* ring, SlotFeed& fd, uint64_t bsl) {
-    fd.bsl = bsl;
-    uint4 v[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) v[g] = walk_load(a, 8 * bsl + 4 * g);
-    const uint64_t gq = (bsl + 2) & ~1ull;
-    fd.gin = 8 * gq + 16 <= a.nwords;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) fd.pre[g] = walk_load(a, 8 * gq + 4 * g);
-    if ((bsl + 2) & 1) {
-        fd.pre[0] = fd.pre[2];
-        fd.pre[1] = fd.pre[3];
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) v[g] = walk_fix(a, 8 * bsl + 4 * g, v[g]);
-    slot_put(ring, 0, v[0], v[1]);
-    slot_put(ring, 1, v[2], v[3]);
-    fd.f = 2;
-}
-
-// Once per round: slot f goes into the ring when the walk at p no longer reads slot f - 2 (the window
-// reads words floor(p / 32) and up); the next group is loaded once the current one is in the ring.
-HZ_DEV void slot_feed(const WalkArgs& a, uint32_t* ring, SlotFeed& fd, uint32_t p) {
-    // pre[0..1] always holds slot f (the group's second slot moves down after the first is put: no
-    // select between slots, whose loads the compiler would fold into a dynamically indexed array)
-    if (fd.f <= (p >> 8) + 1) {
-        const uint64_t q = fd.bsl + fd.f;
-        uint4 x0 = fd.pre[0], x1 = fd.pre[1];
-        if (!fd.gin) {
-            x0 = walk_fix(a, 8 * q, x0);
-            x1 = walk_fix(a, 8 * q + 4, x1);
-        }
-        slot_put(ring, fd.f & 1, x0, x1);
-        ++fd.f;
-        if (q & 1) {  // the group is in the ring: the next one
-            const uint64_t w = 8 * (q + 1);
-            fd.gin = w + 16 <= a.nwords;
-            if (fd.gin) {
-                const uint4* src = reinterpret_cast<const uint4*>(a.words + w);
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) fd.pre[i] = src[i];
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; ++i) fd.pre[i] = walk_load(a, w + 4 * i);
-            }
-        } else {
-            fd.pre[0] = fd.pre[2];
-            fd.pre[1] = fd.pre[3];
-        }
-    }
-}
-
 // Length of the code at view bit P through the decode LUT in global memory (k_chain_walk<DEEP>: codes
 // longer than the escape table's m bits; rare, never on the path of codebooks within m bits).
 HZ_DEV uint32_t deep_len(const WalkArgs& a, uint64_t P) {
@@ -3705,8 +3630,7 @@ HZ_DEV uint32_t deep_len(const WalkArgs& a, uint64_t P) {
 template <bool DEEP>
 __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a, ChainArgs y) {
     // the byte length table (build_walk8: 2^16 windows at most, 64 KiB) at LDS address 0, the rings and
-    // record buffers after it
-    // (+ one zero word: the byte a lane past its limit reads)
+    // record buffers after it (+ one zero word: the byte a lane past its limit reads)
     __shared__ __attribute__((aligned(16))) uint32_t wtab[(1u << 16) / 4 + 4];
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (threadIdx.x == 0) wtab[(1u << 16) / 4] = 0;
@@ -3722,9 +3646,9 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     const uint64_t ce = cs + y.cbits < y.pend ? cs + y.cbits : y.pend;
     const uint64_t x0 = cs - (cs < a.lead ? cs : a.lead);  // lead-in: resynchronised by cs (mostly)
     const uint64_t P0 = y.start + a.bit_adj + x0;
-    SlotFeed fd;
-    slot_feed_init(a, ring, fd, P0 / kSlotBits);
-    uint32_t p = (uint32_t)(P0 - kSlotBits * fd.bsl);  // ring bit position of the walk (< 256)
+    SegFeed fd;
+    seg_feed_init(a, ring, fd, (P0 >> 7) - 1);  // one chunk before the walk (wraps to ~0 at the payload's start: zeros)
+    uint32_t p = (uint32_t)(P0 - 128 * fd.bch);    // ring bit position of the walk (>= 128)
     const uint64_t abs0 = y.start + x0 - p;        // absolute stream bit of ring position q: abs0 + q
     const uint32_t end = live ? p + (uint32_t)(ce - x0) : p;
     const uint32_t csr = p + (uint32_t)(cs - x0);  // the chain's first bit
@@ -3737,13 +3661,14 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     // nothing is stored (k_chain_tail decodes those codewords).
     // (the buffer write needs no capacity test: rows past the capacity are never stored)
     auto rec_put = [&](uint32_t rp) {
-        rbuf[rj & 7] = (uint16_t)((uint32_t)abs0 + rp);
+        const uint64_t ab = abs0 + rp;
+        rbuf[rj & 7] = (uint16_t)ab;
         const bool in = rj < y.cap;
         const bool row = in & ((rj & 7) == 7);
         const bool ck = (in & ((rj & (kChainRecs - 1)) == 0)) | (rj == y.cap);  // at the capacity: the first codeword past it
         if (row | ck) {  // one branch for both rare stores
             if (row) *reinterpret_cast<uint4*>(recp + (rj & ~7u)) = *reinterpret_cast<const uint4*>(rbuf);
-            if (ck) ckp[in ? rj / kChainRecs : y.bpc] = abs0 + rp;
+            if (ck) ckp[in ? rj / kChainRecs : y.bpc] = ab;
         }
         ++rj;
     };
@@ -3752,97 +3677,74 @@ __global__ __launch_bounds__(kChainWalkWaves * 64) void k_chain_walk(WalkArgs a,
     if (on && p < end) rec_put(p);
     uint32_t m = kRingM0 - p;  // the walk's position, descending (seg_window)
     const uint32_t mend = kRingM0 - end;
-    const uint32_t ml = (uint32_t)a.m;  // longest code: the most one step moves
-    // One half-round. FAST: every lane of the wave is at least 7 codes away from its limit (the chain's
-    // end, or its first bit during the lead-in) and the ring holds 6 codes past it, so no step needs a
-    // limit test (two VALU per step fewer) and nothing enters or leaves a chain; otherwise each step
-    // tests the limit and a lane past it reads the zero byte after the table.
-    auto half_round = [&](auto fastc, bool feed) {
-        constexpr bool FAST = decltype(fastc)::value;
-        const uint32_t fill = kSlotBits * fd.f - 31;  // a window at p < fill reads filled ring words
+    for (;;) {
+        if (!__any(m > mend)) break;
+        const uint32_t fill = 128 * fd.f - 96;  // filled data: both window words lie below p + 64
         const uint32_t mlim = kRingM0 - min(on ? end : csr, fill);  // a step needs m > mlim
-        // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
-        // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
-        // A step reads the code's length (0: an escape), or, past the limit, the zero byte after the
-        // table: a chain that reads 0 stays put and reads 0 again, so the advancing steps are a prefix
-        // with no park flags, and an escape's window is the half's last (no lane masks and no SALU
-        // per step: 281 vs 330 clocks per step in tools/microbench/mb_walk_step.hip).
-        constexpr int S = kSegSteps / kWalkHalves;
-        uint32_t q[S];
-        uint32_t na = 0, W = 0, e = 0;
-        bool ok = true;
-        // issue priority over the dependent steps and the escape gather's issue, normal for the
-        // record select, feed and stores (extract 21.14-21.45 -> 20.48-20.62 ms, A/B)
-        __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-        for (int t = 0; t < S; ++t) {
-            W = seg_window(ring, m);
-            if constexpr (FAST) {
-                e = lds8[W >> (32 - k8)];
-            } else {
+        for (int half = 0; half < kWalkHalves; ++half) {
+            // the half's codewords end at q[0 .. na - 1] (the advancing steps are a prefix: a chain
+            // that parks or reaches its limit stays put for the rest of the half), then at m for an escape
+            // A step reads the code's length (0: an escape), or, past the limit, the zero byte after the
+            // table: a chain that reads 0 stays put and reads 0 again, so the advancing steps are a prefix
+            // with no park flags, and an escape's window is the half's last (no lane masks and no SALU
+            // per step: 281 vs 330 clocks per step in tools/microbench/mb_walk_step.hip).
+            constexpr int S = kSegSteps / kWalkHalves;
+            uint32_t q[S];
+            uint32_t na = 0, W = 0, e = 0;
+            bool ok = false;
+            // issue priority over the dependent steps and the escape gather's issue, normal for the
+            // record select, feed and stores (extract 21.14-21.45 -> 20.48-20.62 ms, A/B)
+            __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+            for (int t = 0; t < S; ++t) {
                 ok = m > mlim;
+                W = seg_window(ring, m);
                 e = lds8[ok ? W >> (32 - k8) : 1u << 16];
+                HZ_WALK_FENCE();
+                m -= e;
+                na += e != 0u ? 1u : 0u;
+                q[t] = m;
             }
-            HZ_WALK_FENCE();
-            m -= e;
-            na += e != 0u ? 1u : 0u;
-            q[t] = m;
-        }
-        const bool pk = ok & (e == 0u);  // parked on an escape
-        const uint32_t nm = na + (pk ? 1u : 0u);
-        // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
-        // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
-        const uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
-        __builtin_amdgcn_s_setprio(0);
-        // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
-        // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
-        const uint32_t j1 = 8u - (cc & 7u);
-        const uint32_t jj = j1 <= na ? j1 : 0u;
-        static_assert(S <= 7, "q[jj - 1] for jj < 8");
-        uint32_t v[8];
-        v[0] = 0;
+            const bool pk = ok & (e == 0u);  // parked on an escape
+            const uint32_t nm = na + (pk ? 1u : 0u);
+            // the escape's gather by every lane (the others read byte 0): no branch, and its wait sits at
+            // the first use, behind the record select (11.2 vs 11.5 ms, A/B in one run)
+            uint32_t ev = a.esc[pk ? W >> (32 - a.m) : 0u];
+            __builtin_amdgcn_s_setprio(0);
+            // record of codeword 8 i: it starts where the half's codeword j1 ends (1-based): q[j1 - 1],
+            // or m after the escape when j1 is the escaped codeword (jj = 0); a three-level select
+            const uint32_t j1 = 8u - (cc & 7u);
+            const uint32_t jj = j1 <= na ? j1 : 0u;
+            static_assert(S <= 7, "q[jj - 1] for jj < 8");
+            uint32_t v[8];
+            v[0] = 0;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : 0u;
-        const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
-        const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
-        const uint32_t sel = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
-        m -= pk ? ev : 0u;
-        if constexpr (DEEP) {  // an escape the table leaves at 0: the code is longer than its m bits
-            const bool deep = pk & (ev == 0u);
-            if (__any(deep)) {
-                if (deep) m -= deep_len(a, abs0 + (kRingM0 - m) + a.bit_adj);
+            for (int t = 0; t < 7; ++t) v[t + 1] = t < S ? q[t < S ? t : 0] : 0u;
+            const bool b0 = jj & 1u, b1 = jj & 2u, b2 = jj & 4u;
+            const uint32_t a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
+            const uint32_t sel = b2 ? (b1 ? a3 : a2) : (b1 ? a1 : a0);
+            if constexpr (DEEP) {  // the escape table holds 0: a code longer than its m bits (decode LUT)
+                const bool deep = pk & (ev == 0u);
+                if (__any(deep)) {
+                    if (deep) ev = deep_len(a, abs0 + (kRingM0 - m) + a.bit_adj);
+                }
             }
-        }
-        // the round's feed right after its last escape wait and before the half's record stores: its
-        // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
-        // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
-        if (feed) slot_feed(a, ring, fd, kRingM0 - m);
-        const uint32_t pc = kRingM0 - m;
-        const uint32_t rm = jj ? sel : m;
-        const uint32_t rp = on ? kRingM0 - rm : pc;
-        if constexpr (FAST) {
-            const bool rec = on & (j1 <= nm);  // (FAST: every codeword of the half starts before the end)
-            cc = on ? cc + nm : 0u;
-            if (rec) rec_put(rp);
-        } else {
+            m -= pk ? ev : 0u;
+            // the round's feed right after its last escape wait and before the half's record stores: its
+            // wait on the group registers then waits for no fresh store (12.23 vs 12.60 ms at the round's
+            // end, 16 GiB Zipf, A/B in one run; without the record stores 11.67 ms)
+            if (half == kWalkHalves - 1) seg_feed(a, ring, fd, kRingM0 - m);
+            const uint32_t pc = kRingM0 - m;
+            const uint32_t rm = jj ? sel : m;
             // the lead-in's last step lands on the entry: the entry is the record, counting starts there
             const bool enter = !on & (pc >= csr);
+            const uint32_t rp = on ? kRingM0 - rm : pc;
             const bool rec = (on ? j1 <= nm : enter) & (rp < end);  // (a codeword starting at the end is the next chain's)
             ent = enter ? pc : ent;
             cc = on ? cc + nm : 0u;
             on |= enter;
             if (rec) rec_put(rp);
-        }
-    };
-    for (;;) {
-        if (!__any(m > mend)) break;
-#pragma unroll
-        for (int half = 0; half < kWalkHalves; ++half) {
-            // FAST when every lane has 7 codes to its limit and 6 codes of filled ring (wave-uniform)
-            const uint32_t pp = kRingM0 - m;
-            const bool fast = pp + 7 * ml < (on ? end : csr) && pp + 6 * ml < kSlotBits * fd.f - 31;
-            if (__all(fast)) half_round(std::true_type(), half == kWalkHalves - 1);
-            else half_round(std::false_type(), half == kWalkHalves - 1);
         }
     }
     p = kRingM0 - m;
@@ -4335,6 +4237,40 @@ static void fill_chain_dec_args(DecArgs& d, const Tables& t, const uint8_t* d_pa
     d.k = t.chain_k;
     d.level_bits = t.chain_level_bits;
     d.l2 = t.chain_l2;
+}
+
+// Payloads under 16 bytes (the walk's 16-byte loads need at least 4 words): one thread decodes the
+// codewords serially from start_bit, as Decompressor.cu:259-291 does, stream-ordered; a payload with
+// fewer than nsym codewords reports the end bit UINT64_MAX.
+__global__ __launch_bounds__(64) void k_decode_tiny(DecArgs a, uint64_t start, uint64_t payload_bits,
+                                                    unsigned long long* end) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    copy_lds_table(lds, a.lds_img, a.lds_words);
+    if (threadIdx.x) return;
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(a.out);
+    BitReader r;
+    br_init(r, a, start + a.bit_adj);
+    uint64_t p = start, i = 0;
+    for (; i < a.nsym && p <= payload_bits; ++i) {  // (every code >= 1 bit: at most 128 steps)
+        uint32_t sym;
+        const uint32_t L = br_next<DEC_LUT>(r, a, lds, sym);
+        if (L == 0) { atomicOr(a.err, 2u); break; }
+        p += L;
+        if (p <= payload_bits) out16[i] = (uint16_t)sym;
+    }
+    if (end) *end = i == a.nsym && p <= payload_bits ? p : ~0ull;
+}
+
+hipError_t chain_decode_tiny(const Tables& t, const uint8_t* d_payload, uint64_t payload_bytes, uint64_t start_bit,
+                             uint64_t nsym, uint8_t* d_out, unsigned long long* d_end, uint32_t* d_err, hipStream_t s) {
+    if (!seg_decode_supported(t)) return hipErrorInvalidValue;
+    DecArgs d;
+    fill_chain_dec_args(d, t, d_payload, payload_bytes, nsym);
+    d.starts = nullptr; d.subs = nullptr; d.out = d_out; d.err = d_err;
+    hipError_t e = ensure_lds_limit((const void*)k_decode_tiny, kLdsBytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_decode_tiny, dim3(1), dim3(64), t.chain_lds_bytes, s, d, start_bit, payload_bytes * 8, d_end);
+    return hipGetLastError();
 }
 
 // HZ_CAPTURE_DEBUG=1 (debug): the stream's capture status after each step of the launchers.

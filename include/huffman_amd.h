@@ -228,8 +228,8 @@ int hz_index_build(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes
  * stream-ordered). Every other codebook takes the chain path: DENSE codebooks
  * through a LUT built beside their tables, codes longer than 25 bits through
  * DEEP escapes (the walk resolves them in the decode LUT) and a serial record
- * decoder. Only payloads under 16 bytes go through hz_index_build + hz_decode
- * (that path synchronises). */
+ * decoder. Payloads under 16 bytes decode serially in one device thread (also
+ * stream-ordered). */
 int hz_decode_indexless(hz_ctx *ctx, const uint8_t *d_payload, uint64_t payload_bytes, uint64_t start_bit,
                         uint64_t nsym, uint8_t *d_out, uint64_t *d_end_bit);
 

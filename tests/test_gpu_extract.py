@@ -196,8 +196,9 @@ def test_indexless_skewed_rounds(codec):
 def test_indexless_graph_capture(codec):
     """hz_decode_indexless is stream-ordered (no host synchronisation inside, fix-ups iterated on the
     device): captured into a HIP graph on the context's stream and replayed, it decodes bit-exact. A
-    host sync inside the call would break the capture. (The stream's longest code is 24 bits: longer
-    codes take the index-building path, which sizes its scratch on the host.)"""
+    host sync inside the call would break the capture. (Every codebook takes a stream-ordered path:
+    test_indexless_dense_codebook_256mib_chain_path, test_indexless_31_bit_codes_chain_path,
+    test_indexless_tiny_payload_captured.)"""
     import torch
     from huffman_amd import index_starts
     n = (24 << 20) + 6
@@ -348,3 +349,22 @@ def test_indexless_31_bit_codes_chain_path(codec, shift):
         codec.sync()
         eager, replay, _ = _captured_indexless(codec, x, plan, payload, nsym)
         assert eager and replay
+
+
+@pytest.mark.parametrize("n", [3, 9, 17])
+def test_indexless_tiny_payload_captured(codec, n):
+    """Payloads under 16 bytes (too short for the walk): one device thread decodes them serially --
+    stream-ordered too (captured in a HIP graph and replayed), bit-exact, end bit equal to pack's."""
+    from huffman_amd import index_starts
+    import torch
+    x = torch.tensor(list(range(7, 7 + n)), dtype=torch.uint8, device="cuda")
+    nsym = n // 2
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    assert payload.numel() < 16 + 16
+    end_pack = int(index_starts(index.cpu().numpy(), nsym)[-1])
+    pbytes = (plan.start_bit + plan.payload_bits + 7) // 8
+    assert pbytes < 16
+    payload = payload[:pbytes]
+    eager, replay, end_bit = _captured_indexless(codec, x, plan, payload, nsym)
+    assert eager and replay and end_bit == end_pack
