@@ -49,7 +49,7 @@ void radix_sort_u64(uint64_t* k, uint64_t* tmp, uint32_t n, int lo) {
 struct CbScratch {
     std::unique_ptr<uint64_t[]> keys{new uint64_t[HZ_NSYM]}, tmp{new uint64_t[HZ_NSYM]};
     std::unique_ptr<uint64_t[]> f{new uint64_t[2 * HZ_NSYM]}, cw{new uint64_t[2 * HZ_NSYM]};
-    std::unique_ptr<uint32_t[]> lc{new uint32_t[2 * HZ_NSYM]}, rc{new uint32_t[2 * HZ_NSYM]};
+    std::unique_ptr<uint32_t[]> up{new uint32_t[2 * HZ_NSYM]};
     std::unique_ptr<uint8_t[]> dep{new uint8_t[2 * HZ_NSYM]};
 };
 
@@ -118,30 +118,33 @@ extern "C" int hz_codebook_build(const uint64_t* hist, hz_codebook* cb) {
         cb->max_len = cb->min_len = 1;
         return HZ_OK;
     }
+    // Merge with two FIFO queues (leaves by (count, symbol), then merged nodes in creation
+    // order); the leaf head wins a tie. Each node records its parent and the branch bit it
+    // hangs on, and the codes are then assigned top-down in reverse creation order.
     const uint32_t nn = 2 * U - 1;
     uint64_t* f = sc.f.get();
-    uint32_t *lc = sc.lc.get(), *rc = sc.rc.get();
+    uint32_t* up = sc.up.get();  // parent << 1 | branch bit ('1' for the first child)
     for (uint32_t i = 0; i < U; ++i) f[i] = keys[i] >> 16;
     uint32_t li = 0, qi = U;
     for (uint32_t nx = U; nx < nn; ++nx) {
-        uint32_t pick[2];
-        for (int j = 0; j < 2; ++j) {
-            if (li < U && (qi >= nx || f[li] <= f[qi])) pick[j] = li++;  // leaf wins ties (older)
-            else pick[j] = qi++;
-        }
-        f[nx] = f[pick[0]] + f[pick[1]];
-        lc[nx] = pick[0];
-        rc[nx] = pick[1];
+        auto take = [&]() -> uint32_t {
+            const bool leaf = li < U && (qi == nx || f[li] <= f[qi]);
+            return leaf ? li++ : qi++;
+        };
+        const uint32_t a = take(), b = take();
+        f[nx] = f[a] + f[b];
+        up[a] = nx << 1 | 1u;
+        up[b] = nx << 1;
     }
     uint8_t* dep = sc.dep.get();
     uint64_t* cw = sc.cw.get();
     dep[nn - 1] = 0;
     cw[nn - 1] = 0;
-    for (uint32_t v = nn - 1; v >= U; --v) {
-        const uint32_t d = dep[v] + 1u;
+    for (uint32_t i = nn - 1; i-- > 0;) {  // a parent is always created after its children
+        const uint32_t p = up[i] >> 1, d = dep[p] + 1u;
         if (d > HZ_MAXLEN) return HZ_ETOOLONG;
-        dep[lc[v]] = (uint8_t)d; cw[lc[v]] = (cw[v] << 1) | 1u;  // first child '1'
-        dep[rc[v]] = (uint8_t)d; cw[rc[v]] = cw[v] << 1;         // second child '0'
+        dep[i] = (uint8_t)d;
+        cw[i] = cw[p] << 1 | (up[i] & 1u);
     }
     uint32_t mx = 0, mn = 255;
     for (uint32_t i = 0; i < U; ++i) {
