@@ -589,6 +589,7 @@ int build_dec_lut(const hz_codebook* cb, std::vector<uint32_t>& img, std::vector
     const uint64_t est_bits = (uint64_t)(kbits * kBlockSyms * 1.0625) + 256;
     add_lds_level(cb, img, l2, K1,
                   (long)(kLdsBytes / 4) - (long)img.size() - (long)kDecMaxWaves * (long)dec_slot_words(est_bits, (int)cb->max_len) - 64);
+    while (img.size() < kDecMinLdsWords) img.push_back(leaf(1, 0));  // unused words: the slots start past LDS bit 1024
     return HZ_OK;
 }
 

@@ -130,6 +130,11 @@ __host__ __device__ inline uint32_t lut_leaf_entry(uint32_t L, uint32_t sym) {
 __host__ __device__ inline uint32_t lut_leaf_len(uint32_t e) { return (e >> 24) & 63u; }
 __host__ __device__ inline uint32_t lut_leaf_sym(uint32_t e) { return (e >> 8) & 0xffffu; }
 constexpr int kDecMaxWaves = 16;
+// Smallest LDS image of a LUT (words): the pipelined decoders' staging slots follow the table, and their
+// window addresses carry a bias of 128 bits per step taken (up to 7 * 128 below a lane's true bit address,
+// dec_pipe_ldsn's adj): the lowest slot must start at LDS bit 1024 or more so the biased address never
+// wraps below 0. (A DENSE codebook's chain LUT has 2^max_len entries: 4 words for 2-bit codes.)
+constexpr uint32_t kDecMinLdsWords = 32;
 // Index walker (k_idx_walk): one chain per lane, kWalkWaves waves per CU; per
 // chain an LDS ring of 4 payload chunks (16 B) and kWalkMarkChunks mark chunks,
 // beside a 4-bit code-length table of the top kWalkK window bits.

@@ -2422,6 +2422,7 @@ static hipError_t run_decode(const DecArgs& a, uint64_t payload_bits, int ncu, h
     uint32_t est = dec_slot_words(avg + avg / 16 + 256, a.max_len);
     est = est < worst ? est : worst;
     const uint32_t table = a.lds_words;
+    if (MODE == DEC_LUT && PIPE == 2 && table < kDecMinLdsWords) return hipErrorInvalidValue;  // biased windows
     int best_w = 0, best_g = 1;
     for (int g = 1; g <= 2; ++g) {
         const uint32_t room = kLdsBytes / 4 / (uint32_t)g;
@@ -4458,7 +4459,7 @@ hipError_t chain_decode(ChainState* st, const Tables& t, uint64_t nsym, uint8_t*
         uint32_t est = dec_slot_words(avg + avg / 16 + 256, d.max_len);
         est = est < worst ? est : worst;
         const uint32_t table = d.lds_words;
-        if (table + worst > kLdsBytes / 4) return hipErrorInvalidValue;
+        if (table < kDecMinLdsWords || table + worst > kLdsBytes / 4) return hipErrorInvalidValue;  // (biased windows)
         uint32_t nslot = (kLdsBytes / 4 - table) / est;
         nslot = nslot > 2 * kDecPipe2Threads / 64 ? 2 * kDecPipe2Threads / 64 : nslot;
         nslot &= ~1u;

@@ -190,6 +190,11 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
             g.manual_seed(5)
             s = torch.randint(0, 3000, (n_total // 2,), dtype=torch.int32, device=dev, generator=g)
             x = (s * 19 + 7).to(torch.int16).view(torch.uint8)
+        elif kind == "tiny3":  # three symbols, codes of 1-2 bits: a 4-entry chain LUT (padded LDS image)
+            import numpy as np
+            rng = np.random.default_rng(9)
+            s = rng.choice(np.array([5, 300, 40000], dtype="<u2"), size=n_total // 2, p=[0.6, 0.3, 0.1])
+            x = torch.from_numpy(s.view(np.uint8).copy()).to(dev)
         else:  # "deep": Fibonacci counts, codes of up to 31 bits (DEEP escapes, serial records)
             from test_gpu_extract import _fib_stream
             x = torch.from_numpy(_fib_stream(2)).to(dev)
@@ -242,10 +247,12 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world,n_total,lead,kind", [(2, (8 << 20) + 2, None, "zipf"), (3, (24 << 20) + 6, None, "zipf"),
                                                      (8, (64 << 20) + 2, None, "zipf"), (4, (16 << 20) + 2, 0, "zipf"),
-                                                     (3, (64 << 20) + 2, None, "dense"), (2, 0, None, "deep")])
+                                                     (3, (64 << 20) + 2, None, "dense"), (2, 0, None, "deep"),
+                                                     (3, (24 << 20) + 2, None, "tiny3")])
 def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead, kind):
     """One index-less stream split over `world` ranks on one GPU: Zipf (LUT tables), a DEC_DENSE codebook
-    (hz_indexless_scan used to refuse it) and 31-bit codes (DEEP escapes, serial records)."""
+    (hz_indexless_scan used to refuse it), 31-bit codes (DEEP escapes, serial records) and a three-symbol
+    alphabet (1-2 bit codes)."""
     mp.start_processes(_split_worker, args=(world, _free_port(), n_total, lead, str(tmp_path), kind), nprocs=world,
                        join=True, start_method="spawn")
     for r in range(world):

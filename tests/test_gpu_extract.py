@@ -23,6 +23,12 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 @pytest.fixture(scope="module")
+def hz(built_lib):
+    import huffman_amd
+    return huffman_amd
+
+
+@pytest.fixture(scope="module")
 def codec(built_lib):
     from huffman_amd.pipeline import StreamCodec
     return StreamCodec(0)
@@ -62,8 +68,7 @@ def test_indexless_zipf(codec, n, shift):
 
 @pytest.mark.parametrize("name", ["dense8", "short", "mid20", "long24"])
 def test_indexless_table_shapes(codec, name):
-    """Every table shape: the two-pass decoder where it applies (LUT tables, codes <= 22 bits),
-    hz_index_build + hz_decode otherwise (DENSE tables, codes > 22 bits): the same output."""
+    """Every table shape (DENSE, LUT with short, mid and 24-bit codes) through the chain path."""
     import torch
     from test_gpu import _shape_stream
     x = torch.from_numpy(_shape_stream(name)).cuda()
@@ -368,3 +373,59 @@ def test_indexless_tiny_payload_captured(codec, n):
     payload = payload[:pbytes]
     eager, replay, end_bit = _captured_indexless(codec, x, plan, payload, nsym)
     assert eager and replay and end_bit == end_pack
+
+
+def _random_stream(rng):
+    """A seeded random symbol stream: alphabet size, distribution shape (power law, geometric,
+    spiky Dirichlet or flat), symbol values and byte length (odd or even) all drawn at random."""
+    U = int(rng.choice([1, 2, 3, 5, 17, 255, 4096, 40000, 65536]))
+    kind = int(rng.integers(0, 4))
+    r = np.arange(1, U + 1, dtype=np.float64)
+    if kind == 0:
+        p = r ** -rng.uniform(0.5, 2.5)
+    elif kind == 1:
+        p = rng.uniform(0.5, 0.999) ** r
+    elif kind == 2:
+        p = rng.dirichlet(np.full(U, 0.05)) + 1e-12
+    else:
+        p = np.ones(U)
+    p /= p.sum()
+    n = int(rng.integers(1, 3 << 20))
+    vals = rng.permutation(65536)[:U].astype(np.uint16)
+    sym = vals[rng.choice(U, size=(n + 1) // 2, p=p)]
+    return sym.astype("<u2").view(np.uint8)[:n].copy(), f"U={U} kind={kind} n={n}"
+
+
+def test_indexless_random_streams(hz, codec):
+    """32 seeded random streams (alphabet sizes 1..65 536, power-law, geometric, spiky and flat
+    counts, 1 byte to 3 MiB): the product's file equals the oracle's, the CPU oracle decodes it,
+    the file decodes back through hz_decode_host (index-less), and the device payload decodes
+    index-less from a random byte offset with the end bit of pack's own index."""
+    import torch
+    rng = np.random.default_rng(20261018)
+    for case in range(32):
+        data, what = _random_stream(rng)
+        blob = hz.encode(data.tobytes())
+        assert blob == oracle_lib.encode(data), what
+        assert oracle_lib.decode(blob) == data.tobytes(), what
+        assert hz.decode(blob) == data.tobytes(), what
+        if data.size >= 2:
+            ok, end_ok = _check(codec, torch.from_numpy(data).cuda(), int(rng.integers(0, 48)))
+            assert ok and end_ok, what
+
+
+def test_random_streams_through_the_file_streams(hz, tmp_path):
+    """12 more seeded random streams through the streaming CLIs' paths: hz_archive_stream in small
+    chunks writes the oracle's file, and hz_extract_stream in small payload windows (each window an
+    index-less part, the next window's entry from the last) restores the input."""
+    rng = np.random.default_rng(7)
+    for case in range(12):
+        data, what = _random_stream(rng)
+        chunk, window = int(rng.integers(1, 64)) * 4096, int(rng.integers(1, 17)) * 4096
+        src, arc, out = tmp_path / "in", tmp_path / "in.compressed", tmp_path / "out"
+        src.write_bytes(data.tobytes())
+        hz.archive_stream(src, arc, chunk_bytes=chunk)
+        blob = arc.read_bytes()
+        assert blob == oracle_lib.encode(data), what
+        hz.extract_stream(arc, out, chunk_bytes=window)
+        assert out.read_bytes() == data.tobytes(), what + f" window={window}"
