@@ -190,6 +190,11 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
             g.manual_seed(5)
             s = torch.randint(0, 3000, (n_total // 2,), dtype=torch.int32, device=dev, generator=g)
             x = (s * 19 + 7).to(torch.int16).view(torch.uint8)
+        elif kind.startswith("random:"):  # test_gpu_extract._random_stream with this seed
+            import numpy as np
+            from test_gpu_extract import _random_stream
+            data, _ = _random_stream(np.random.default_rng(int(kind.split(":")[1])))
+            x = torch.from_numpy(data).to(dev)
         elif kind == "tiny3":  # three symbols, codes of 1-2 bits: a 4-entry chain LUT (padded LDS image)
             import numpy as np
             rng = np.random.default_rng(9)
@@ -248,7 +253,9 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
 @pytest.mark.parametrize("world,n_total,lead,kind", [(2, (8 << 20) + 2, None, "zipf"), (3, (24 << 20) + 6, None, "zipf"),
                                                      (8, (64 << 20) + 2, None, "zipf"), (4, (16 << 20) + 2, 0, "zipf"),
                                                      (3, (64 << 20) + 2, None, "dense"), (2, 0, None, "deep"),
-                                                     (3, (24 << 20) + 2, None, "tiny3")])
+                                                     (3, (24 << 20) + 2, None, "tiny3"), (4, 0, None, "random:1"),
+                                                     (3, 0, None, "random:9"), (5, 0, None, "random:11"),
+                                                     (2, 0, None, "random:7")])
 def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead, kind):
     """One index-less stream split over `world` ranks on one GPU: Zipf (LUT tables), a DEC_DENSE codebook
     (hz_indexless_scan used to refuse it), 31-bit codes (DEEP escapes, serial records) and a three-symbol

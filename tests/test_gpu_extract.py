@@ -399,8 +399,8 @@ def _random_stream(rng):
 def test_indexless_random_streams(hz, codec):
     """32 seeded random streams (alphabet sizes 1..65 536, power-law, geometric, spiky and flat
     counts, 1 byte to 3 MiB): the product's file equals the oracle's, the CPU oracle decodes it,
-    the file decodes back through hz_decode_host (index-less), and the device payload decodes
-    index-less from a random byte offset with the end bit of pack's own index."""
+    the file decodes back through hz_decode_host (index-less), the device payload decodes index-less
+    from a random byte offset with the end bit of pack's own index, and through that index (k_decode)."""
     import torch
     rng = np.random.default_rng(20261018)
     for case in range(32):
@@ -410,8 +410,16 @@ def test_indexless_random_streams(hz, codec):
         assert oracle_lib.decode(blob) == data.tobytes(), what
         assert hz.decode(blob) == data.tobytes(), what
         if data.size >= 2:
-            ok, end_ok = _check(codec, torch.from_numpy(data).cuda(), int(rng.integers(0, 48)))
+            x = torch.from_numpy(data).cuda()
+            ok, end_ok = _check(codec, x, int(rng.integers(0, 48)))
             assert ok and end_ok, what
+            # and the headline path: pack's block index, k_decode
+            nsym = data.size // 2
+            plan, payload, index = codec.encode(x)
+            out = torch.empty(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+            codec.dev.decode(payload.data_ptr(), payload.numel(), nsym, index.data_ptr(), out.data_ptr())
+            codec.sync()
+            assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what
 
 
 def test_random_streams_through_the_file_streams(hz, tmp_path):
