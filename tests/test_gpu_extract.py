@@ -400,7 +400,8 @@ def test_indexless_random_streams(hz, codec):
     """32 seeded random streams (alphabet sizes 1..65 536, power-law, geometric, spiky and flat
     counts, 1 byte to 3 MiB): the product's file equals the oracle's, the CPU oracle decodes it,
     the file decodes back through hz_decode_host (index-less), the device payload decodes index-less
-    from a random byte offset with the end bit of pack's own index, and through that index (k_decode)."""
+    from a random byte offset with the end bit of pack's own index, and through that index (k_decode);
+    hz_index_build rebuilds that index from the payload alone."""
     import torch
     rng = np.random.default_rng(20261018)
     for case in range(32):
@@ -420,6 +421,13 @@ def test_indexless_random_streams(hz, codec):
             codec.dev.decode(payload.data_ptr(), payload.numel(), nsym, index.data_ptr(), out.data_ptr())
             codec.sync()
             assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what
+            # the self-synchronising index builder rebuilds pack's index from the payload alone
+            from huffman_amd import index_bytes
+            rebuilt = torch.full_like(index, -1)
+            codec.dev.index_build(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, rebuilt.data_ptr())
+            codec.sync()
+            nb = index_bytes(nsym)
+            assert np.array_equal(index.cpu().numpy().view(np.uint8)[:nb], rebuilt.cpu().numpy().view(np.uint8)[:nb]), what
 
 
 def test_random_streams_through_the_file_streams(hz, tmp_path):
@@ -437,3 +445,29 @@ def test_random_streams_through_the_file_streams(hz, tmp_path):
         assert blob == oracle_lib.encode(data), what
         hz.extract_stream(arc, out, chunk_bytes=window)
         assert out.read_bytes() == data.tobytes(), what + f" window={window}"
+
+
+@pytest.mark.parametrize("seed,U,kind", [(1, 3, 0), (2, 17, 1), (3, 300, 2), (4, 65536, 1)])
+def test_random_streams_range_plan(codec, seed, U, kind):
+    """256 MiB + 1 random streams (the range-plan encoder: histogram snapshots, dot products, pack
+    over ranges) with small and large alphabets: the file equals the oracle's, pack's index decodes
+    it (k_decode) and the bare payload decodes index-less (chain path) with pack's end bit."""
+    import torch
+    rng = np.random.default_rng(seed)
+    n = (256 << 20) + 1
+    r = np.arange(1, U + 1, dtype=np.float64)
+    p = [r ** -rng.uniform(0.5, 2.5), rng.uniform(0.5, 0.999) ** r, rng.dirichlet(np.full(U, 0.05)) + 1e-12][kind]
+    cdf = np.cumsum(p / p.sum())
+    idx = np.minimum(np.searchsorted(cdf, rng.random((n + 1) // 2)), U - 1)
+    host = rng.permutation(65536)[:U].astype("<u2")[idx].view(np.uint8)[:n].copy()
+    x = torch.from_numpy(host).cuda()
+    plan, payload, index = codec.encode(x)
+    codec.sync()
+    assert codec.file_image(plan, payload) == oracle_lib.encode(host)
+    nsym = n // 2
+    out = torch.empty(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+    codec.decode(payload, nsym, index, out)
+    codec.sync()
+    assert torch.equal(out[:2 * nsym], x[:2 * nsym])
+    ok, end_ok = _check(codec, x, 3)
+    assert ok and end_ok
