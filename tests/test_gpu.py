@@ -720,3 +720,18 @@ def test_fixed16_block_kernels_any_start(hz, start_bit):
     assert np.array_equal(got[:(start_bit % 8 + 16 * nsym) // 8], ref[:(start_bit % 8 + 16 * nsym) // 8])
     assert np.array_equal(dec[:data.size].cpu().numpy(), data)
     dev.close()
+
+
+@pytest.mark.parametrize("name", ["romeo.txt", "zipf_odd"])
+def test_integration_example_archives_like_the_oracle(hz, tmp_path, name):
+    """INTEGRATION.md §2's C++ binding, compiled against the C ABI (tests/test_host.py), run on the
+    device: the file it writes equals the oracle's (romeo.txt and a 3 MiB + 1 Zipf file)."""
+    import subprocess
+    from test_host import build_integration_example
+    exe = build_integration_example(tmp_path)
+    data = read(name) if name == "romeo.txt" else oracle_lib.generate((3 << 20) + 1, kind=1, seed=4).tobytes()
+    src, dst = tmp_path / "in", tmp_path / "out"
+    src.write_bytes(data)
+    r = subprocess.run([str(exe), str(src), str(dst)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert dst.read_bytes() == oracle_lib.encode(data)

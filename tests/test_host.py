@@ -125,3 +125,45 @@ def test_index_geometry(built_lib):
     assert built_lib.hz_index_bytes(1) == 8 * 3 + 512
     assert built_lib.hz_index_bytes(2049) == 8 * 4 + 2 * 512
     assert built_lib.hz_index_bytes(1 << 33) == 8 * ((1 << 22) + 2) + 512 * (1 << 22)
+
+
+def build_integration_example(tmp_path):
+    """INTEGRATION.md §2's C++ binding (archive_buffer) with a main that archives argv[1] into argv[2],
+    compiled with g++ against include/huffman_amd.h and linked with the library: the binding a
+    maintainer would add is valid C++ against the ABI as declared."""
+    import subprocess
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        code = re.findall(r"```cpp\n(.*?)```", f.read(), re.S)[0]
+    main = r'''
+#include <cstdio>
+int main(int argc, char** argv) {
+    if (argc != 3) return 2;
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    std::vector<uint8_t> in;
+    for (int c; (c = fgetc(f)) != EOF;) in.push_back((uint8_t)c);
+    fclose(f);
+    std::vector<uint8_t> file;
+    const int st = archive_buffer(in.data(), in.size(), file);
+    if (st != HZ_OK) { fprintf(stderr, "status %d\n", st); return 1; }
+    FILE* o = fopen(argv[2], "wb");
+    fwrite(file.data(), 1, file.size(), o);
+    fclose(o);
+    return 0;
+}
+'''
+    src = tmp_path / "archive_amd.cpp"
+    src.write_text(code + main)
+    exe = tmp_path / "archive_amd"
+    lib_dir = os.path.join(ROOT, "huffman_amd", "lib")
+    r = subprocess.run(["g++", "-std=c++17", "-w", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                        "-I" + os.path.join(ROOT, "include"), str(src), "-L" + lib_dir, "-lhuffman_amd",
+                        "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath," + lib_dir, "-o", str(exe)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return exe
+
+
+def test_integration_example_compiles_and_links(built_lib, tmp_path):
+    exe = build_integration_example(tmp_path)
+    assert os.access(exe, os.X_OK)
