@@ -195,6 +195,11 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
             from test_gpu_extract import _random_stream
             data, _ = _random_stream(np.random.default_rng(int(kind.split(":")[1])))
             x = torch.from_numpy(data).to(dev)
+        elif kind == "skew90":  # 90 % one symbol (~1.1 bits per codeword against a ~1.5-bit Kraft estimate)
+            import numpy as np
+            rng = np.random.default_rng(5)
+            s = np.where(rng.random(n_total // 2) < 0.9, 0, rng.integers(1, 301, n_total // 2)).astype("<u2")
+            x = torch.from_numpy(s.view(np.uint8).copy()).to(dev)
         elif kind == "tiny3":  # three symbols, codes of 1-2 bits: a 4-entry chain LUT (padded LDS image)
             import numpy as np
             rng = np.random.default_rng(9)
@@ -253,7 +258,8 @@ def _split_worker(rank, world, port, n_total, lead, result_dir, kind="zipf"):
 @pytest.mark.parametrize("world,n_total,lead,kind", [(2, (8 << 20) + 2, None, "zipf"), (3, (24 << 20) + 6, None, "zipf"),
                                                      (8, (64 << 20) + 2, None, "zipf"), (4, (16 << 20) + 2, 0, "zipf"),
                                                      (3, (64 << 20) + 2, None, "dense"), (2, 0, None, "deep"),
-                                                     (3, (24 << 20) + 2, None, "tiny3"), (4, 0, None, "random:1"),
+                                                     (3, (24 << 20) + 2, None, "tiny3"), (3, (12 << 20) + 2, None, "skew90"),
+                                                     (4, 0, None, "random:1"),
                                                      (3, 0, None, "random:9"), (5, 0, None, "random:11"),
                                                      (2, 0, None, "random:7")])
 def test_indexless_split_over_ranks_on_device(tmp_path, world, n_total, lead, kind):
