@@ -71,6 +71,7 @@ struct Staging {
     uint8_t* p = nullptr;
     size_t cap = 0, used = 0;
     hipEvent_t done = nullptr;
+    std::vector<StageSeg> pend;  // staged, not yet copied (staging_flush)
 };
 
 struct hz_ctx {
@@ -89,7 +90,11 @@ struct hz_ctx {
     double thr_alpha = -1.0;
     hipEvent_t ev[5][2] = {};
     bool ev_used[5] = {false, false, false, false, false};
-    Staging stage_enc, stage_dec;
+    // encode tables, decode tables, and the index-less decoder's tables (walk length and escape tables,
+    // a DENSE codebook's chain LUT): built with the decode tables, copied by the first call that needs
+    // them (hz_decode_indexless, hz_indexless_scan, hz_index_build) -- a decode with a block index never
+    // uploads them
+    Staging stage_enc, stage_dec, stage_walk;
     size_t cap_enc_lds = 0, cap_enc_esc = 0, cap_enc_wide = 0, cap_len8 = 0, cap_lenpair = 0, cap_dec_lds = 0,
            cap_dec_l2 = 0, cap_walk_lds = 0, cap_walk_esc = 0, cap_walk8 = 0, cap_chain_lds = 0, cap_chain_l2 = 0,
            cap_chain_esc = 0;
@@ -171,7 +176,7 @@ extern "C" int hz_ctx_destroy(hz_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_tables(c->t);
-    for (Staging* st : {&c->stage_enc, &c->stage_dec}) {
+    for (Staging* st : {&c->stage_enc, &c->stage_dec, &c->stage_walk}) {
         if (st->done) (void)hipEventDestroy(st->done);
         (void)hipHostFree(st->p);
     }
@@ -299,15 +304,28 @@ extern "C" int hz_header_parse_device(hz_ctx* c, const uint8_t* d_file, uint64_t
 }
 
 // Device tables live in per-context buffers that only grow; host images are
-// staged in pinned memory and copied asynchronously on the context stream, so
-// an upload never synchronises and the decode tables can be built on the host
-// while the pack kernel runs (bench step: upload_encode -> pack ->
-// upload_decode -> decode). Stream order keeps in-flight kernels on the
+// staged in pinned memory and copied asynchronously on the context stream (one
+// scatter kernel per set), so an upload never synchronises and the decode tables
+// can be built on the host while the pack kernel runs (bench step: upload_encode
+// -> pack -> upload_decode -> decode). Stream order keeps in-flight kernels on the
 // previous tables; a staging buffer is reused only after its last copy's event.
 static int staging_begin(Staging& st) {
     if (!st.done) HZ_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
     else HZ_TRY(hipEventSynchronize(st.done));
     st.used = 0;
+    st.pend.clear();  // (a set never flushed is dropped)
+    return HZ_OK;
+}
+
+// The staged segments to their tables, stream-ordered. Under stream capture the copy is captured and
+// the segments stay pending, so a later uncaptured call copies them again.
+static int staging_flush(hz_ctx* c, Staging& st) {
+    if (st.pend.empty()) return HZ_OK;
+    HZ_TRY(stage_scatter(st.p, st.pend.data(), (int)st.pend.size(), c->stream));
+    HZ_TRY(hipEventRecord(st.done, c->stream));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HZ_TRY(hipStreamIsCapturing(c->stream, &cs));
+    if (cs == hipStreamCaptureStatusNone) st.pend.clear();
     return HZ_OK;
 }
 
@@ -322,18 +340,19 @@ static int stage_copy(hz_ctx* c, Staging& st, T** dptr, size_t* dcap, const std:
         *dcap = bytes;
     }
     if (st.used + bytes > st.cap) {
-        // grow (rare): earlier copies of this batch must land first
-        HZ_TRY(hipStreamSynchronize(c->stream));
+        // grow (rare): the segments staged so far move along (no copy of this staging is in flight:
+        // staging_begin waited for the last one)
         uint8_t* np = nullptr;
         const size_t ncap = std::max(st.cap * 2, st.used + bytes + (1u << 20));
         HZ_TRY(hipHostMalloc(&np, ncap, hipHostMallocDefault));
+        if (st.used) memcpy(np, st.p, st.used);
         (void)hipHostFree(st.p);
         st.p = np;
         st.cap = ncap;
-        st.used = 0;
     }
+    static_assert(sizeof(T) % 4 == 0, "tables of 4-byte words (k_stage_scatter)");
     memcpy(st.p + st.used, v.data(), bytes);
-    HZ_TRY(hipMemcpyAsync(*dptr, st.p + st.used, bytes, hipMemcpyHostToDevice, c->stream));
+    if (bytes) st.pend.push_back(StageSeg{(void*)*dptr, (uint64_t)st.used, (uint64_t)bytes});
     st.used += (bytes + 255) & ~(size_t)255;
     return HZ_OK;
 }
@@ -381,7 +400,7 @@ static int hz_codebook_upload_encode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (mode != ENC_FIXED16 &&
         (rc = stage_copy(c, c->stage_enc, &t.d_lenpair, &c->cap_lenpair, build_lenpair(cb))))
         return rc;
-    HZ_TRY(hipEventRecord(c->stage_enc.done, c->stream));
+    if ((rc = staging_flush(c, c->stage_enc))) return rc;
     t.enc_mode = mode;
     return HZ_OK;
 }
@@ -420,6 +439,9 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (l2.empty()) l2.push_back(lut_leaf_entry(1, 0));
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
+    if ((rc = staging_flush(c, c->stage_dec))) return rc;
+    // the index-less tables, staged now and copied by the first call that needs them (flush_walk)
+    if ((rc = staging_begin(c->stage_walk))) return rc;
     // the index walker's length tables (FIXED16 streams have an arithmetic index)
     t.walk_lds_bytes = 0;
     t.walk8_bytes = 0;
@@ -427,9 +449,9 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (mode != DEC_FIXED16 && cb->max_len >= 1 && cb->max_len <= kWalkMaxLen) {
         build_walk_len(cb, wimg, wesc, t.walk_k, t.walk_m, t.walk_bias);
         if (wimg.size() * 4 <= (1u << kWalkK) / 2) {  // k_idx_walk's static table
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
+            if ((rc = stage_copy(c, c->stage_walk, &t.d_walk_lds, &c->cap_walk_lds, wimg))) return rc;
             if (wesc.empty()) wesc.push_back(0x01010101u);
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;
+            if ((rc = stage_copy(c, c->stage_walk, &t.d_walk_esc, &c->cap_walk_esc, wesc))) return rc;
             t.walk_lds_bytes = (uint32_t)(wimg.size() * 4);
         }
     }
@@ -438,7 +460,7 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     if (mode != DEC_FIXED16 && cb->max_len >= 1) {
         std::vector<uint32_t> w8;
         build_walk8(cb, w8, t.walk8_k);
-        if ((rc = stage_copy(c, c->stage_dec, &t.d_walk8, &c->cap_walk8, w8))) return rc;
+        if ((rc = stage_copy(c, c->stage_walk, &t.d_walk8, &c->cap_walk8, w8))) return rc;
         t.walk8_bytes = (uint32_t)(w8.size() * 4);
         if (t.walk_lds_bytes > 0) {
             t.chain_esc = reinterpret_cast<const uint8_t*>(t.d_walk_esc);
@@ -446,7 +468,7 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
         } else {
             std::vector<uint32_t> cesc;
             build_chain_esc(cb, cesc, t.chain_esc_m);
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_esc, &c->cap_chain_esc, cesc))) return rc;
+            if ((rc = stage_copy(c, c->stage_walk, &t.d_chain_esc, &c->cap_chain_esc, cesc))) return rc;
             t.chain_esc = reinterpret_cast<const uint8_t*>(t.d_chain_esc);
         }
         if (mode == DEC_LUT) {
@@ -460,14 +482,13 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
             if ((rc = build_dec_lut(cb, cimg, cl2, t.chain_k, t.chain_level_bits))) return rc;
             while (cimg.size() % 4) cimg.push_back(0);
             if (cl2.empty()) cl2.push_back(lut_leaf_entry(1, 0));
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_lds, &c->cap_chain_lds, cimg))) return rc;
-            if ((rc = stage_copy(c, c->stage_dec, &t.d_chain_l2, &c->cap_chain_l2, cl2))) return rc;
+            if ((rc = stage_copy(c, c->stage_walk, &t.d_chain_lds, &c->cap_chain_lds, cimg))) return rc;
+            if ((rc = stage_copy(c, c->stage_walk, &t.d_chain_l2, &c->cap_chain_l2, cl2))) return rc;
             t.chain_lds = t.d_chain_lds;
             t.chain_l2 = t.d_chain_l2;
             t.chain_lds_bytes = (uint32_t)(cimg.size() * 4);
         }
     }
-    HZ_TRY(hipEventRecord(c->stage_dec.done, c->stream));
     t.dec_mode = mode;
     return HZ_OK;
 }
@@ -565,6 +586,7 @@ extern "C" int hz_index_build(hz_ctx* c, const uint8_t* d_payload, uint64_t payl
     if (nsym <= (UINT64_MAX - start_bit) / 64 && payload_bytes > reach) payload_bytes = reach;
     int rc = ensure_scratch(c, index_scratch_words(payload_bytes, start_bit));
     if (rc) return rc;
+    if ((rc = staging_flush(c, c->stage_walk))) return rc;  // the walk tables
     HZ_TRY(stage_event(c, HZ_STAGE_INDEX, 0));
     HZ_TRY(launch_index_build(c->t, d_payload, payload_bytes, start_bit, nsym,
                               reinterpret_cast<unsigned long long*>(d_index), c->d_desc, c->d_err, c->h_err + 2,
@@ -603,6 +625,10 @@ extern "C" int hz_decode_indexless(hz_ctx* c, const uint8_t* d_payload, uint64_t
         return arm_err_check(c);
     }
     if (!seg_decode_supported(c->t)) return HZ_EINVAL;  // (every codebook but FIXED16 has chain tables)
+    {
+        const int rf = staging_flush(c, c->stage_walk);  // the chain tables
+        if (rf) return rf;
+    }
     if (payload_bytes < 16) {  // too short for the walk: one thread, serially (stream-ordered too)
         HZ_TRY(stage_event(c, HZ_STAGE_EXTRACT, 0));
         HZ_TRY(chain_decode_tiny(c->t, d_payload, payload_bytes, start_bit, nsym, d_out,
@@ -675,6 +701,7 @@ extern "C" int hz_indexless_scan(hz_ctx* c, const uint8_t* d_payload, uint64_t p
                                                                   (double)std::max<uint64_t>(pbits, 1))) : 0;
     int rc = ensure_scratch(c, chain_scratch_words(part_begin, part_end, hint, c->t, c->ncu));
     if (rc) return rc;
+    if ((rc = staging_flush(c, c->stage_walk))) return rc;  // the chain tables
     HZ_TRY(chain_scan(c->chain, c->t, d_payload, payload_bytes, payload_bit_base, start_bit, hint, part_begin, part_end,
                       entry_bit, c->d_desc, c->d_err, c->ncu, c->stream));
     if ((rc = part_summary(c, d_summary))) return rc;

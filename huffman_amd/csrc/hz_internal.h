@@ -273,6 +273,14 @@ const unsigned long long* chain_info(const ChainState* st);
 void chain_invalidate(ChainState* st);  // the scratch or tables it points into changed
 hipError_t chain_summary(const ChainState* st, unsigned long long* d_dst, hipStream_t s);  // 3 x u64, stream bits
 hipError_t put3(unsigned long long* d_dst, uint64_t a, uint64_t b, uint64_t c, hipStream_t s);  // stream-ordered
+// Table uploads: segments of a pinned host staging buffer copied to their device tables by one kernel
+// (it reads the host memory over PCIe: one launch per upload instead of one copy per table).
+struct StageSeg {
+    void* dst;
+    uint64_t off, bytes;  // off: 16-byte aligned in the staging buffer; bytes: a multiple of 4
+};
+constexpr int kStageMaxSegs = 16;
+hipError_t stage_scatter(const uint8_t* h_src, const StageSeg* segs, int nseg, hipStream_t s);
 hipError_t launch_codebook(const unsigned long long* d_hist, hz_codebook* d_cb, unsigned long long* d_ws,
                            uint32_t* d_err, hipStream_t s);  // hz_codebook_gpu.hip
 uint64_t codebook_ws_words();

@@ -4329,6 +4329,41 @@ __global__ void k_put3(unsigned long long* dst, uint64_t a, uint64_t b, uint64_t
         dst[2] = c;
     }
 }
+struct StageArgs {
+    const uint8_t* src;
+    StageSeg seg[kStageMaxSegs];
+};
+// Segment blockIdx.y of the staging buffer to its table: 16-byte vectors, then the 4-byte tail.
+__global__ __launch_bounds__(256) void k_stage_scatter(StageArgs a) {
+    const StageSeg g = a.seg[blockIdx.y];
+    const uint4* src = reinterpret_cast<const uint4*>(a.src + g.off);
+    uint4* dst = reinterpret_cast<uint4*>(g.dst);
+    const uint64_t nv = g.bytes / 16;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < (g.bytes % 16) / 4) {
+        const uint64_t w = nv * 4 + threadIdx.x;
+        reinterpret_cast<uint32_t*>(g.dst)[w] = reinterpret_cast<const uint32_t*>(a.src + g.off)[w];
+    }
+}
+
+hipError_t stage_scatter(const uint8_t* h_src, const StageSeg* segs, int nseg, hipStream_t s) {
+    for (int i0 = 0; i0 < nseg; i0 += kStageMaxSegs) {
+        StageArgs a;
+        a.src = h_src;
+        const int n = nseg - i0 < kStageMaxSegs ? nseg - i0 : kStageMaxSegs;
+        uint64_t most = 0;
+        for (int i = 0; i < n; ++i) {
+            a.seg[i] = segs[i0 + i];
+            most = a.seg[i].bytes > most ? a.seg[i].bytes : most;
+        }
+        uint64_t blocks = (most / 16 + 255) / 256;
+        blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
+        hipLaunchKernelGGL(k_stage_scatter, dim3((uint32_t)blocks, (uint32_t)n), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
 hipError_t put3(unsigned long long* d_dst, uint64_t a, uint64_t b, uint64_t c, hipStream_t s) {
     hipLaunchKernelGGL(k_put3, dim3(1), dim3(64), 0, s, d_dst, a, b, c);
     return hipGetLastError();
