@@ -3499,7 +3499,8 @@ struct ChainBlk {
     unsigned long long rec;     // index of the block's first record in ChainArgs::rec
     long long out;              // output index of the block's first record's first symbol
     uint32_t lo, hi;            // valid records [lo, hi) of the block
-    uint32_t last, pad;         // symbols of record hi - 1 (8 unless it is the chain's last codewords)
+    uint32_t last;              // symbols of record hi - 1 (8 unless it is the chain's last codewords)
+    uint32_t lhl;               // lo | hi << 9 | last << 18: one SGPR per block in the block decoder
 };
 static_assert(sizeof(ChainBlk) == 48, "ChainBlk");
 
@@ -3896,7 +3897,7 @@ __global__ __launch_bounds__(256) void k_chain_meta(ChainArgs y) {
                 d.hi = hi < kChainRecs ? hi : kChainRecs;
                 // the chain's last record (not cut by the capacity) holds n - 8 (nrec - 1) codewords
                 d.last = nrec <= y.cap && kChainRecs * j + d.hi == nrec ? (uint32_t)(n - 8ull * (nrec - 1)) : 8u;
-                d.pad = 0;
+                d.lhl = d.lo | d.hi << 9 | d.last << 18;
                 bk[j - j0] = d;
                 maxb = d.b1 - d.b0 > maxb ? d.b1 - d.b0 : maxb;
             }
@@ -3911,39 +3912,59 @@ __global__ __launch_bounds__(256) void k_chain_meta(ChainArgs y) {
     if ((threadIdx.x & 63) == 0 && maxb) atomicMax(y.info + 1, (unsigned long long)maxb);
 }
 
-// Block metadata of the chain decoder: the descriptor's stream bits (for the staging), the lane's
-// four record low bits (chain slots 64 k + lane; invalid records read as the block start, decoded and
-// never stored), output index, valid range.
+// Block metadata of the chain decoder, as loaded: the descriptor (scalar loads that nothing waits for
+// until the next block iteration, so they never turn an LDS wait of the current one into lgkmcnt(0))
+// and the lane's four record low bits (chain slots 64 k + lane), loaded a whole block iteration
+// before they are used (chain_rec_load) and unconditionally: a select of the loaded values in the same
+// iteration made the compiler branch around each load, splitting the block loop (k_chain_decode 10.76
+// against k_decode's 9.89 ms). Records past hi read stale rows of the chain's capacity and are
+// replaced by the block start in chain_meta_sub.
 struct ChainMeta {
-    uint64_t b0, b1, sub;
+    uint64_t b0, b1, rec;
     long long out;
-    uint32_t lo, hi, last;
+    uint32_t lhl;  // ChainBlk::lhl
+    bool valid;    // a block of the decode (else: any block, decoded, never stored)
+    uint64_t sub;  // the four record words as loaded
 };
 
-HZ_DEV void chain_meta_load(const ChainArgs& y, uint64_t b, uint64_t nb, int lane, ChainMeta& m) {
+HZ_DEV void chain_meta_load(const ChainArgs& y, uint64_t b, uint64_t nb, ChainMeta& m) {
     const uint64_t bb = b < nb ? b : (nb ? nb - 1 : 0);  // past the end: any block, never stored
-    // the descriptor through the scalar cache (6 u64: b0, b1, rec, out, lo | hi << 32, last)
+    // the descriptor through the scalar cache (b0, b1, rec, out, lhl)
     typedef const __attribute__((address_space(4))) unsigned long long* cu64p;
     const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bb >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bb);
     const cu64p d = (cu64p)y.blk + 6 * bu;
     m.b0 = d[0];
     m.b1 = d[1];
-    const uint64_t rec = d[2];
+    m.rec = d[2];
     m.out = (long long)d[3];
-    const uint64_t lohi = d[4];
-    m.lo = (uint32_t)lohi;
-    m.hi = b < nb ? (uint32_t)(lohi >> 32) : 0u;
-    m.last = (uint32_t)d[5];
-    const uint16_t* s16 = y.rec + rec + (uint32_t)lane;
+    m.lhl = (uint32_t)(d[5] >> 32);
+    m.valid = b < nb;
+}
+
+// The lane's four records of a block whose descriptor has landed (one load per slot, always issued;
+// y.rec holds a whole capacity of rows per chain, so rows past the block's valid ones exist).
+HZ_DEV void chain_rec_load(const ChainArgs& y, int lane, ChainMeta& m) {
+    const uint16_t* s16 = y.rec + m.rec + (uint32_t)lane;
+    uint64_t sub = 0;
+#pragma unroll
+    for (int c = 0; c < kChainsPerLane; ++c) sub |= (uint64_t)s16[64 * c] << (16 * c);
+    m.sub = sub;
+}
+
+HZ_DEV uint32_t chain_meta_hi(const ChainMeta& m) { return m.valid ? (m.lhl >> 9) & 0x1ffu : 0u; }
+
+// The lane's chain starts (low 16 bits): its records below hi, else the block start.
+HZ_DEV uint64_t chain_meta_sub(const ChainMeta& m, int lane) {
+    const uint32_t hi = chain_meta_hi(m);
     uint64_t sub = 0;
 #pragma unroll
     for (int c = 0; c < kChainsPerLane; ++c) {
         const uint32_t t = 64u * c + (uint32_t)lane;
-        const uint16_t v = s16[t < m.hi ? 64 * c : 0];  // one load per slot, always issued
-        sub |= (uint64_t)(t < m.hi ? v : (uint16_t)m.b0) << (16 * c);
+        const uint64_t v = t < hi ? (m.sub >> (16 * c)) & 0xffffu : (uint64_t)(uint16_t)m.b0;
+        sub |= v << (16 * c);
     }
-    m.sub = sub;
+    return sub;
 }
 
 // A chain block's symbols: record t = 64 c + lane of the block, 8 symbols at output index out + 8 t
@@ -3951,7 +3972,8 @@ HZ_DEV void chain_meta_load(const ChainArgs& y, uint64_t b, uint64_t nb, int lan
 // stream end's symbol by symbol.
 HZ_DEV void chain_store(const DecArgs& a, const ChainMeta& m, int lane, const uint32_t* pk) {
     uint16_t* out16 = reinterpret_cast<uint16_t*>(a.out);
-    const bool full = m.lo == 0 && m.hi == kChainRecs && m.last == 8 && m.out >= 0 &&
+    const uint32_t lo = m.lhl & 0x1ffu, hi = chain_meta_hi(m), last = m.lhl >> 18;
+    const bool full = lo == 0 && hi == kChainRecs && last == 8 && m.out >= 0 &&
                       (uint64_t)m.out + (uint64_t)kBlockSyms <= a.nsym;
     if (full) {
         const long long ob = m.out;
@@ -3966,10 +3988,10 @@ HZ_DEV void chain_store(const DecArgs& a, const ChainMeta& m, int lane, const ui
 #pragma unroll
     for (int c = 0; c < kChainsPerLane; ++c) {
         const uint32_t t = 64u * c + (uint32_t)lane;
-        if (t < m.lo || t >= m.hi) continue;
+        if (t < lo || t >= hi) continue;
         const long long o = m.out + 8ll * t;
         if (o < 0 || (uint64_t)o >= a.nsym) continue;
-        uint32_t cn = t + 1 == m.hi ? m.last : 8u;
+        uint32_t cn = t + 1 == hi ? last : 8u;
         cn = a.nsym - (uint64_t)o < cn ? (uint32_t)(a.nsym - (uint64_t)o) : cn;
         if (cn == 8) {
             *reinterpret_cast<u32x4a2*>(out16 + o) = u32x4a2{pk[4 * c], pk[4 * c + 1], pk[4 * c + 2], pk[4 * c + 3]};
@@ -3990,20 +4012,25 @@ HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, co
     uint4 sc[2][kStageUnroll], sn[2][kStageUnroll];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        chain_meta_load(y, b + j, nb, lane, mc[j]);
-        chain_meta_load(y, b + stride + j, nb, lane, mn[j]);
+        chain_meta_load(y, b + j, nb, mc[j]);
+        chain_meta_load(y, b + stride + j, nb, mn[j]);
     }
-    auto as_pipe = [](const ChainMeta& m) { PipeMeta p; p.b0 = m.b0; p.b1 = m.b1; p.sub = m.sub; return p; };
+#pragma unroll
+    for (int j = 0; j < 2; ++j) chain_rec_load(y, lane, mc[j]);
+    auto as_pipe = [](const ChainMeta& m) { PipeMeta p; p.b0 = m.b0; p.b1 = m.b1; p.sub = 0; return p; };
 #pragma unroll
     for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, as_pipe(mc[j]), lane, sc[j]);
     for (; b < nb; b += stride) {
+        // the next blocks' records, a block iteration ahead (their descriptors landed last iteration)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) chain_rec_load(y, lane, mn[j]);
         uint32_t p1[C];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint64_t w0;
             dec_stage_commit<true>(a, as_pipe(mc[j]), slot >> 2, stg + j * slot, lane, sc[j], w0);
             uint32_t off[kChainsPerLane];
-            dec_chain_offsets(mc[j].sub, mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
+            dec_chain_offsets(chain_meta_sub(mc[j], lane), mc[j].b0, mc[j].b1 - mc[j].b0, lane, off);
             const uint32_t top = (uint32_t)(stg - lds) + (uint32_t)(j + 1) * slot - 1u;
             const uint32_t base = top * 32u - (uint32_t)(mc[j].b0 + a.bit_adj - (w0 << 5));
 #pragma unroll
@@ -4041,7 +4068,7 @@ HZ_DEV void dec_wave_chain(const DecArgs& a, const ChainArgs& y, uint64_t nb, co
 #pragma unroll
                 for (int j = 0; j < 2; ++j) dec_stage_prefetch(a, as_pipe(mn[j]), lane, sn[j]);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) chain_meta_load(y, b + 2 * stride + j, nb, lane, mn2[j]);
+                for (int j = 0; j < 2; ++j) chain_meta_load(y, b + 2 * stride + j, nb, mn2[j]);
             }
 #pragma unroll
             for (int c = 0; c < 4; ++c) finish(c, q);
