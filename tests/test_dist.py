@@ -91,6 +91,33 @@ def test_shard_ranges_cover_and_align():
         assert all(b % 2 == 0 for b, _ in rs)
 
 
+def test_part_range_and_window_properties():
+    """Equal bit parts of one payload over `world` ranks (dist.part_range), 2 000 seeded random
+    geometries: the parts tile [0, P) in rank order on 128-bit boundaries, every non-empty part is at
+    least 128 bits unless the whole payload is shorter, empty parts come last; each part's window
+    (dist.part_window) covers its lead-in (1 024 bits, or the stream from its start) and max_len bits
+    past its end, in whole words."""
+    import random
+    from huffman_amd import dist as hd
+    rnd = random.Random(6)
+    for _ in range(2000):
+        P = rnd.choice([0, 1, 127, 128, 129, 1000, rnd.randrange(1 << 40)])
+        world = rnd.randrange(1, 17)
+        parts = [hd.part_range(P, world, r) for r in range(world)]
+        assert parts[0][0] == 0 and parts[-1][1] == P
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        nonempty = [(b, e) for b, e in parts if e > b]
+        assert all(parts[i][1] > parts[i][0] for i in range(len(nonempty)))  # empty parts last
+        assert all(b % 128 == 0 for b, _ in nonempty)
+        if P >= 128:
+            assert all(e - b >= 128 for b, e in nonempty)
+        start, max_len = rnd.randrange(0, 4096), rnd.randrange(1, 57)
+        for b, e in nonempty:
+            lo, hi = hd.part_window(start, b, e, max_len)
+            assert 32 * lo <= start + b - min(1024, b) and start + e + max_len <= 32 * hi
+            assert 32 * lo > start + b - min(1024, b) - 32 and 32 * hi < start + e + max_len + 32
+
+
 def _subgroup_worker(rank, world, port, n_total, result_dir):
     """Two 2-rank subgroups of a 4-rank job, {0, 2} and {1, 3}: each encodes the
     whole (odd) stream sharded over its members. The members' group ranks differ
