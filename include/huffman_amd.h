@@ -129,9 +129,15 @@ int hz_header_parse(const uint8_t *file, uint64_t len, hz_codebook *cb, hz_heade
 int hz_header_parse_device(hz_ctx *ctx, const uint8_t *d_file, uint64_t len, hz_codebook *d_cb, uint64_t *d_info);
 
 /* Upload a codebook's device tables to the context: encode tables (needed by
- * hz_pack), decode tables (needed by hz_decode / hz_index_build), or both.
- * Asynchronous on the context stream; the decode half can be built on the
- * host while a hz_pack launched before it runs. */
+ * hz_pack), decode tables (needed by hz_decode / hz_index_build /
+ * hz_decode_indexless / hz_indexless_*), or both. Asynchronous on the context
+ * stream: the tables are built on the host (the decode half while a hz_pack
+ * launched before it runs), staged in pinned memory and copied by one device
+ * kernel per table set. The index-less decoder's tables (walk length and escape
+ * tables, a DENSE codebook's chain LUT) are copied by the first call that reads
+ * them (hz_decode_indexless, hz_indexless_scan, hz_index_build), in its stream
+ * order, so a decode through a block index never copies them; under stream
+ * capture that copy is part of the captured work. */
 int hz_codebook_upload(hz_ctx *ctx, const hz_codebook *cb);
 int hz_codebook_upload_encode(hz_ctx *ctx, const hz_codebook *cb);
 int hz_codebook_upload_decode(hz_ctx *ctx, const hz_codebook *cb);
