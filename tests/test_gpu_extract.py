@@ -471,3 +471,46 @@ def test_random_streams_range_plan(codec, seed, U, kind):
     assert torch.equal(out[:2 * nsym], x[:2 * nsym])
     ok, end_ok = _check(codec, x, 3)
     assert ok and end_ok
+
+
+def test_indexless_random_streams_captured_first(codec):
+    """Six seeded random streams whose first index-less decode after a table upload is captured in a
+    HIP graph: the capture holds the copy of the index-less tables (staged by the upload, copied by
+    their first reader), the replay decodes bit-exact, and an eager call afterwards copies them again
+    and decodes bit-exact too. (An eager decode first sizes the context's scratch: growing it
+    synchronises, which a capture does not allow -- include/huffman_amd.h.)"""
+    import torch
+    rng = np.random.default_rng(31)
+    done = 0
+    while done < 6:
+        data, what = _random_stream(rng)
+        if data.size < 64:
+            continue
+        nsym = data.size // 2
+        x = torch.from_numpy(data).cuda()
+        plan, payload, _ = codec.encode(x)
+        codec.sync()
+        out = torch.zeros(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+        end = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+
+        def call():
+            codec.dev.decode_indexless(payload.data_ptr(), payload.numel(), plan.start_bit, nsym, out.data_ptr(),
+                                       end.data_ptr())
+
+        call()  # sizes the scratch
+        codec.upload_decode(plan)  # the index-less tables staged again, not yet copied
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=codec.stream):
+            call()
+        out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what + " (replay)"
+        out.zero_()
+        torch.cuda.synchronize()
+        call()
+        codec.sync()
+        assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what + " (eager after the capture)"
+        done += 1
