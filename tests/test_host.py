@@ -69,6 +69,44 @@ def test_codebook_matches_oracle(built_lib, U, hi):
     assert cb.max_len == ln.max() and cb.min_len == ln[ln > 0].min()
 
 
+def test_codebook_matches_oracle_random_histograms(built_lib):
+    """300 seeded random histograms (1..65 536 symbols; flat, power-law, geometric, tie-heavy and
+    Fibonacci-like counts up to 2^40): the host builder's order, lengths and codes equal the oracle's,
+    or both refuse codes past HZ_MAXLEN."""
+    import huffman_amd
+    rng = np.random.default_rng(17)
+    for case in range(300):
+        U = int(rng.choice([1, 2, 3, 7, 64, 1000, 4096, 65536]))
+        kind = case % 5
+        r = np.arange(1, U + 1, dtype=np.float64)
+        if kind == 0:
+            c = rng.integers(1, 1 << int(rng.integers(1, 40)), U)
+        elif kind == 1:
+            c = np.maximum(1, (1e9 * r ** -rng.uniform(0.5, 2.5)).astype(np.int64))
+        elif kind == 2:
+            c = np.maximum(1, (1e12 * rng.uniform(0.3, 0.95) ** r).astype(np.int64))
+        elif kind == 3:
+            c = rng.integers(1, 4, U)  # ties everywhere
+        else:
+            f = [1, 1]
+            while len(f) < U:
+                f.append(min(f[-1] + f[-2], 1 << 40))
+            c = np.array(f[:U], dtype=np.int64)
+        h = np.zeros(65536, dtype=np.uint64)
+        h[rng.choice(65536, U, replace=False)] = c.astype(np.uint64)
+        try:
+            o_order, o_ln, o_code = oracle_lib.codebook(h)
+        except RuntimeError:
+            with pytest.raises(Exception):
+                huffman_amd.build_codebook(h)
+            continue
+        cb = huffman_amd.build_codebook(h)
+        order, ln, code = huffman_amd.codebook_arrays(cb)
+        assert np.array_equal(order, o_order), (case, U, kind)
+        assert np.array_equal(ln, o_ln), (case, U, kind)
+        assert np.array_equal(code, o_code), (case, U, kind)
+
+
 @pytest.mark.parametrize("name", ["romeo.txt", "synth_zipf_65537.bin", "synth_unif_65536.bin", "synth_zipf_4099.bin"])
 def test_header_matches_golden(built_lib, name):
     import huffman_amd
