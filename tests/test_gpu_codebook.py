@@ -279,3 +279,30 @@ def test_device_header_parse_mutations(env, name):
         if ora is not None:
             _assert_parse_equal(dev, ora)
     assert rejected >= 4
+
+
+def test_device_codebook_random_histograms(env):
+    """80 seeded random histograms (1..65 536 symbols; flat, power-law, geometric and tie-heavy counts)
+    built by the device GenerateCL equal the host builder's codebook (order, lengths, codes)."""
+    torch, hz, codec = env
+    rng = np.random.default_rng(23)
+    for case in range(80):
+        U = int(rng.choice([1, 2, 3, 7, 64, 1000, 4096, 65536]))
+        kind = case % 4
+        r = np.arange(1, U + 1, dtype=np.float64)
+        if kind == 0:
+            c = rng.integers(1, 1 << int(rng.integers(1, 36)), U)
+        elif kind == 1:
+            c = np.maximum(1, (1e9 * r ** -rng.uniform(0.5, 2.5)).astype(np.int64))
+        elif kind == 2:
+            c = np.maximum(1, (1e12 * rng.uniform(0.3, 0.95) ** r).astype(np.int64))
+        else:
+            c = rng.integers(1, 4, U)
+        h = np.zeros(65536, dtype=np.uint64)
+        h[rng.choice(65536, U, replace=False)] = c.astype(np.uint64)
+        try:
+            host = hz.build_codebook(h)
+        except Exception:  # codes past HZ_MAXLEN: covered by test_device_codebook_rejects_huge_counts
+            continue
+        dev, _ = _device_codebook(env, torch.from_numpy(h.view(np.int64)).cuda())
+        assert _same(dev, host), (case, U, kind)
