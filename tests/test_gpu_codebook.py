@@ -306,3 +306,26 @@ def test_device_codebook_random_histograms(env):
             continue
         dev, _ = _device_codebook(env, torch.from_numpy(h.view(np.int64)).cuda())
         assert _same(dev, host), (case, U, kind)
+
+
+def test_device_header_random_codebooks(env):
+    """40 seeded random histograms: the device header writer equals the host writer (bytes, pending
+    bits), and the device parser reads the written header back equal to the oracle's parse."""
+    torch, hz, codec = env
+    rng = np.random.default_rng(29)
+    for case in range(40):
+        U = int(rng.choice([1, 2, 3, 7, 64, 1000, 4096, 65536]))
+        h = np.zeros(65536, dtype=np.uint64)
+        h[rng.choice(65536, U, replace=False)] = rng.integers(1, 1 << int(rng.integers(1, 30)), U).astype(np.uint64)
+        odd = case % 2
+        n = 2 * int(h.sum()) + odd
+        last = 0xa5 if odd else 0
+        _, d_cb = _device_codebook(env, torch.from_numpy(h.view(np.int64)).cuda())
+        got = _device_header(env, d_cb, n, last)
+        want = hz.write_header(hz.build_codebook(h), n, last)
+        assert got[0] == want[0] and got[1] == want[1], (case, U)
+        if got[1]:
+            assert got[2] >> (8 - got[1]) == want[2] >> (8 - want[1]), (case, U)
+        dev, ora = _parse_both(env, _header_blob(hz, h, odd))
+        assert dev is not None and ora is not None, (case, U)
+        _assert_parse_equal(dev, ora)
