@@ -440,7 +440,8 @@ static int hz_codebook_upload_decode_impl(hz_ctx* c, const hz_codebook* cb) {
     t.dec_l2_entries = l2.size();
     if ((rc = stage_copy(c, c->stage_dec, &t.d_dec_l2, &c->cap_dec_l2, l2))) return rc;
     if ((rc = staging_flush(c, c->stage_dec))) return rc;
-    // the index-less tables, staged now and copied by the first call that needs them (flush_walk)
+    // the index-less tables, staged now and copied by the first call that needs them (staging_flush
+    // from hz_decode_indexless, hz_indexless_scan or hz_index_build)
     if ((rc = staging_begin(c->stage_walk))) return rc;
     // the index walker's length tables (FIXED16 streams have an arithmetic index)
     t.walk_lds_bytes = 0;
