@@ -514,3 +514,60 @@ def test_indexless_random_streams_captured_first(codec):
         codec.sync()
         assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what + " (eager after the capture)"
         done += 1
+
+
+def test_indexless_parts_from_slices(codec):
+    """The split API in one context, part after part: eight seeded random streams cut at 1-4 random
+    payload bits; each part is scanned from a 16-byte aligned slice holding only its lead-in, its bits
+    and max_len bits after (payload_bit_base), from its true entry (the previous part's exit) or from
+    its walked entry and then refixed to the true one, and decoded at the sum of the codewords before
+    it. The parts together restore the stream bit-exactly."""
+    import torch
+    from huffman_amd.dist import UNKNOWN_ENTRY
+    rng = np.random.default_rng(41)
+    summ = torch.zeros(4, dtype=torch.int64, device="cuda")
+    done = 0
+    while done < 8:
+        data, what = _random_stream(rng)
+        if data.size < 4096:
+            continue
+        nsym = data.size // 2
+        x = torch.from_numpy(data).cuda()
+        plan, payload, _ = codec.encode(x)
+        codec.sync()
+        start, P, max_len = int(plan.start_bit), int(plan.payload_bits), int(plan.cb.max_len)
+        k = int(rng.integers(2, 6))
+        cuts = sorted(set(int(v) for v in rng.integers(1, P, k - 1)))
+        bounds = [0] + cuts + [P]
+        out = torch.zeros(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+
+        def read():
+            codec.sync()
+            return [int(v) & ((1 << 64) - 1) for v in summ[:3].cpu().tolist()]
+
+        entry, first = start, 0
+        for pb, pe in zip(bounds, bounds[1:]):
+            lo_bit = start + pb - min(1024, pb)
+            hi_bit = start + pe + max_len
+            b0 = lo_bit // 8 // 16 * 16
+            b1 = min(payload.numel(), ((hi_bit + 7) // 8 + 16 + 15) // 16 * 16)
+            known = bool(rng.random() < 0.5) or pb == 0
+            codec.dev.indexless_scan(payload.data_ptr() + b0, b1 - b0, start, pb, pe,
+                                     entry if known else UNKNOWN_ENTRY, summ.data_ptr(), nsym=nsym,
+                                     payload_bit_base=8 * b0)
+            cnt, xit, ent = read()
+            if ent != entry:
+                codec.dev.indexless_refix(entry, summ.data_ptr())
+                cnt, xit, ent = read()
+            assert ent == entry, what
+            take = min(cnt, nsym - first)
+            tmp = torch.zeros(2 * take + 16, dtype=torch.uint8, device="cuda")
+            codec.dev.indexless_decode(take, tmp.data_ptr())
+            codec.sync()
+            out[2 * first:2 * (first + take)] = tmp[:2 * take]
+            first += cnt
+            entry = xit
+        codec.sync()
+        assert first == nsym, what
+        assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what
+        done += 1
