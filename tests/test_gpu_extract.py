@@ -571,3 +571,41 @@ def test_indexless_parts_from_slices(codec):
         assert first == nsym, what
         assert torch.equal(out[:2 * nsym], x[:2 * nsym]), what
         done += 1
+
+
+def test_indexless_parts_from_slices_fixed16(codec):
+    """The split API on a FIXED16 stream (every code 16 bits, 64 MiB of uniform bytes): parts at
+    random bits, each from its own slice, entries arithmetic (start + 16 i), walked or given."""
+    import torch
+    from huffman_amd.dist import UNKNOWN_ENTRY
+    n = (64 << 20) + 2
+    x = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.dev.generate(x.data_ptr(), n, offset=0, kind=0, alpha=1.1, seed=3)
+    plan, payload, _ = codec.encode(x)
+    codec.sync()
+    assert int(plan.cb.min_len) == 16 and int(plan.cb.max_len) == 16
+    nsym = n // 2
+    start, P = int(plan.start_bit), int(plan.payload_bits)
+    rng = np.random.default_rng(43)
+    bounds = [0] + sorted(set(int(v) for v in rng.integers(1, P, 4))) + [P]
+    summ = torch.zeros(4, dtype=torch.int64, device="cuda")
+    out = torch.zeros(2 * nsym + 16, dtype=torch.uint8, device="cuda")
+    entry, first = start, 0
+    for i, (pb, pe) in enumerate(zip(bounds, bounds[1:])):
+        b0 = (start + pb - min(1024, pb)) // 8 // 16 * 16
+        b1 = min(payload.numel(), ((start + pe + 16 + 7) // 8 + 16 + 15) // 16 * 16)
+        codec.dev.indexless_scan(payload.data_ptr() + b0, b1 - b0, start, pb, pe,
+                                 entry if i % 2 == 0 else UNKNOWN_ENTRY, summ.data_ptr(), nsym=nsym,
+                                 payload_bit_base=8 * b0)
+        codec.sync()
+        cnt, xit, ent = [int(v) & ((1 << 64) - 1) for v in summ[:3].cpu().tolist()]
+        assert ent == entry
+        take = min(cnt, nsym - first)
+        tmp = torch.zeros(2 * take + 16, dtype=torch.uint8, device="cuda")
+        codec.dev.indexless_decode(take, tmp.data_ptr())
+        codec.sync()
+        out[2 * first:2 * (first + take)] = tmp[:2 * take]
+        first += cnt
+        entry = xit
+    assert first == nsym
+    assert torch.equal(out[:2 * nsym], x[:2 * nsym])
